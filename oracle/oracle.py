@@ -1,0 +1,169 @@
+"""ctypes wrapper of the CPU parity oracle (oracle/ocp_qp_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product package.  The product
+path (libsrbd_qp.so) has no CPU fallback and does not link this library.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import time
+from pathlib import Path
+from typing import Dict, Optional
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "build" / "liboracle.so"
+
+_dp = C.POINTER(C.c_double)
+
+
+class _QP(C.Structure):
+    _fields_ = [("N", C.c_int), ("nx", C.c_int), ("nu", C.c_int), ("ng", C.c_int)] + [
+        (n, _dp) for n in (
+            "A", "B", "b", "Q", "S", "R", "q", "r",
+            "lbu", "ubu", "lbu_mask", "ubu_mask",
+            "lbx", "ubx", "lbx_mask", "ubx_mask",
+            "C", "D", "lg", "ug", "lg_mask", "ug_mask")
+    ]
+
+
+class _Settings(C.Structure):
+    _fields_ = [("iter_max", C.c_int), ("alpha_min", C.c_double), ("mu0", C.c_double),
+                ("tol_stat", C.c_double), ("tol_eq", C.c_double), ("tol_ineq", C.c_double),
+                ("tol_comp", C.c_double), ("reg_prim", C.c_double), ("warm_start", C.c_int),
+                ("pred_corr", C.c_int), ("split_step", C.c_int)]
+
+
+class _Result(C.Structure):
+    _fields_ = [("status", C.c_int), ("iter", C.c_int), ("res", C.c_double * 4), ("obj", C.c_double)]
+
+
+_lib = None
+
+
+def build() -> Path:
+    """Compile the oracle with its Makefile (gcc only)."""
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        _lib = C.CDLL(str(LIB_PATH))
+        _lib.oracle_solve.restype = C.c_int
+        _lib.oracle_solve.argtypes = [C.POINTER(_QP), C.POINTER(_Settings), _dp, _dp, _dp, _dp,
+                                      _dp, _dp, _dp, _dp, C.POINTER(_Result)]
+        _lib.oracle_solve_batch.restype = C.c_int
+        _lib.oracle_solve_batch.argtypes = [C.c_int, C.POINTER(_QP), C.POINTER(_Settings), _dp,
+                                            _dp, _dp, _dp, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                            C.c_int]
+    return _lib
+
+
+def _ptr(a: Optional[np.ndarray]):
+    if a is None:
+        return _dp()
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_dp)
+
+
+DEFAULT_SETTINGS = dict(iter_max=15, alpha_min=1e-8, mu0=1e2, tol_stat=1e-8, tol_eq=1e-8,
+                        tol_ineq=1e-8, tol_comp=1e-8, reg_prim=1e-12, warm_start=0, pred_corr=1,
+                        split_step=0)
+
+
+def _settings(s: Optional[Dict]) -> _Settings:
+    d = dict(DEFAULT_SETTINGS)
+    if s:
+        d.update({k: v for k, v in s.items() if k in d})
+    return _Settings(**d)
+
+
+def _make_qp(p: Dict[str, Optional[np.ndarray]], N, nx, nu, ng, keep) -> _QP:
+    qp = _QP()
+    qp.N, qp.nx, qp.nu, qp.ng = N, nx, nu, ng
+    for name, _ in _QP._fields_[4:]:
+        arr = p.get(name)
+        if arr is not None:
+            arr = np.ascontiguousarray(arr, dtype=np.float64)
+            keep.append(arr)
+        setattr(qp, name, _ptr(arr))
+    return qp
+
+
+def solve(batch, settings: Optional[Dict] = None, x0: Optional[np.ndarray] = None,
+          x_init=None, u_init=None, riccati: bool = True):
+    """Solve every QP of an OcpQpBatch one by one; returns a dict of arrays."""
+    p = batch.packed()
+    N, nx, nu, ng, nb = batch.N, batch.nx, batch.nu, batch.ng, batch.batch
+    st = _settings(settings)
+    out = {
+        "x": np.zeros((nb, N + 1, nx)), "u": np.zeros((nb, N, nu)), "pi": np.zeros((nb, N + 1, nx)),
+        "P": np.zeros((nb, N + 1, nx, nx)), "p": np.zeros((nb, N + 1, nx)),
+        "K": np.zeros((nb, N, nu, nx)), "k": np.zeros((nb, N, nu)),
+        "status": np.zeros(nb, dtype=np.int32), "iter": np.zeros(nb, dtype=np.int32),
+        "res": np.zeros((nb, 4)), "obj": np.zeros(nb),
+    }
+    if x_init is not None:
+        out["x"][:] = x_init
+    if u_init is not None:
+        out["u"][:] = u_init
+    x0 = np.zeros((nb, nx)) if x0 is None else np.asarray(x0, dtype=np.float64).reshape(nb, nx)
+    L = lib()
+    for i in range(nb):
+        keep = []
+        pi_ = {k: (None if v is None else v[i]) for k, v in p.items()}
+        qp = _make_qp(pi_, N, nx, nu, ng, keep)
+        x = np.ascontiguousarray(out["x"][i])
+        u = np.ascontiguousarray(out["u"][i])
+        pi = np.zeros((N + 1, nx))
+        P = np.zeros((N + 1, nx, nx))
+        pv = np.zeros((N + 1, nx))
+        K = np.zeros((N, nx, nu))  # col-major nu x nx blocks
+        k = np.zeros((N, nu))
+        r = _Result()
+        x0i = np.ascontiguousarray(x0[i])
+        rc = L.oracle_solve(C.byref(qp), C.byref(st), _ptr(x0i), _ptr(x), _ptr(u), _ptr(pi),
+                            _ptr(P) if riccati else _dp(), _ptr(pv) if riccati else _dp(),
+                            _ptr(K) if riccati else _dp(), _ptr(k) if riccati else _dp(),
+                            C.byref(r))
+        if rc != 0:
+            raise ValueError(f"oracle_solve failed with code {rc}")
+        out["x"][i], out["u"][i], out["pi"][i] = x, u, pi
+        out["P"][i] = np.swapaxes(P, -1, -2)
+        out["p"][i] = pv
+        out["K"][i] = np.swapaxes(K, -1, -2)
+        out["k"][i] = k
+        out["status"][i], out["iter"][i] = r.status, r.iter
+        out["res"][i] = list(r.res)
+        out["obj"][i] = r.obj
+    return out
+
+
+def solve_batch_threaded(batch, settings: Optional[Dict] = None, x0=None, threads: int = 0):
+    """Threaded batch solve (x, u, pi only) -- the cpu_baseline 'port'.  Returns (out, seconds)."""
+    p = batch.packed()
+    N, nx, nu, ng, nb = batch.N, batch.nx, batch.nu, batch.ng, batch.batch
+    threads = threads or os.cpu_count() or 1
+    keep = []
+    qp = _make_qp(p, N, nx, nu, ng, keep)
+    st = _settings(settings)
+    x0 = np.zeros((nb, nx)) if x0 is None else np.ascontiguousarray(x0, dtype=np.float64).reshape(nb, nx)
+    x = np.zeros((nb, N + 1, nx))
+    u = np.zeros((nb, N, nu))
+    pi = np.zeros((nb, N + 1, nx))
+    status = np.zeros(nb, dtype=np.int32)
+    iters = np.zeros(nb, dtype=np.int32)
+    t0 = time.perf_counter()
+    lib().oracle_solve_batch(nb, C.byref(qp), C.byref(st), _ptr(x0), _ptr(x), _ptr(u), _ptr(pi),
+                             status.ctypes.data_as(C.POINTER(C.c_int)),
+                             iters.ctypes.data_as(C.POINTER(C.c_int)), int(threads))
+    dt = time.perf_counter() - t0
+    return {"x": x, "u": u, "pi": pi, "status": status, "iter": iters}, dt

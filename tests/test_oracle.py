@@ -1,0 +1,93 @@
+"""Pin the CPU oracle against the reference's own tests and golden vectors.
+
+* unconstrained: textbook Riccati of hpipm-cpp/test/ocp_qp_ipm_solver.cpp:22-110
+  (status Success, iter == 0, x/u/pi/P/-p/K/k at isApprox 1e-10), plus an
+  independent dense-KKT solve.
+* compareResults: OSQP golden trajectories sol0..14.txt
+  (test/ocp_qp_ipm_solver.cpp:170-315) -- box constraints, one-sided masks,
+  warm start, 15 closed-loop steps, isApprox 1e-9.
+* constrained: test/ocp_qp_ipm_solver.cpp:112-168 (status Success, x[0] == x0)
+  plus KKT optimality checks the reference test does not make.
+"""
+import numpy as np
+import pytest
+
+import helpers
+
+
+def test_unconstrained_textbook(OcpQpBatch, oracle):
+    for seed in range(4):
+        qp, x0 = helpers.random_unconstrained(1, 20, 5, 3, seed, OcpQpBatch)
+        out = oracle.solve(qp, dict(iter_max=15), x0=x0)
+        assert out["status"][0] == 0
+        assert out["iter"][0] == 0
+        x, u, lmd, P, s, K, k = helpers.textbook_riccati(qp, x0[0])
+        prec = 1e-10
+        assert helpers.is_approx(out["x"][0, 0], x0[0], 1e-15)
+        for i in range(qp.N + 1):
+            assert helpers.is_approx(x[i], out["x"][0, i], prec)
+            assert helpers.is_approx(lmd[i], out["pi"][0, i], prec)
+            assert helpers.is_approx(P[i], out["P"][0, i], prec)
+            assert helpers.is_approx(s[i], -out["p"][0, i], prec)
+        for i in range(qp.N):
+            assert helpers.is_approx(u[i], out["u"][0, i], prec)
+            assert helpers.is_approx(K[i], out["K"][0, i], prec)
+            assert helpers.is_approx(k[i], out["k"][0, i], prec)
+
+
+@pytest.mark.parametrize("dims", [(20, 5, 3), (10, 12, 12), (20, 12, 12), (7, 3, 5)])
+def test_unconstrained_dense_kkt(OcpQpBatch, oracle, dims):
+    N, nx, nu = dims
+    qp, x0 = helpers.random_unconstrained(2, N, nx, nu, 11 + nx, OcpQpBatch)
+    out = oracle.solve(qp, None, x0=x0)
+    for i in range(2):
+        x, u, pi = helpers.dense_kkt(qp, x0[i], i)
+        assert helpers.is_approx(x, out["x"][i], 1e-9)
+        assert helpers.is_approx(u, out["u"][i], 1e-9)
+        assert helpers.is_approx(pi[1:], out["pi"][i, 1:], 1e-9)
+        assert out["res"][i, 0] < 1e-9 and out["res"][i, 1] < 1e-9
+
+
+def test_compare_results_osqp_golden(OcpQpBatch, oracle):
+    """test/ocp_qp_ipm_solver.cpp:170-315 against sol{t}.txt."""
+    qp, d, goldens, A, B, b = helpers.quadcopter(OcpQpBatch)
+    st = dict(d["settings"])
+    N, nx, nu = qp.N, qp.nx, qp.nu
+    x = np.zeros(nx)
+    xw = np.zeros((1, N + 1, nx))
+    uw = np.full((1, N, nu), d["u0"])
+    for t in range(d["sim_steps"]):
+        out = oracle.solve(qp, st, x0=x[None], x_init=xw, u_init=uw)
+        assert out["status"][0] == 0, (t, out["status"][0], out["res"][0])
+        cat = np.concatenate([out["x"][0].ravel(), out["u"][0].ravel()])
+        assert helpers.is_approx(cat, goldens[t], d["rel_prec"]), (
+            t, np.linalg.norm(cat - goldens[t]) / np.linalg.norm(goldens[t]))
+        xw, uw = out["x"], out["u"]  # warm start from the previous solution
+        x = A @ x + B @ out["u"][0, 0] + b
+
+
+@pytest.mark.parametrize("ng", [0, 2])
+def test_constrained_kkt(OcpQpBatch, oracle, ng):
+    qp, x0 = helpers.random_constrained(3, 20, 5, 3, ng, 5 + ng, OcpQpBatch)
+    st = dict(iter_max=30)  # hpipm-cpp default tolerances (1e-8), settings.hpp:26-86
+    out = oracle.solve(qp, st, x0=x0)
+    for i in range(3):
+        assert out["status"][i] == 0, out["res"][i]
+        assert helpers.is_approx(out["x"][i, 0], x0[i], 1e-15)
+        assert np.all(out["res"][i] <= 1e-8)
+        # primal feasibility of the box constraints
+        u = out["u"][i]
+        assert np.all(u[:, :3] >= qp.lbu[i][:, :3] - 1e-9) and np.all(u[:, :3] <= qp.ubu[i][:, :3] + 1e-9)
+
+
+def test_constrained_matches_unconstrained_when_inactive(OcpQpBatch, oracle):
+    """Far-away bounds: the IPM must land on the unconstrained Riccati solution."""
+    qp, x0 = helpers.random_unconstrained(2, 15, 6, 4, 3, OcpQpBatch)
+    ref = oracle.solve(qp, None, x0=x0)
+    qp.lbu = np.full((2, 15, 4), -1e4); qp.ubu = np.full((2, 15, 4), 1e4)
+    out = oracle.solve(qp, dict(iter_max=60, tol_stat=1e-12, tol_eq=1e-12, tol_ineq=1e-12,
+                                tol_comp=1e-9), x0=x0)
+    assert np.all(out["status"] == 0)
+    for i in range(2):
+        assert helpers.is_approx(out["x"][i], ref["x"][i], 1e-8)
+        assert helpers.is_approx(out["u"][i], ref["u"][i], 1e-8)
