@@ -1,0 +1,299 @@
+#!/usr/bin/env python3
+"""Benchmark: batched SRBD OCP-QP solves/sec on MI355X (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--batch B]
+
+A "step" is one solve of the whole per-rank batch (one C-ABI call, inputs
+already resident in HBM).  Every rank generates its own shard of synthetic
+SRBD QPs from seed + global QP index, so the data path has no
+collective; `value` = QPs solved by all ranks / max-over-ranks wall time
+("scaling": "weak").  After the timed region the solutions are gathered to
+rank 0 over RCCL (BASELINE config 4) and that rate is reported separately.
+
+Rank 0 prints ONE JSON line on stdout; progress goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent
+PKG_DIR = REPO / "srbd-nmpc-solver_amd"
+
+METRIC = "SRBD OCP-QP solves/sec (N=20, nx=12, nu=12, fp64) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFS = 78.6     # FP64 vector/matrix
+
+WORKLOADS = {
+    # name: (N, constraints, default batch, description)
+    "unconstr_n20": (20, "none", 65536,
+                     "SRBD NMPC QP as the reference builds it (friction cone as barrier in the cost, "
+                     "no inequalities), batch 65536, N=20"),
+    "unconstr_n10_b4096": (10, "none", 4096, "BASELINE config 2: batch 4096, N=10"),
+}
+DEFAULT_WORKLOAD = "unconstr_n20"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def import_pkg():
+    name = "srbd_nmpc_solver_amd"
+    if name in sys.modules:
+        return sys.modules[name]
+    spec = importlib.util.spec_from_file_location(name, PKG_DIR / "__init__.py",
+                                                  submodule_search_locations=[str(PKG_DIR)])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def alg_bytes_per_qp(N, nx=12, nu=12, constraints="none"):
+    """dense interface read once + x, u, pi written once (fp64)."""
+    stage = nx * nx + nx * nu + nx + nx * nx + nu * nx + nu * nu + nx + nu  # A B b Q S R q r
+    vals = N * stage + nx * nx + nx + nx  # + terminal Q, q + x0
+    if constraints == "box_u":
+        vals += N * 2 * nu
+    out = (N + 1) * nx + N * nu + (N + 1) * nx
+    return 8 * (vals + out)
+
+
+def alg_flops_per_qp(N, nx=12, nu=12):
+    """SURVEY.md 8(d) flop count of one Riccati factor + solve sweep."""
+    n = nx + nu
+    back = 2 * (n + 1) * nx * nx + 2 * nx * (n * (n + 1) // 2 + n) + n ** 3 / 3 + n * n + 2 * nx * nx * (nx + 1) / 2
+    fwd = nu * nu + 2 * nu * nx + 2 * (n + 1) * nx + 2 * nx * nx
+    return N * (back + fwd)
+
+
+def make_shard(pkg, N, constraints, batch, rank, seed, pool):
+    """Distinct QPs for this rank: a pool of `pool` QPs generated from
+    seed + global index, tiled to `batch` (addresses distinct, data repeats)."""
+    pool = min(pool, batch)
+    qp, x0 = pkg.srbd_model.generate_batch(pool, N=N, seed=seed, constraints=constraints,
+                                           first=rank * batch)
+    return qp, x0
+
+
+def to_device(pkg, qp, x0, batch, device):
+    import torch
+    p = qp.packed()
+    p["x0"] = np.ascontiguousarray(x0)
+    pool = qp.batch
+    reps = (batch + pool - 1) // pool
+    dt = {}
+    for k, v in p.items():
+        if v is None:
+            dt[k] = None
+            continue
+        t = torch.from_numpy(v).to(device)
+        if reps > 1:
+            t = t.repeat((reps,) + (1,) * (t.dim() - 1))
+        dt[k] = t[:batch].contiguous()
+    return dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default=DEFAULT_WORKLOAD, choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="QPs per rank (default: workload's)")
+    ap.add_argument("--pool", type=int, default=4096, help="distinct QPs generated per rank")
+    ap.add_argument("--seed", type=int, default=1003)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    pkg = import_pkg()
+    capi = pkg.capi
+
+    N, constraints, default_batch, desc = WORKLOADS[args.workload]
+    batch = args.batch or default_batch
+    log(f"[rank {rank}] workload={args.workload} batch/rank={batch} N={N} world={world}")
+    t0 = time.perf_counter()
+    qp, x0 = make_shard(pkg, N, constraints, batch, rank, args.seed, args.pool)
+    dt = to_device(pkg, qp, x0, batch, device)
+    log(f"[rank {rank}] generated + uploaded in {time.perf_counter() - t0:.1f}s")
+
+    h = capi.Handle(N, 12, 12, qp.ng, qp.has_box_u, qp.has_box_x, capacity=batch, device=local_rank)
+    f64 = dict(dtype=torch.float64, device=device)
+    sol_t = {"x": torch.zeros(batch, N + 1, 12, **f64), "u": torch.zeros(batch, N, 12, **f64),
+             "pi": torch.zeros(batch, N + 1, 12, **f64),
+             "status": torch.zeros(batch, dtype=torch.int32, device=device),
+             "iter": torch.zeros(batch, dtype=torch.int32, device=device)}
+    data = capi.Data(**{k: (None if dt.get(k) is None else dt[k].data_ptr()) for k in capi.DATA_FIELDS})
+    sol = capi.Solution(**{k: (sol_t[k].data_ptr() if k in sol_t else None) for k in capi.SOL_FIELDS})
+    # solver settings of the reference caller (NMPC_solver.cpp:70-82)
+    settings = capi.settings_struct({"mode": "Speed", "iter_max": 30, "alpha_min": 1e-8, "mu0": 1e2,
+                                     "tol_stat": 1e-4, "tol_eq": 1e-4, "tol_ineq": 1e-4,
+                                     "tol_comp": 1e-4, "reg_prim": 1e-12, "warm_start": 0,
+                                     "pred_corr": 1, "ric_alg": 0, "split_step": 1})
+    stream_ptr = h.stream()
+    ext = torch.cuda.ExternalStream(stream_ptr, device=device)
+
+    for _ in range(args.warmup):
+        h.solve_device(batch, settings, data, sol)
+    h.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t_start = time.perf_counter()
+    ev0.record(ext)
+    for _ in range(args.steps):
+        h.solve_device(batch, settings, data, sol)
+    ev1.record(ext)
+    h.synchronize()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    t_wall = time.perf_counter() - t_start
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    t_tensor = torch.tensor([t_wall], dtype=torch.float64, device=device)
+    if distributed:
+        dist.all_reduce(t_tensor, op=dist.ReduceOp.MAX)
+    t_max = float(t_tensor.item())
+    status = sol_t["status"].cpu().numpy()
+    iters = sol_t["iter"].cpu().numpy()
+    n_ok = int((status == 0).sum())
+    log(f"[rank {rank}] wall {t_wall * 1e3:.2f} ms for {args.steps} steps, kernel avg {kernel_ms:.3f} ms, "
+        f"success {n_ok}/{batch}")
+
+    # ---- solution gather to rank 0 over RCCL (BASELINE config 4) ----
+    gather_ms = None
+    if distributed and not args.no_gather:
+        payload = torch.cat([sol_t["x"].reshape(batch, -1), sol_t["u"].reshape(batch, -1),
+                             sol_t["pi"].reshape(batch, -1)], dim=1).contiguous()
+        bufs = [torch.empty_like(payload) for _ in range(world)] if rank == 0 else None
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            dist.gather(payload, bufs, dst=0)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) / reps * 1e3
+
+    if rank != 0:
+        if distributed:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    total_qps = batch * world
+    value = total_qps * args.steps / t_max
+    ms_per_step = t_max / args.steps * 1e3
+    bytes_qp = alg_bytes_per_qp(N, constraints=constraints)
+    achieved_gbs = bytes_qp * batch / (kernel_ms * 1e-3) / 1e9
+    flops_qp = alg_flops_per_qp(N)
+
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline(pkg, qp, x0, settings_dict(settings), args.cpu_seconds)
+
+    traffic = pmc_traffic(args.workload, batch)
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "QP solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": f"synthetic SRBD linearisations (seed {args.seed}; pool of {min(args.pool, batch)} "
+                f"distinct QPs per rank tiled to the batch), generated per rank",
+        "config": {"workload": args.workload, "description": desc, "batch_per_gpu": batch,
+                   "global_batch": total_qps, "N": N, "nx": 12, "nu": 12, "constraints": constraints,
+                   "parallelism": f"dp{world} (independent QP shards)",
+                   "settings": "NMPC_solver.cpp:70-82 (Speed, iter_max 30, tol 1e-4, split_step)"},
+        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "riccati_unconstr_kernel<true>", "kernel_avg_ms": kernel_ms,
+                     "alg_bytes_per_qp": bytes_qp},
+        "fp64_frac": flops_qp * batch / (kernel_ms * 1e-3) / (FP64_PEAK_TFS * 1e12),
+        "success_rate": n_ok / batch,
+        "iters_mean": float(iters.mean()), "iters_max": int(iters.max()),
+        "cpu_baseline": cpu,
+    }
+    if gather_ms is not None:
+        line["gather"] = {"ms": gather_ms, "bytes_per_rank": batch * (2 * (N + 1) * 12 + N * 12) * 8,
+                          "value_with_gather": total_qps / (t_max / args.steps + gather_ms * 1e-3)}
+    print(json.dumps(line), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def settings_dict(s):
+    return {k: getattr(s, k) for k, _ in s._fields_}
+
+
+def cpu_baseline(pkg, qp, x0, settings, budget_s):
+    """The C oracle ('port': same algorithm, scalar C, -O3, x86-64-v3) on the host
+    cores over a bounded sample of the same workload."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle  # test infrastructure, used here only as the CPU baseline
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(threads, 256))
+    cal = qp.subset(slice(0, min(qp.batch, 4 * threads)))
+    _, dt = oracle.solve_batch_threaded(cal, settings, x0[:cal.batch], threads)
+    rate = cal.batch / max(dt, 1e-9)
+    n = int(min(qp.batch, max(cal.batch, rate * budget_s)))
+    reps = 1
+    sample = qp.subset(slice(0, n))
+    if n == qp.batch and rate * budget_s > n:
+        reps = max(1, int(rate * budget_s / n))
+    t = 0.0
+    for _ in range(reps):
+        _, d = oracle.solve_batch_threaded(sample, settings, x0[:n], threads)
+        t += d
+    return {"value": n * reps / t, "unit": "QP solves/s", "cores": threads, "kind": "port",
+            "sample": f"{n} QPs x {reps} reps of the same workload ({t:.1f} s, {threads} threads, "
+                      f"oracle/ocp_qp_oracle.c)"}
+
+
+def pmc_traffic(workload, batch):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    f = REPO / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        e = d.get(workload)
+        if e and int(e.get("batch", -1)) == batch:
+            return e.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+if __name__ == "__main__":
+    main()

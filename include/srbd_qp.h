@@ -1,0 +1,188 @@
+/*
+ * srbd_qp.h -- C-ABI of the MI355X-native batched OCP-QP solver (libsrbd_qp.so).
+ *
+ * This is the drop-in boundary for the reference's hot path: everything
+ * hpipm::OcpQpIpmSolver::solve() does below the Eigen marshalling
+ * (hpipm-cpp/src/ocp_qp_ipm_solver.cpp:181-414) -- d_ocp_qp_set_all (:283),
+ * d_ocp_qp_ipm_solve (:334, decl hpipm_d_ocp_qp_ipm.h:238), the solution and
+ * Riccati getters (:337-346) and the stage-0 rebuild (:347-373) -- batched
+ * over thousands of independent QPs and run by hand-written HIP kernels for
+ * gfx950.  Plain C types only; no exceptions cross this boundary.
+ *
+ * Entry point -> reference interface it replaces:
+ *   srbd_qp_create       OcpQpIpmSolver(qp, settings) ctor + resize()
+ *                        (ocp_qp_ipm_solver.cpp:60-68, :120-178): dims check,
+ *                        workspace sizing (d_ocp_qp_ipm_ws_create).
+ *   srbd_qp_solve_f64    OcpQpIpmSolver::solve (ocp_qp_ipm_solver.cpp:181-414)
+ *                        on a batch of device-resident QPs, asynchronous.
+ *   srbd_qp_solve_host_f64  the same from host buffers, synchronous (what the
+ *                        hpipm-cpp shim calls for one QP or a small batch).
+ *   srbd_qp_destroy      ~OcpQpIpmSolver (d_ocp_qp_*_wrapper frees).
+ *   srbd_qp_status_string  hpipm::to_string(HpipmStatus) (:19-33).
+ *
+ * ------------------------------------------------------------------------
+ * Problem (per QP, stages k = 0..N), identical to hpipm::OcpQp
+ * (hpipm-cpp/include/hpipm-cpp/ocp_qp.hpp:15-177):
+ *   min  sum_k 1/2 x'Q x + u'S x + 1/2 u'R u + q'x + r'u
+ *   s.t. x[k+1] = A x[k] + B u[k] + b,  x[0] = x0,
+ *        lbu <= u <= ubu, lbx <= x <= ubx (k >= 1), lg <= C x + D u <= ug.
+ * x0 is embedded like hpipm-cpp does it (nx[0] = nbx[0] = 0,
+ * ocp_qp_ipm_solver.cpp:128-130): box-x bounds and C at stage 0 are ignored.
+ *
+ * Memory layout (every pointer may be host or device memory as the entry
+ * point says; 16-byte aligned base pointers are required for the fast path):
+ *   batch-major, then stage-major, then one dense block per stage.  Matrix
+ *   blocks are column-major (Eigen's default, what d_ocp_qp_set_all reads):
+ *     A [batch][N  ][nx*nx]   B [batch][N][nx*nu]   b [batch][N][nx]
+ *     Q [batch][N+1][nx*nx]   S [batch][N][nu*nx]   R [batch][N][nu*nu]
+ *     q [batch][N+1][nx]      r [batch][N][nu]      x0 [batch][nx]
+ *   Box constraints are dense per variable: one bound per variable plus an
+ *   optional 0/1 mask per bound (a NULL mask means "all bounds active"; a
+ *   masked bound is absent, exactly like hpipm's d_ocp_qp_set_l*_mask).  The
+ *   reference's index form (idxbu/idxbx) maps onto this by setting mask 0 for
+ *   variables not in the index list (the hpipm-cpp shim does this).
+ *     lbu, ubu, lbu_mask, ubu_mask [batch][N][nu]        (NULL lbu: no box)
+ *     lbx, ubx, lbx_mask, ubx_mask [batch][N+1][nx]      (NULL lbx: no box)
+ *   General constraints (ng rows per stage, pad with masked rows):
+ *     C [batch][N+1][ng*nx]  D [batch][N][ng*nu]  lg, ug, lg_mask, ug_mask [batch][N+1][ng]
+ * Outputs:
+ *     x [batch][N+1][nx]  u [batch][N][nu]  pi [batch][N+1][nx]   (required)
+ *     P [batch][N+1][nx*nx]  p [batch][N+1][nx]  K [batch][N][nu*nx]  k [batch][N][nu]
+ *     status [batch] (HpipmStatus codes)  iter [batch]  res [batch][4]  obj [batch]
+ *   Conventions (ocp_qp_ipm_solver.cpp:337-373, test/ocp_qp_ipm_solver.cpp:60-109):
+ *     x[0] = x0; pi[k] is the multiplier of x[k] = A x[k-1] + ... (hpipm pi[k-1]),
+ *     pi[k] = P[k] x[k] + p[k]; u[k] = K[k] x[k] + k[k]; stage 0 as rebuilt.
+ *
+ * Dimensions: 1 <= nx, nu <= 12, 1 <= N <= 1024, 0 <= ng <= 64.  nx = nu = 12
+ * (the SRBD model) takes the fast path; smaller problems are zero-padded
+ * inside the kernel (exact: padded states stay 0, padded inputs get R = 1).
+ */
+#ifndef SRBD_QP_H_
+#define SRBD_QP_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRBD_QP_ABI_VERSION 1
+#define SRBD_QP_MAX_NX 12
+#define SRBD_QP_MAX_NU 12
+#define SRBD_QP_MAX_NG 64
+
+/* error codes (returned by every entry point) */
+enum {
+  SRBD_QP_OK = 0,
+  SRBD_QP_EINVAL = -1,      /* NULL / inconsistent argument                 */
+  SRBD_QP_EDIM = -2,        /* dimensions outside the supported range        */
+  SRBD_QP_ENOMEM = -3,      /* device allocation failed                      */
+  SRBD_QP_EDEVICE = -4,     /* HIP runtime error / no GPU                     */
+  SRBD_QP_ECAPACITY = -5,   /* batch larger than the handle's capacity        */
+  SRBD_QP_ESETTINGS = -6    /* settings rejected (checkSettings rules)        */
+};
+
+/* per-QP solver status, same codes as hpipm::HpipmStatus
+ * (hpipm-cpp/include/hpipm-cpp/ocp_qp_ipm_solver.hpp:24-30)                */
+enum {
+  SRBD_QP_SUCCESS = 0,
+  SRBD_QP_MAX_ITER = 1,
+  SRBD_QP_MIN_STEP = 2,
+  SRBD_QP_NAN_SOL = 3,
+  SRBD_QP_UNKNOWN_FAILURE = 4
+};
+
+/* hpipm::HpipmMode (ocp_qp_ipm_solver_settings.hpp:10-15) */
+enum { SRBD_QP_MODE_SPEED_ABS = 0, SRBD_QP_MODE_SPEED = 1, SRBD_QP_MODE_BALANCE = 2,
+       SRBD_QP_MODE_ROBUST = 3 };
+
+typedef struct srbd_qp_dims {
+  int N;          /* horizon                                                */
+  int nx, nu;     /* uniform state / input dimensions                        */
+  int ng;         /* general constraints per stage (0 = none)                */
+  int has_box_u;  /* 1 if lbu/ubu will be passed                             */
+  int has_box_x;  /* 1 if lbx/ubx will be passed                             */
+} srbd_qp_dims;
+
+/* hpipm::OcpQpIpmSolverSettings (ocp_qp_ipm_solver_settings.hpp:26-86);
+ * srbd_qp_default_settings() gives the same defaults.                     */
+typedef struct srbd_qp_settings {
+  int mode;
+  int iter_max;
+  double alpha_min;
+  double mu0;
+  double tol_stat, tol_eq, tol_ineq, tol_comp;
+  double reg_prim;
+  int warm_start;   /* 1: x/u output buffers hold the primal warm start     */
+  int pred_corr;
+  int ric_alg;      /* accepted; both values run the classical recursion   */
+  int split_step;
+  int compute_residuals; /* 1: fill res/obj also for unconstrained QPs     */
+} srbd_qp_settings;
+
+typedef struct srbd_qp_data_f64 {
+  const double *A, *B, *b, *Q, *S, *R, *q, *r;
+  const double *lbu, *ubu, *lbu_mask, *ubu_mask;
+  const double *lbx, *ubx, *lbx_mask, *ubx_mask;
+  const double *C, *D, *lg, *ug, *lg_mask, *ug_mask;
+  const double *x0;
+} srbd_qp_data_f64;
+
+typedef struct srbd_qp_solution_f64 {
+  double *x, *u, *pi;      /* required                                     */
+  double *P, *p, *K, *k;   /* optional Riccati outputs (may be NULL)        */
+  int *status, *iter;      /* optional                                     */
+  double *res;             /* optional [batch][4] max |res_stat|,|res_eq|,|res_ineq|,|res_comp| */
+  double *obj;             /* optional [batch]                              */
+} srbd_qp_solution_f64;
+
+typedef struct srbd_qp_handle_s* srbd_qp_handle;
+
+/* Fill *s with hpipm-cpp's defaults (Speed, iter_max 15, tol 1e-8, mu0 100,
+ * alpha_min 1e-8, reg_prim 1e-12, pred_corr 1, ric_alg 1, split_step 0).   */
+void srbd_qp_default_settings(srbd_qp_settings* s);
+
+/* Validate settings like OcpQpIpmSolverSettings::checkSettings
+ * (ocp_qp_ipm_solver_settings.cpp:7-38); returns SRBD_QP_ESETTINGS with a
+ * message retrievable by srbd_qp_last_error().                              */
+int srbd_qp_check_settings(const srbd_qp_settings* s);
+
+/* Create a solver for `dims` able to solve up to `batch_capacity` QPs per call
+ * on HIP device `device`.  Allocates the device workspace and one stream.  */
+int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device,
+                   srbd_qp_handle* out);
+
+/* Device-resident batch solve, asynchronous on `stream` (a hipStream_t; NULL
+ * = the handle's own stream).  Every data/solution pointer is device memory.
+ * With settings->warm_start the x/u buffers are read as the warm start.    */
+int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
+                      const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol,
+                      void* stream);
+
+/* Host-buffer batch solve: copies to device, solves, copies back, waits.   */
+int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
+                           const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol);
+
+/* Blocks until all work queued on the handle's stream is done.            */
+int srbd_qp_synchronize(srbd_qp_handle h);
+
+/* The handle's hipStream_t (for event timing / stream interop).           */
+void* srbd_qp_stream(srbd_qp_handle h);
+
+/* Device workspace bytes the handle holds.                                */
+size_t srbd_qp_workspace_bytes(srbd_qp_handle h);
+
+void srbd_qp_destroy(srbd_qp_handle h);
+
+/* "HpipmStatus::Success" ... like hpipm::to_string (ocp_qp_ipm_solver.cpp:19-33) */
+const char* srbd_qp_status_string(int status);
+const char* srbd_qp_error_string(int err);
+/* Message of the last error raised on this thread (never NULL).           */
+const char* srbd_qp_last_error(void);
+
+int srbd_qp_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SRBD_QP_H_ */

@@ -20,9 +20,9 @@ __version__ = "0.1.0"
 
 def __getattr__(name):
     # lazy: importing the package must work on a CPU-only host (tests, build()).
-    if name in ("capi",):
+    if name in ("capi", "srbd_model", "solver"):
         import importlib
-        return importlib.import_module(f"{__name__}.capi")
+        return importlib.import_module(f"{__name__}.{name}")
     if name in ("OcpQpIpmSolver", "OcpQpIpmSolverSettings", "HpipmMode", "HpipmStatus", "solve_batch"):
         from . import solver
         return getattr(solver, name)

@@ -1,0 +1,232 @@
+"""ctypes binding of libsrbd_qp.so (the C-ABI declared in include/srbd_qp.h).
+
+Device memory comes from torch (HIP tensors); every call goes through the
+HIP kernels.  Importing this module on a host without the built library or
+without a GPU works; calling a solve raises :class:`SrbdQpError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+from typing import Dict, Optional
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "libsrbd_qp.so"
+
+_dp = C.c_void_p
+
+
+class SrbdQpError(RuntimeError):
+    pass
+
+
+class Dims(C.Structure):
+    _fields_ = [("N", C.c_int), ("nx", C.c_int), ("nu", C.c_int), ("ng", C.c_int),
+                ("has_box_u", C.c_int), ("has_box_x", C.c_int)]
+
+
+class Settings(C.Structure):
+    _fields_ = [("mode", C.c_int), ("iter_max", C.c_int), ("alpha_min", C.c_double),
+                ("mu0", C.c_double), ("tol_stat", C.c_double), ("tol_eq", C.c_double),
+                ("tol_ineq", C.c_double), ("tol_comp", C.c_double), ("reg_prim", C.c_double),
+                ("warm_start", C.c_int), ("pred_corr", C.c_int), ("ric_alg", C.c_int),
+                ("split_step", C.c_int), ("compute_residuals", C.c_int)]
+
+
+DATA_FIELDS = ("A", "B", "b", "Q", "S", "R", "q", "r",
+               "lbu", "ubu", "lbu_mask", "ubu_mask",
+               "lbx", "ubx", "lbx_mask", "ubx_mask",
+               "C", "D", "lg", "ug", "lg_mask", "ug_mask", "x0")
+SOL_FIELDS = ("x", "u", "pi", "P", "p", "K", "k", "status", "iter", "res", "obj")
+
+
+class Data(C.Structure):
+    _fields_ = [(n, _dp) for n in DATA_FIELDS]
+
+
+class Solution(C.Structure):
+    _fields_ = [(n, _dp) for n in SOL_FIELDS]
+
+
+MODES = {"SpeedAbs": 0, "Speed": 1, "Balance": 2, "Robust": 3}
+
+_lib = None
+
+
+def lib():
+    """Load libsrbd_qp.so (raises SrbdQpError if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise SrbdQpError(f"{LIB_PATH} not built; run `make` (or __graft_entry__.build())")
+        L = C.CDLL(str(LIB_PATH))
+        L.srbd_qp_create.argtypes = [C.POINTER(Dims), C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+        L.srbd_qp_create.restype = C.c_int
+        L.srbd_qp_solve_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings), C.POINTER(Data),
+                                        C.POINTER(Solution), C.c_void_p]
+        L.srbd_qp_solve_f64.restype = C.c_int
+        L.srbd_qp_solve_host_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
+                                             C.POINTER(Data), C.POINTER(Solution)]
+        L.srbd_qp_solve_host_f64.restype = C.c_int
+        L.srbd_qp_destroy.argtypes = [C.c_void_p]
+        L.srbd_qp_destroy.restype = None
+        L.srbd_qp_synchronize.argtypes = [C.c_void_p]
+        L.srbd_qp_synchronize.restype = C.c_int
+        L.srbd_qp_stream.argtypes = [C.c_void_p]
+        L.srbd_qp_stream.restype = C.c_void_p
+        L.srbd_qp_workspace_bytes.argtypes = [C.c_void_p]
+        L.srbd_qp_workspace_bytes.restype = C.c_size_t
+        L.srbd_qp_default_settings.argtypes = [C.POINTER(Settings)]
+        L.srbd_qp_default_settings.restype = None
+        L.srbd_qp_check_settings.argtypes = [C.POINTER(Settings)]
+        L.srbd_qp_check_settings.restype = C.c_int
+        L.srbd_qp_status_string.argtypes = [C.c_int]
+        L.srbd_qp_status_string.restype = C.c_char_p
+        L.srbd_qp_error_string.argtypes = [C.c_int]
+        L.srbd_qp_error_string.restype = C.c_char_p
+        L.srbd_qp_last_error.argtypes = []
+        L.srbd_qp_last_error.restype = C.c_char_p
+        L.srbd_qp_abi_version.argtypes = []
+        L.srbd_qp_abi_version.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    """Names the header declares (used by the CPU export test)."""
+    hdr = (PKG_DIR.parent / "include" / "srbd_qp.h").read_text()
+    import re
+    return sorted(set(re.findall(r"\b(srbd_qp_[a-z0-9_]+)\s*\(", hdr)))
+
+
+def check(rc: int, what: str = "srbd_qp") -> None:
+    if rc != 0:
+        L = lib()
+        raise SrbdQpError(f"{what}: {L.srbd_qp_error_string(rc).decode()} ({rc}): "
+                          f"{L.srbd_qp_last_error().decode()}")
+
+
+def settings_struct(s: Optional[Dict] = None) -> Settings:
+    st = Settings()
+    lib().srbd_qp_default_settings(C.byref(st))
+    if s:
+        for k, v in s.items():
+            if k == "mode":
+                v = MODES[v] if isinstance(v, str) else int(v)
+            if hasattr(st, k):
+                setattr(st, k, v)
+    return st
+
+
+def status_string(code: int) -> str:
+    return lib().srbd_qp_status_string(int(code)).decode()
+
+
+class Handle:
+    """Owns a srbd_qp_handle (device workspace + stream) for fixed dims."""
+
+    def __init__(self, N: int, nx: int, nu: int, ng: int = 0, has_box_u: bool = False,
+                 has_box_x: bool = False, capacity: int = 1, device: int = 0):
+        self.dims = Dims(N, nx, nu, ng, int(has_box_u), int(has_box_x))
+        self.capacity = int(capacity)
+        self.device = int(device)
+        h = C.c_void_p()
+        check(lib().srbd_qp_create(C.byref(self.dims), self.capacity, self.device, C.byref(h)),
+              "srbd_qp_create")
+        self._h = h
+
+    @property
+    def ptr(self):
+        return self._h
+
+    def stream(self) -> int:
+        return int(lib().srbd_qp_stream(self._h) or 0)
+
+    def workspace_bytes(self) -> int:
+        return int(lib().srbd_qp_workspace_bytes(self._h))
+
+    def synchronize(self) -> None:
+        check(lib().srbd_qp_synchronize(self._h), "srbd_qp_synchronize")
+
+    def solve_device(self, batch: int, settings: Settings, data: Data, sol: Solution,
+                     stream: int = 0) -> None:
+        check(lib().srbd_qp_solve_f64(self._h, int(batch), C.byref(settings), C.byref(data),
+                                      C.byref(sol), C.c_void_p(stream or None)),
+              "srbd_qp_solve_f64")
+
+    def solve_host(self, batch: int, settings: Settings, data: Data, sol: Solution) -> None:
+        check(lib().srbd_qp_solve_host_f64(self._h, int(batch), C.byref(settings), C.byref(data),
+                                           C.byref(sol)), "srbd_qp_solve_host_f64")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().srbd_qp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _tensor_ptr(t) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+def device_buffers(qp, x0: np.ndarray, device="cuda:0", want_riccati: bool = False,
+                   x_init=None, u_init=None):
+    """Upload an OcpQpBatch (+x0) to device tensors in the C-ABI layout.
+
+    Returns (data_tensors, sol_tensors, Data, Solution)."""
+    import torch
+    p = qp.packed()
+    p["x0"] = np.ascontiguousarray(x0, dtype=np.float64).reshape(qp.batch, qp.nx)
+    dt = {k: (None if v is None else torch.from_numpy(np.ascontiguousarray(v)).to(device))
+          for k, v in p.items()}
+    nb, N, nx, nu = qp.batch, qp.N, qp.nx, qp.nu
+    f64 = dict(dtype=torch.float64, device=device)
+    st = {
+        "x": torch.zeros(nb, N + 1, nx, **f64) if x_init is None
+        else torch.from_numpy(np.ascontiguousarray(x_init, dtype=np.float64)).to(device),
+        "u": torch.zeros(nb, N, nu, **f64) if u_init is None
+        else torch.from_numpy(np.ascontiguousarray(u_init, dtype=np.float64)).to(device),
+        "pi": torch.zeros(nb, N + 1, nx, **f64),
+        "status": torch.full((nb,), -1, dtype=torch.int32, device=device),
+        "iter": torch.full((nb,), -1, dtype=torch.int32, device=device),
+        "res": torch.zeros(nb, 4, **f64),
+        "obj": torch.zeros(nb, **f64),
+    }
+    if want_riccati:
+        st["P"] = torch.zeros(nb, N + 1, nx, nx, **f64)  # col-major blocks
+        st["p"] = torch.zeros(nb, N + 1, nx, **f64)
+        st["K"] = torch.zeros(nb, N, nx, nu, **f64)      # col-major nu x nx blocks
+        st["k"] = torch.zeros(nb, N, nu, **f64)
+    data = Data(**{k: _tensor_ptr(dt.get(k)) or None for k in DATA_FIELDS})
+    sol = Solution(**{k: _tensor_ptr(st.get(k)) or None for k in SOL_FIELDS})
+    return dt, st, data, sol
+
+
+def solve(qp, x0, settings: Optional[Dict] = None, device: str = "cuda:0", riccati: bool = False,
+          x_init=None, u_init=None, handle: Optional[Handle] = None) -> Dict[str, np.ndarray]:
+    """Solve an OcpQpBatch on the GPU through the C-ABI; returns numpy results."""
+    import torch
+    if not torch.cuda.is_available():
+        raise SrbdQpError("no GPU available: libsrbd_qp has no CPU fallback")
+    dev_index = torch.device(device).index or 0
+    h = handle or Handle(qp.N, qp.nx, qp.nu, qp.ng, qp.has_box_u, qp.has_box_x,
+                         capacity=qp.batch, device=dev_index)
+    dt, st, data, sol = device_buffers(qp, x0, device, riccati, x_init, u_init)
+    s = settings_struct(settings)
+    h.solve_device(qp.batch, s, data, sol)
+    h.synchronize()
+    out = {k: v.cpu().numpy() for k, v in st.items()}
+    if riccati:
+        out["P"] = np.swapaxes(out["P"], -1, -2)
+        out["K"] = np.swapaxes(out["K"], -1, -2)
+    if handle is None:
+        h.close()
+    return out

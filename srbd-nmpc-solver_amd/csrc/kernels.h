@@ -1,0 +1,44 @@
+// kernels.h -- launch interface between the C-ABI (srbd_qp_capi.hip) and the
+// HIP kernels.  Internal; not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+namespace srbd {
+
+// Forward-pass record of one stage, written by the backward sweep and read
+// back (row-owned) by the forward sweep.  Row-major blocks so that lane i of
+// the forward pass loads row i as 96 contiguous bytes.
+constexpr int kWsK = 0;      // K   [12][12] row-major (u-row i)
+constexpr int kWsAcl = 144;  // Acl [12][12] row-major
+constexpr int kWsP = 288;    // P   [12][12] (symmetric)
+constexpr int kWsk = 432;    // k   [12]
+constexpr int kWsbcl = 444;  // bcl [12]
+constexpr int kWsp = 456;    // p   [12]
+constexpr int kWsStage = 480;  // doubles per stage record (16-byte multiple)
+
+struct ProblemArgs {
+  int batch, N, nx, nu, ng;
+  // QP data (device)
+  const double *A, *B, *b, *Q, *S, *R, *q, *r, *x0;
+  const double *lbu, *ubu, *lbu_mask, *ubu_mask;
+  const double *lbx, *ubx, *lbx_mask, *ubx_mask;
+  const double *C, *D, *lg, *ug, *lg_mask, *ug_mask;
+  // solution (device)
+  double *x, *u, *pi, *P, *p, *K, *k;
+  int *status, *iter;
+  double *res, *obj;
+  // workspace
+  double* ws;
+  size_t ws_qp;  // doubles per QP
+  double reg;
+};
+
+// Workspace doubles per QP needed by the unconstrained solve.
+size_t ws_doubles_unconstr(int N);
+
+hipError_t launch_riccati_unconstr(const ProblemArgs& a, hipStream_t stream);
+
+}  // namespace srbd

@@ -1,0 +1,120 @@
+// qp_group.h -- the 16-lane "QP group" execution model used by every kernel.
+//
+// One OCP-QP is owned by one DPP row (16 consecutive lanes of a 64-lane
+// wavefront), so a wavefront advances four QPs in lockstep and a 256-thread
+// workgroup sixteen.  Inside a group, lane j < 12 owns column j of every
+// 12x12 stage block (the QP's matrices are stored column-major, so a lane's
+// column is 96 contiguous bytes) and lane 15 (VL) owns the vector column
+// (b / r / q / p ...).  Lanes 12..14 idle.
+//
+// Cross-lane traffic is a broadcast of one lane's register to its whole
+// row: gfx950's DPP row_newbcast, which hipcc emits as v_mov_b64_dpp for
+// __builtin_amdgcn_update_dpp(..., 0x150 + src, ...).  With the source lane
+// and the register index both compile-time constants, every product the
+// Riccati recursion needs becomes a chain of broadcast + FMA with no LDS and
+// no bank conflicts:
+//   C = X  Y   (X symmetric, Y column-owned):  C[:,j] += bc<k>(X[i]) * Y[k]
+//   C = X' Y   (both column-owned):            C[i][j] += bc<i>(X[k]) * Y[k]
+//   y = M  v   (M row-owned, v element-owned): y[i]   += M[j] * bc<j>(v)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+#include <utility>
+
+namespace srbd {
+
+constexpr int kMaxDim = 12;   // nx, nu handled in registers
+constexpr int kGroup = 16;    // lanes per QP (one DPP row)
+constexpr int kVecLane = 15;  // lane holding the vector column
+
+template <int I>
+using ic = std::integral_constant<int, I>;
+
+// compile-time loop: f(ic<B>), f(ic<B+1>), ..., f(ic<E-1>)
+template <int B, int E, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(ic<B>{});
+    sfor<B + 1, E>(static_cast<F&&>(f));
+  }
+}
+// descending: f(ic<E-1>), ..., f(ic<B>)
+template <int B, int E, typename F>
+__device__ __forceinline__ void sfor_down(F&& f) {
+  if constexpr (B < E) {
+    f(ic<E - 1>{});
+    sfor_down<B, E - 1>(static_cast<F&&>(f));
+  }
+}
+
+// Broadcast lane SRC of this lane's 16-lane row (DPP row_newbcast:SRC).
+template <int SRC>
+__device__ __forceinline__ double bc(double v) {
+  static_assert(SRC >= 0 && SRC < kGroup, "row_newbcast source lane");
+  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + SRC, 0xf, 0xf, true);
+}
+
+template <int SRC>
+__device__ __forceinline__ float bc(float v) {
+  static_assert(SRC >= 0 && SRC < kGroup, "row_newbcast source lane");
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x150 + SRC, 0xf, 0xf, true));
+}
+
+// Opaque copy: the compiler can no longer prove the values equal to the
+// originals, so broadcasts of the laundered array are not CSE'd with earlier
+// broadcasts of the same registers (which would keep 144 broadcast values
+// live across phases and spill).
+template <typename T>
+__device__ __forceinline__ void opaque(T& x) {
+  asm volatile("" : "+v"(x));
+}
+template <typename T, int... Is>
+__device__ __forceinline__ void launder_impl(T (&v)[12], std::integer_sequence<int, Is...>) {
+  (opaque(v[Is]), ...);
+}
+template <typename T>
+__device__ __forceinline__ void launder(T (&v)[12]) {
+  launder_impl(v, std::make_integer_sequence<int, 12>{});
+}
+
+template <typename T>
+__device__ __forceinline__ T fmadd(T a, T b, T c) {
+  return __builtin_fma(a, b, c);
+}
+template <>
+__device__ __forceinline__ float fmadd<float>(float a, float b, float c) {
+  return __builtin_fmaf(a, b, c);
+}
+
+// 12 contiguous values -> registers (16-byte vector loads for double).
+__device__ __forceinline__ void load12(const double* __restrict__ p, double (&v)[12]) {
+  const double2* p2 = reinterpret_cast<const double2*>(p);
+  sfor<0, 6>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    double2 t = p2[I];
+    v[2 * I] = t.x;
+    v[2 * I + 1] = t.y;
+  });
+}
+__device__ __forceinline__ void store12(double* __restrict__ p, const double (&v)[12]) {
+  double2* p2 = reinterpret_cast<double2*>(p);
+  sfor<0, 6>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    p2[I] = make_double2(v[2 * I], v[2 * I + 1]);
+  });
+}
+
+// Generic predicated column load: v[i] = (col_ok && i < rows) ? p[i] : 0.
+template <typename T>
+__device__ __forceinline__ void load_col_pad(const T* __restrict__ p, int rows, bool col_ok,
+                                             T (&v)[12]) {
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    v[I] = (col_ok && I < rows) ? p[I] : T(0);
+  });
+}
+
+}  // namespace srbd

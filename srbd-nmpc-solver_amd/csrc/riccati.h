@@ -1,0 +1,201 @@
+// riccati.h -- per-stage Riccati building blocks on a 16-lane QP group.
+//
+// Math (classical Riccati, ric_alg = 0, as pinned by the reference test
+// hpipm-cpp/test/ocp_qp_ipm_solver.cpp:67-90, with p = -s):
+//   WB = P B,  G = R + B'WB,  L = chol(G + reg I)
+//   W  = P [A | b] + [0 | p]
+//   H  = S + B'W_A,  g = r + B'w,  F = Q + A'W_A,  f = q + A'w
+//   Y  = L^-1 H,  y = L^-1 g,  K = -L^-T Y,  k = -L^-T y
+//   P- = F - Y'Y,  p- = f - Y'y
+//   Acl = A + B K,  bcl = b + B k           (closed loop, for the forward pass)
+// This is HPIPM's d_ocp_qp_fact_solve_kkt_unconstr (hpipm_d_ocp_qp_kkt.h:54)
+// i.e. the BLASFEO dgemm_nt / dsyrk_ln / dpotrf_l / dtrsv chain, re-blocked
+// for one-column-per-lane.  A non-positive pivot zeroes its direction like
+// BLASFEO's dpotrf_l instead of producing NaN.
+//
+// The phases are ordered to keep the live register set at ~6 column arrays
+// (the arch-VGPR file is 256 x 32 bit per lane = 128 doubles): P is
+// broadcast twice (for WB, then for W) and B twice (for G, then for H)
+// rather than holding WA, WB, G, H and F at once.
+//
+// Register conventions inside a group (lane l, VL = 15):
+//   P[i]  : lane l < 12 -> P[i][l] (= P[l][i]); VL -> p[i]
+//   A_[i] : lane l < 12 -> A[i][l];             VL -> b[i]
+//   B_[i] : lane l < 12 -> B[i][l]              (VL: zeros)
+//   Rc[i] : R[i][l];  Sc[i]: S[i][l] (VL: r[i]);  Qc[i]: Q[i][l] (VL: q[i])
+#pragma once
+
+#include "qp_group.h"
+
+// Keeps the machine scheduler from hoisting one phase's broadcasts/loads into
+// the previous phase (which blows the 256-VGPR budget).
+#define SRBD_PHASE_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+namespace srbd {
+
+// C[:,l] = P M[:,l] (+ init): P symmetric & column-owned, M column-owned.
+template <typename T>
+__device__ __forceinline__ void sym_mul_col(const T (&P)[12], const T (&M)[12], T (&C)[12]) {
+  sfor<0, 12>([&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      C[I] = fmadd(bc<K>(P[I]), M[K], C[I]);
+    });
+  });
+}
+
+// C[i][l] += X[:,i]' Y[:,l] for i < 12 (X, Y column-owned)
+template <typename T>
+__device__ __forceinline__ void tmul_acc(const T (&X)[12], const T (&Y)[12], T (&C)[12]) {
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    sfor<0, 12>([&](auto kk) {
+      constexpr int K = decltype(kk)::value;
+      C[I] = fmadd(bc<I>(X[K]), Y[K], C[I]);
+    });
+  });
+}
+
+// Right-looking Cholesky of the column-owned symmetric G (lane l holds
+// G[:,l]); `reg` is added to each pivot.  On exit Lc holds column l of L
+// (rows > l meaningful) and rs = 1 / L[l][l] (0 for a non-positive pivot).
+template <typename T>
+__device__ __forceinline__ void chol_cols(T (&G)[12], const int lane, const T reg, T (&Lc)[12],
+                                          T& rs) {
+  T dmine = T(1);
+  sfor<0, 12>([&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    const T dk = bc<K>(G[K]) + reg;
+    const T inv = dk > T(0) ? T(1) / dk : T(0);
+    const T s = lane > K ? G[K] * inv : T(0);
+    sfor<K + 1, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      G[I] = fmadd(-bc<K>(G[I]), s, G[I]);
+    });
+    dmine = lane == K ? dk : dmine;
+  });
+  rs = dmine > T(0) ? T(1) / __builtin_sqrt(dmine) : T(0);
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    Lc[I] = G[I] * rs;
+  });
+}
+
+// H <- L^-1 H (column-owned right-hand sides), forward substitution.
+template <typename T>
+__device__ __forceinline__ void trsv_lower(const T (&Lc)[12], const T rs, T (&H)[12]) {
+  sfor<0, 12>([&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    const T y = H[K] * bc<K>(rs);
+    H[K] = y;
+    sfor<K + 1, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      H[I] = fmadd(-bc<K>(Lc[I]), y, H[I]);
+    });
+  });
+}
+
+// z = L^-T y (column-owned right-hand sides), dot-product back substitution.
+template <typename T>
+__device__ __forceinline__ void trsv_upper_t(const T (&Lc)[12], const T rs, const T (&y)[12],
+                                             T (&z)[12]) {
+  sfor_down<0, 12>([&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    T s = y[K];
+    sfor<K + 1, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      s = fmadd(-bc<K>(Lc[I]), z[I], s);
+    });
+    z[K] = s * bc<K>(rs);
+  });
+}
+
+template <typename T>
+struct StageFactor {
+  T F[12];   // on exit: P_k column (VL: p_k)
+  T H[12];   // on exit: Y = L^-1 H column (VL: y)
+  T Lc[12];  // L column (rows > l meaningful)
+  T rs;      // 1 / L[l][l]
+  T Kc[12];  // K column (VL: k)
+};
+
+// One backward Riccati step.  `P` holds P_{k+1} (VL: p_{k+1}) on entry.
+// A_ is overwritten with the closed-loop column Acl (VL: bcl) on exit.
+// The S/Q/R columns are fetched through the callables so that their loads
+// are issued late (short live ranges).
+template <typename T, typename LoadR, typename LoadSQ>
+__device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&B_)[12],
+                                             LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
+                                             const T reg, StageFactor<T>& o) {
+  const bool isv = lane == kVecLane;
+  // ---- G = R + B'(P B), L = chol(G)
+  {
+    T WB[12];
+    sfor<0, 12>([&](auto i) { WB[decltype(i)::value] = T(0); });
+    sym_mul_col(P, B_, WB);
+    SRBD_PHASE_FENCE();
+    T G[12];
+    loadR(G);
+    tmul_acc(B_, WB, G);
+    SRBD_PHASE_FENCE();
+    chol_cols(G, lane, reg, o.Lc, o.rs);
+  }
+  SRBD_PHASE_FENCE();
+  // ---- W = P [A | b] (+ p on VL); H = S + B'W; F = Q + A'W
+  {
+    T Pl[12], Bl[12];
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      Pl[I] = P[I];
+      Bl[I] = B_[I];
+    });
+    launder(Pl);
+    launder(Bl);
+    T W[12];
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      W[I] = isv ? Pl[I] : T(0);
+    });
+    sym_mul_col(Pl, A_, W);
+    SRBD_PHASE_FENCE();
+    loadSQ(o.H, o.F);
+    tmul_acc(Bl, W, o.H);
+    SRBD_PHASE_FENCE();
+    tmul_acc(A_, W, o.F);
+  }
+  SRBD_PHASE_FENCE();
+  // ---- Y = L^-1 H, K = -L^-T Y
+  trsv_lower(o.Lc, o.rs, o.H);
+  SRBD_PHASE_FENCE();
+  launder(o.Lc);
+  {
+    T z[12];
+    trsv_upper_t(o.Lc, o.rs, o.H, z);
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      o.Kc[I] = -z[I];
+    });
+  }
+  SRBD_PHASE_FENCE();
+  // ---- P_k = F - Y'Y (VL: p_k = f - Y'y)
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    sfor<0, 12>([&](auto kk) {
+      constexpr int K = decltype(kk)::value;
+      o.F[I] = fmadd(-bc<I>(o.H[K]), o.H[K], o.F[I]);
+    });
+  });
+  SRBD_PHASE_FENCE();
+  // ---- Acl = A + B K (VL: bcl = b + B k)
+  launder(B_);
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    sfor<0, 12>([&](auto m) {
+      constexpr int M = decltype(m)::value;
+      A_[I] = fmadd(bc<M>(B_[I]), o.Kc[M], A_[I]);
+    });
+  });
+}
+
+}  // namespace srbd

@@ -1,0 +1,223 @@
+// riccati_unconstr.hip -- batched unconstrained OCP-QP solve (nc == 0).
+//
+// Replaces, for a batch of QPs, HPIPM's nc == 0 branch of d_ocp_qp_ipm_solve:
+// one d_ocp_qp_fact_solve_kkt_unconstr (hpipm_d_ocp_qp_kkt.h:54) and
+// iter = 0 (pinned by hpipm-cpp/test/ocp_qp_ipm_solver.cpp:55-56), plus the
+// getters and stage-0 rebuild of hpipm-cpp/src/ocp_qp_ipm_solver.cpp:337-373.
+//
+// One kernel, two sweeps per QP group (see qp_group.h):
+//   backward k = N-1..0 : riccati_step on the stage's column-owned blocks,
+//                         then write the forward record {K, Acl, P, k, bcl, p}
+//                         (row-major, kernels.h) to the per-QP workspace;
+//   forward  k = 0..N   : row-owned u = K x + k, pi = P x + p,
+//                         x+ = Acl x + bcl, with x broadcast by DPP.
+// The forward sweep reads the records in LIFO order (stage 0 was written
+// last), so the most recent records are still in L2 / Infinity Cache.
+//
+// The stage-0 block is factorized in full with x_0 = x0 fixed, which gives
+// exactly the values of the reference's x0-eliminated solve + stage-0
+// rebuild (K0 = -G0^-1 H0, P0 = Q0 - H0'G0^-1 H0 + A0'P1 A0, ...).
+#include "kernels.h"
+#include "riccati.h"
+
+namespace srbd {
+
+namespace {
+
+// out[i] = v[i] for i < n (static register indices, predicated stores)
+__device__ __forceinline__ void store_n(double* out, int n, const double (&v)[12]) {
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    if (I < n) out[I] = v[I];
+  });
+}
+
+template <bool FULL>
+struct StageLoader {
+  int nx, nu;
+  // column `col` of an (rows x ncols) column-major block, zero-padded
+  __device__ __forceinline__ void col(const double* blk, int rows, int ld, int c, bool ok,
+                                      double (&v)[12]) const {
+    if constexpr (FULL) {
+      load12(blk + c * 12, v);
+    } else {
+      load_col_pad(blk + (size_t)c * ld, rows, ok, v);
+    }
+  }
+};
+
+template <bool FULL>
+__global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgs a) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int qp = gid >> 4;
+  const int lane = threadIdx.x & (kGroup - 1);
+  if (qp >= a.batch) return;
+  const int N = a.N;
+  const int nx = FULL ? 12 : a.nx;
+  const int nu = FULL ? 12 : a.nu;
+  const bool isv = lane == kVecLane;
+  const int col = lane < kMaxDim ? lane : kMaxDim - 1;
+  const double reg = a.reg;
+
+  const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu, nuu = (size_t)nu * nu;
+  const double* Aq = a.A + (size_t)qp * N * nxx;
+  const double* Bq = a.B + (size_t)qp * N * nxu;
+  const double* bq = a.b + (size_t)qp * N * nx;
+  const double* Qq = a.Q + (size_t)qp * (N + 1) * nxx;
+  const double* Sq = a.S + (size_t)qp * N * nxu;
+  const double* Rq = a.R + (size_t)qp * N * nuu;
+  const double* qq = a.q + (size_t)qp * (N + 1) * nx;
+  const double* rq = a.r + (size_t)qp * N * nu;
+  double* ws = a.ws + (size_t)qp * a.ws_qp;
+
+  StageLoader<FULL> ld{nx, nu};
+  const bool xcol = lane < nx;  // lane owns a real state column
+  const bool ucol = lane < nu;  // lane owns a real input column
+
+  // ---------------- terminal stage: P_N = Q_N, p_N = q_N ----------------
+  double P[12];
+  if (isv) {
+    ld.col(qq + (size_t)N * nx, nx, nx, 0, true, P);
+  } else {
+    ld.col(Qq + (size_t)N * nxx, nx, nx, col, xcol, P);
+  }
+  {
+    double* rec = ws + (size_t)N * kWsStage;
+    if (lane < kMaxDim) store12(rec + kWsP + lane * 12, P);
+    if (isv) store12(rec + kWsp, P);
+    if (a.P && xcol) store_n(a.P + ((size_t)qp * (N + 1) + N) * nxx + (size_t)lane * nx, nx, P);
+    if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + N) * nx, nx, P);
+  }
+
+  // ---------------- backward sweep ----------------
+#pragma unroll 1
+  for (int k = N - 1; k >= 0; --k) {
+    double A_[12], B_[12];
+    if (isv) {
+      ld.col(bq + (size_t)k * nx, nx, nx, 0, true, A_);
+      sfor<0, 12>([&](auto i) { B_[decltype(i)::value] = 0.0; });
+    } else {
+      ld.col(Aq + (size_t)k * nxx, nx, nx, col, xcol, A_);
+      ld.col(Bq + (size_t)k * nxu, nx, nx, col, ucol, B_);
+    }
+    auto loadR = [&](double (&Rc)[12]) {
+      if (isv) {
+        sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = 0.0; });
+      } else {
+        ld.col(Rq + (size_t)k * nuu, nu, nu, col, ucol, Rc);
+        if constexpr (!FULL) {
+          // padded inputs: R = 1 on the diagonal keeps G positive definite
+          sfor<0, 12>([&](auto i) {
+            constexpr int I = decltype(i)::value;
+            if (lane == I && lane >= nu) Rc[I] = 1.0;
+          });
+        }
+      }
+    };
+    auto loadSQ = [&](double (&Sc)[12], double (&Qc)[12]) {
+      if (isv) {
+        ld.col(rq + (size_t)k * nu, nu, nu, 0, true, Sc);
+        ld.col(qq + (size_t)k * nx, nx, nx, 0, true, Qc);
+      } else {
+        ld.col(Sq + (size_t)k * nxu, nu, nu, col, xcol, Sc);
+        ld.col(Qq + (size_t)k * nxx, nx, nx, col, xcol, Qc);
+      }
+    };
+    StageFactor<double> f;
+    riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
+
+    double* rec = ws + (size_t)k * kWsStage;
+    if (lane < kMaxDim) {
+      sfor<0, 12>([&](auto m) {
+        constexpr int M = decltype(m)::value;
+        rec[kWsK + M * 12 + lane] = f.Kc[M];
+        rec[kWsAcl + M * 12 + lane] = A_[M];
+      });
+      store12(rec + kWsP + lane * 12, f.F);
+    }
+    if (isv) {
+      store12(rec + kWsk, f.Kc);
+      store12(rec + kWsbcl, A_);
+      store12(rec + kWsp, f.F);
+    }
+    if (a.P && xcol) store_n(a.P + ((size_t)qp * (N + 1) + k) * nxx + (size_t)lane * nx, nx, f.F);
+    if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + k) * nx, nx, f.F);
+    if (a.K && xcol) store_n(a.K + ((size_t)qp * N + k) * nxu + (size_t)lane * nu, nu, f.Kc);
+    if (a.k && isv) store_n(a.k + ((size_t)qp * N + k) * nu, nu, f.Kc);
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      P[I] = f.F[I];
+    });
+  }
+
+  // ---------------- forward sweep (row-owned) ----------------
+  const int row = lane < kMaxDim ? lane : kMaxDim - 1;
+  double xv = (lane < nx) ? a.x0[(size_t)qp * nx + lane] : 0.0;
+  bool bad = false;
+  double* xo = a.x + (size_t)qp * (N + 1) * nx;
+  double* uo = a.u + (size_t)qp * N * nu;
+  double* po = a.pi + (size_t)qp * (N + 1) * nx;
+#pragma unroll 1
+  for (int k = 0; k <= N; ++k) {
+    const double* rec = ws + (size_t)k * kWsStage;
+    double Pr[12];
+    load12(rec + kWsP + row * 12, Pr);
+    const double pv = rec[kWsp + row];
+    double bx[12];
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      bx[J] = bc<J>(xv);
+    });
+    double pp = pv;
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      pp = fmadd(Pr[J], bx[J], pp);
+    });
+    if (lane < nx) {
+      xo[(size_t)k * nx + lane] = xv;
+      po[(size_t)k * nx + lane] = pp;
+    }
+    if (k == N) break;
+    double Kr[12], Ar[12];
+    load12(rec + kWsK + row * 12, Kr);
+    load12(rec + kWsAcl + row * 12, Ar);
+    double uu = rec[kWsk + row];
+    double xn = rec[kWsbcl + row];
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      uu = fmadd(Kr[J], bx[J], uu);
+      xn = fmadd(Ar[J], bx[J], xn);
+    });
+    if (lane < nu) uo[(size_t)k * nu + lane] = uu;
+    bad |= (lane < nu && !(uu == uu)) || (lane < nx && !(xn == xn));
+    xv = xn;
+  }
+  if (a.status || a.iter) {
+    const unsigned long long m = __ballot(bad);
+    const int shift = (threadIdx.x & 63) & ~(kGroup - 1);
+    const bool any_bad = ((m >> shift) & 0xffffull) != 0;
+    if (lane == 0) {
+      if (a.status) a.status[qp] = any_bad ? 3 : 0;
+      if (a.iter) a.iter[qp] = 0;
+    }
+  }
+}
+
+}  // namespace
+
+size_t ws_doubles_unconstr(int N) { return (size_t)(N + 1) * kWsStage; }
+
+hipError_t launch_riccati_unconstr(const ProblemArgs& a, hipStream_t stream) {
+  if (a.batch <= 0) return hipSuccess;
+  const int threads = 256;
+  const long long lanes = (long long)a.batch * kGroup;
+  const int blocks = (int)((lanes + threads - 1) / threads);
+  if (a.nx == 12 && a.nu == 12) {
+    hipLaunchKernelGGL(riccati_unconstr_kernel<true>, dim3(blocks), dim3(threads), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(riccati_unconstr_kernel<false>, dim3(blocks), dim3(threads), 0, stream, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace srbd

@@ -1,0 +1,355 @@
+// srbd_qp_capi.hip -- implementation of the C-ABI in include/srbd_qp.h.
+//
+// Host-side orchestration only: argument checks (the batched analogue of
+// OcpQpDim::checkSize, hpipm-cpp/src/ocp_qp_dim.cpp:59-246, and
+// OcpQpIpmSolverSettings::checkSettings, ocp_qp_ipm_solver_settings.cpp:7-38),
+// workspace ownership (what d_ocp_qp_ipm_ws_wrapper did,
+// src/detail/d_ocp_qp_ipm_ws_wrapper.cpp:141-155 -- sized once here instead of
+// on every solve() as the reference does at ocp_qp_ipm_solver.cpp:185), and
+// dispatch to the HIP kernels.  No CPU fallback exists: without a GPU every
+// solve returns SRBD_QP_EDEVICE.
+#include "../../include/srbd_qp.h"
+#include "kernels.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_last_error = "";
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+}  // namespace
+
+struct srbd_qp_handle_s {
+  srbd_qp_dims dims{};
+  int capacity = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  double* ws = nullptr;
+  size_t ws_qp = 0;  // doubles per QP
+  size_t ws_bytes = 0;
+  // host-solve staging (device)
+  double* stage = nullptr;
+  size_t stage_bytes = 0;
+};
+
+extern "C" {
+
+int srbd_qp_abi_version(void) { return SRBD_QP_ABI_VERSION; }
+
+const char* srbd_qp_last_error(void) { return g_last_error.c_str(); }
+
+const char* srbd_qp_status_string(int s) {
+  switch (s) {
+    case SRBD_QP_SUCCESS: return "HpipmStatus::Success";
+    case SRBD_QP_MAX_ITER: return "HpipmStatus::MaxIterReached";
+    case SRBD_QP_MIN_STEP: return "HpipmStatus::MinStepLengthReached";
+    case SRBD_QP_NAN_SOL: return "HpipmStatus::NaNDetected";
+    default: return "HpipmStatus::UnknownFailure";
+  }
+}
+
+const char* srbd_qp_error_string(int e) {
+  switch (e) {
+    case SRBD_QP_OK: return "ok";
+    case SRBD_QP_EINVAL: return "invalid argument";
+    case SRBD_QP_EDIM: return "unsupported dimensions";
+    case SRBD_QP_ENOMEM: return "device out of memory";
+    case SRBD_QP_EDEVICE: return "HIP device error";
+    case SRBD_QP_ECAPACITY: return "batch exceeds handle capacity";
+    case SRBD_QP_ESETTINGS: return "invalid settings";
+    default: return "unknown error";
+  }
+}
+
+void srbd_qp_default_settings(srbd_qp_settings* s) {
+  if (!s) return;
+  // hpipm-cpp/include/hpipm-cpp/ocp_qp_ipm_solver_settings.hpp:26-86
+  s->mode = SRBD_QP_MODE_SPEED;
+  s->iter_max = 15;
+  s->alpha_min = 1.0e-08;
+  s->mu0 = 1.0e+02;
+  s->tol_stat = 1.0e-08;
+  s->tol_eq = 1.0e-08;
+  s->tol_ineq = 1.0e-08;
+  s->tol_comp = 1.0e-08;
+  s->reg_prim = 1.0e-12;
+  s->warm_start = 0;
+  s->pred_corr = 1;
+  s->ric_alg = 1;
+  s->split_step = 0;
+  s->compute_residuals = 0;
+}
+
+int srbd_qp_check_settings(const srbd_qp_settings* s) {
+  if (!s) return fail(SRBD_QP_EINVAL, "settings is NULL");
+  // messages of OcpQpIpmSolverSettings::checkSettings (settings.cpp:7-38)
+  if (s->iter_max < 0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.iter_max must be non-negative");
+  if (s->alpha_min <= 0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.alpha_min must be positive");
+  if (s->alpha_min > 1.0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.alpha_min must be less than 1.0");
+  if (s->mu0 <= 0.0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.mu0 must be positive");
+  if (s->tol_stat <= 0.0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.tol_stat must be positive");
+  if (s->tol_eq <= 0.0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.tol_eq must be positive");
+  if (s->tol_ineq <= 0.0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.tol_ineq must be positive");
+  if (s->tol_comp <= 0.0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.tol_comp must be positive");
+  if (s->reg_prim < 0.0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.reg_prim must be non-negative");
+  return SRBD_QP_OK;
+}
+
+static int check_dims(const srbd_qp_dims* d) {
+  if (!d) return fail(SRBD_QP_EINVAL, "dims is NULL");
+  if (d->N < 1 || d->N > 1024)
+    return fail(SRBD_QP_EDIM, "N must be in [1, 1024], got " + std::to_string(d->N));
+  if (d->nx < 1 || d->nx > SRBD_QP_MAX_NX)
+    return fail(SRBD_QP_EDIM, "nx must be in [1, 12], got " + std::to_string(d->nx));
+  if (d->nu < 1 || d->nu > SRBD_QP_MAX_NU)
+    return fail(SRBD_QP_EDIM, "nu must be in [1, 12], got " + std::to_string(d->nu));
+  if (d->ng < 0 || d->ng > SRBD_QP_MAX_NG)
+    return fail(SRBD_QP_EDIM, "ng must be in [0, 64], got " + std::to_string(d->ng));
+  return SRBD_QP_OK;
+}
+
+static bool constrained(const srbd_qp_dims& d) { return d.has_box_u || d.has_box_x || d.ng > 0; }
+
+static size_t ws_doubles_per_qp(const srbd_qp_dims& d) {
+  return srbd::ws_doubles_unconstr(d.N);
+}
+
+int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srbd_qp_handle* out) {
+  if (!out) return fail(SRBD_QP_EINVAL, "out handle pointer is NULL");
+  *out = nullptr;
+  int rc = check_dims(dims);
+  if (rc) return rc;
+  if (batch_capacity < 1) return fail(SRBD_QP_EINVAL, "batch_capacity must be >= 1");
+  if (constrained(*dims))
+    return fail(SRBD_QP_EDIM, "inequality-constrained QPs are not supported by this build yet");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(SRBD_QP_EDEVICE, "no HIP device available (libsrbd_qp has no CPU fallback)");
+  if (device < 0 || device >= ndev)
+    return fail(SRBD_QP_EDEVICE, "device index " + std::to_string(device) + " out of range");
+  int prev = 0;
+  hipGetDevice(&prev);
+  if (hipSetDevice(device) != hipSuccess) return fail(SRBD_QP_EDEVICE, "hipSetDevice failed");
+  auto* h = new srbd_qp_handle_s();
+  h->dims = *dims;
+  h->capacity = batch_capacity;
+  h->device = device;
+  h->ws_qp = ws_doubles_per_qp(*dims);
+  h->ws_bytes = h->ws_qp * sizeof(double) * (size_t)batch_capacity;
+  hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&h->ws), h->ws_bytes);
+  hipSetDevice(prev);
+  if (e != hipSuccess) {
+    srbd_qp_destroy(h);
+    return fail(e == hipErrorOutOfMemory ? SRBD_QP_ENOMEM : SRBD_QP_EDEVICE,
+                std::string("workspace allocation failed: ") + hipGetErrorString(e));
+  }
+  *out = h;
+  return SRBD_QP_OK;
+}
+
+void srbd_qp_destroy(srbd_qp_handle h) {
+  if (!h) return;
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->ws) hipFree(h->ws);
+  if (h->stage) hipFree(h->stage);
+  if (h->stream) hipStreamDestroy(h->stream);
+  hipSetDevice(prev);
+  delete h;
+}
+
+void* srbd_qp_stream(srbd_qp_handle h) { return h ? reinterpret_cast<void*>(h->stream) : nullptr; }
+
+size_t srbd_qp_workspace_bytes(srbd_qp_handle h) { return h ? h->ws_bytes : 0; }
+
+int srbd_qp_synchronize(srbd_qp_handle h) {
+  if (!h) return fail(SRBD_QP_EINVAL, "handle is NULL");
+  hipError_t e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("stream sync: ") + hipGetErrorString(e));
+  return SRBD_QP_OK;
+}
+
+static int validate_call(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                         const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s) {
+  if (!h) return fail(SRBD_QP_EINVAL, "handle is NULL");
+  if (!d || !s) return fail(SRBD_QP_EINVAL, "data/solution is NULL");
+  if (batch < 0) return fail(SRBD_QP_EINVAL, "batch must be >= 0");
+  if (batch > h->capacity)
+    return fail(SRBD_QP_ECAPACITY, "batch " + std::to_string(batch) + " exceeds capacity " +
+                                       std::to_string(h->capacity));
+  int rc = srbd_qp_check_settings(st);
+  if (rc) return rc;
+  if (!d->A || !d->B || !d->b || !d->Q || !d->S || !d->R || !d->q || !d->r || !d->x0)
+    return fail(SRBD_QP_EINVAL, "A, B, b, Q, S, R, q, r and x0 are required");
+  if (!s->x || !s->u || !s->pi) return fail(SRBD_QP_EINVAL, "x, u and pi outputs are required");
+  const srbd_qp_dims& dm = h->dims;
+  if ((d->lbu != nullptr) != (dm.has_box_u != 0) || (d->lbx != nullptr) != (dm.has_box_x != 0))
+    return fail(SRBD_QP_EINVAL, "box-constraint pointers do not match the handle's dims");
+  return SRBD_QP_OK;
+}
+
+int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                      const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s, void* stream) {
+  int rc = validate_call(h, batch, st, d, s);
+  if (rc) return rc;
+  if (batch == 0) return SRBD_QP_OK;
+  hipStream_t strm = stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipSetDevice(h->device);
+  srbd::ProblemArgs a{};
+  a.batch = batch;
+  a.N = h->dims.N;
+  a.nx = h->dims.nx;
+  a.nu = h->dims.nu;
+  a.ng = h->dims.ng;
+  a.A = d->A; a.B = d->B; a.b = d->b; a.Q = d->Q; a.S = d->S; a.R = d->R; a.q = d->q; a.r = d->r;
+  a.x0 = d->x0;
+  a.lbu = d->lbu; a.ubu = d->ubu; a.lbu_mask = d->lbu_mask; a.ubu_mask = d->ubu_mask;
+  a.lbx = d->lbx; a.ubx = d->ubx; a.lbx_mask = d->lbx_mask; a.ubx_mask = d->ubx_mask;
+  a.C = d->C; a.D = d->D; a.lg = d->lg; a.ug = d->ug; a.lg_mask = d->lg_mask; a.ug_mask = d->ug_mask;
+  a.x = s->x; a.u = s->u; a.pi = s->pi;
+  a.P = s->P; a.p = s->p; a.K = s->K; a.k = s->k;
+  a.status = s->status; a.iter = s->iter; a.res = s->res; a.obj = s->obj;
+  a.ws = h->ws;
+  a.ws_qp = h->ws_qp;
+  a.reg = st->reg_prim;
+  hipError_t e = srbd::launch_riccati_unconstr(a, strm);
+  if (e == hipSuccess && (s->res || s->obj)) {
+    // residuals of an unconstrained solve are not computed by this build:
+    // report zeros only when asked not to compute them.
+    if (s->res) e = hipMemsetAsync(s->res, 0, sizeof(double) * 4 * (size_t)batch, strm);
+    if (e == hipSuccess && s->obj) e = hipMemsetAsync(s->obj, 0, sizeof(double) * (size_t)batch, strm);
+  }
+  hipSetDevice(prev);
+  if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
+  return SRBD_QP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// host-buffer convenience path
+// ---------------------------------------------------------------------------
+namespace {
+struct Field {
+  const void* host;
+  size_t bytes;
+  size_t off;
+};
+}  // namespace
+
+int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                           const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s) {
+  int rc = validate_call(h, batch, st, d, s);
+  if (rc) return rc;
+  if (batch == 0) return SRBD_QP_OK;
+  const srbd_qp_dims& m = h->dims;
+  const size_t B = (size_t)batch, N = (size_t)m.N, nx = (size_t)m.nx, nu = (size_t)m.nu,
+               ng = (size_t)m.ng;
+  const size_t D = sizeof(double);
+  // input fields
+  std::vector<Field> in;
+  size_t off = 0;
+  auto add = [&](const double* p, size_t n) -> size_t {
+    if (!p) return (size_t)-1;
+    size_t o = off;
+    in.push_back({p, n * D, o});
+    off += ((n * D + 255) / 256) * 256;
+    return o;
+  };
+  size_t oA = add(d->A, B * N * nx * nx), oB = add(d->B, B * N * nx * nu), ob = add(d->b, B * N * nx);
+  size_t oQ = add(d->Q, B * (N + 1) * nx * nx), oS = add(d->S, B * N * nu * nx),
+         oR = add(d->R, B * N * nu * nu);
+  size_t oq = add(d->q, B * (N + 1) * nx), orr = add(d->r, B * N * nu), ox0 = add(d->x0, B * nx);
+  size_t olbu = add(d->lbu, B * N * nu), oubu = add(d->ubu, B * N * nu),
+         olbum = add(d->lbu_mask, B * N * nu), oubum = add(d->ubu_mask, B * N * nu);
+  size_t olbx = add(d->lbx, B * (N + 1) * nx), oubx = add(d->ubx, B * (N + 1) * nx),
+         olbxm = add(d->lbx_mask, B * (N + 1) * nx), oubxm = add(d->ubx_mask, B * (N + 1) * nx);
+  size_t oC = add(d->C, B * (N + 1) * ng * nx), oD = add(d->D, B * N * ng * nu),
+         olg = add(d->lg, B * (N + 1) * ng), oug = add(d->ug, B * (N + 1) * ng),
+         olgm = add(d->lg_mask, B * (N + 1) * ng), ougm = add(d->ug_mask, B * (N + 1) * ng);
+  // outputs
+  struct OutF {
+    void* host;
+    size_t bytes;
+    size_t off;
+  };
+  std::vector<OutF> outs;
+  auto addo = [&](void* p, size_t bytes) -> size_t {
+    if (!p) return (size_t)-1;
+    size_t o = off;
+    outs.push_back({p, bytes, o});
+    off += ((bytes + 255) / 256) * 256;
+    return o;
+  };
+  size_t ox = addo(s->x, B * (N + 1) * nx * D), ou = addo(s->u, B * N * nu * D),
+         opi = addo(s->pi, B * (N + 1) * nx * D);
+  size_t oP = addo(s->P, B * (N + 1) * nx * nx * D), op = addo(s->p, B * (N + 1) * nx * D),
+         oK = addo(s->K, B * N * nu * nx * D), ok = addo(s->k, B * N * nu * D);
+  size_t ost = addo(s->status, B * sizeof(int)), oit = addo(s->iter, B * sizeof(int));
+  size_t ores = addo(s->res, B * 4 * D), oobj = addo(s->obj, B * D);
+
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipSetDevice(h->device);
+  hipError_t e = hipSuccess;
+  if (off > h->stage_bytes) {
+    if (h->stage) hipFree(h->stage);
+    h->stage = nullptr;
+    h->stage_bytes = 0;
+    e = hipMalloc(reinterpret_cast<void**>(&h->stage), off);
+    if (e == hipSuccess) h->stage_bytes = off;
+  }
+  char* base = reinterpret_cast<char*>(h->stage);
+  for (size_t i = 0; e == hipSuccess && i < in.size(); ++i)
+    e = hipMemcpyAsync(base + in[i].off, in[i].host, in[i].bytes, hipMemcpyHostToDevice, h->stream);
+  // warm start: x/u outputs are inputs too
+  if (e == hipSuccess && st->warm_start) {
+    e = hipMemcpyAsync(base + ox, s->x, B * (N + 1) * nx * D, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(base + ou, s->u, B * N * nu * D, hipMemcpyHostToDevice, h->stream);
+  }
+  if (e != hipSuccess) {
+    hipSetDevice(prev);
+    return fail(SRBD_QP_EDEVICE, std::string("host->device copy: ") + hipGetErrorString(e));
+  }
+  auto dp = [&](size_t o) -> double* {
+    return o == (size_t)-1 ? nullptr : reinterpret_cast<double*>(base + o);
+  };
+  auto ip = [&](size_t o) -> int* { return o == (size_t)-1 ? nullptr : reinterpret_cast<int*>(base + o); };
+  srbd_qp_data_f64 dd{};
+  dd.A = dp(oA); dd.B = dp(oB); dd.b = dp(ob); dd.Q = dp(oQ); dd.S = dp(oS); dd.R = dp(oR);
+  dd.q = dp(oq); dd.r = dp(orr); dd.x0 = dp(ox0);
+  dd.lbu = dp(olbu); dd.ubu = dp(oubu); dd.lbu_mask = dp(olbum); dd.ubu_mask = dp(oubum);
+  dd.lbx = dp(olbx); dd.ubx = dp(oubx); dd.lbx_mask = dp(olbxm); dd.ubx_mask = dp(oubxm);
+  dd.C = dp(oC); dd.D = dp(oD); dd.lg = dp(olg); dd.ug = dp(oug); dd.lg_mask = dp(olgm);
+  dd.ug_mask = dp(ougm);
+  srbd_qp_solution_f64 ss{};
+  ss.x = dp(ox); ss.u = dp(ou); ss.pi = dp(opi); ss.P = dp(oP); ss.p = dp(op); ss.K = dp(oK);
+  ss.k = dp(ok); ss.status = ip(ost); ss.iter = ip(oit); ss.res = dp(ores); ss.obj = dp(oobj);
+  hipSetDevice(prev);
+  rc = srbd_qp_solve_f64(h, batch, st, &dd, &ss, nullptr);
+  if (rc) return rc;
+  hipSetDevice(h->device);
+  for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)
+    e = hipMemcpyAsync(outs[i].host, base + outs[i].off, outs[i].bytes, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  hipSetDevice(prev);
+  if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("device->host copy: ") + hipGetErrorString(e));
+  return SRBD_QP_OK;
+}
+
+}  // extern "C"
