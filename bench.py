@@ -261,8 +261,11 @@ def cpu_baseline(pkg, qp, x0, settings, budget_s):
     cores over a bounded sample of the same workload."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle  # test infrastructure, used here only as the CPU baseline
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = max(1, min(threads, 256))
+    # the GPU box's CPU share is OMP_NUM_THREADS (16 per GPU there); nproc shows
+    # the whole machine
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
+    threads = max(1, min(threads, avail, 64))
     cal = qp.subset(slice(0, min(qp.batch, 4 * threads)))
     _, dt = oracle.solve_batch_threaded(cal, settings, x0[:cal.batch], threads)
     rate = cal.batch / max(dt, 1e-9)

@@ -16,7 +16,7 @@ timeout -k 10 600 python bench.py $BENCH_ARGS > gpurun_out/bench_${TAG}.json 2> 
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_${TAG}.json; tail -3 gpurun_out/bench_${TAG}.log
 [ $rc -eq 0 ] || exit $rc
 if [ -z "$NO_PROF" ]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline $PROF_ARGS > gpurun_out/prof_${TAG}.log 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline $PROF_ARGS > gpurun_out/prof_${TAG}.log 2>&1
   rc=$?; echo "rocprof rc=$rc"
   find gpurun_out/prof_${TAG} -name "*stats*" | head
 fi

@@ -1,0 +1,941 @@
+// ipm_box.hip -- batched box-constrained OCP-QP interior-point solve.
+//
+// Replaces, for a batch of QPs, HPIPM's d_ocp_qp_ipm_solve (hpipm_d_ocp_qp_ipm.h:238)
+// in its relative formulation: Mehrotra predictor-corrector with the
+// residuals of hpipm_d_ocp_qp_res.h:57-67 and the core ops of
+// hpipm_d_core_qp_ipm_aux.h:44-62 (Gamma/gamma, alpha, mu_aff, centering
+// correction, update), the KKT factorization of d_ocp_qp_fact_solve_kkt_step
+// (hpipm_d_ocp_qp_kkt.h:56) and the corrector solve d_ocp_qp_solve_kkt_step
+// (:60).  The arithmetic is restated in oracle/ocp_qp_oracle.c (ipm loop), the
+// parity reference.
+//
+// One 16-lane group per QP runs the whole IPM; a wavefront advances four QPs
+// and idles groups that have exited.  Each iteration is six sweeps over the
+// horizon (k = stage):
+//   RU  k = 0..N  apply the previous step, residuals res_g / res_b / res_d /
+//                 res_m at the new iterate (element-owned), norms, mu, obj
+//   B1  k = N..0  Gamma / gamma (predictor), factorize the barrier-augmented
+//                 KKT system with riccati_step (column-owned), write the stage
+//                 record {L, K, Acl, P, 1/diag L, k, bcl, p}
+//   F1  k = 0..N  predictor step (row-owned from the record), dt / dlam,
+//                 alpha_aff
+//   M   k = 0..N  mu_aff -> sigma = (mu_aff / mu)^3
+//   B2  k = N..0  corrector right-hand side, vector-only Riccati recursion
+//                 reusing the record (element-owned)
+//   F2  k = 0..N  corrector step, dt / dlam, alpha_prim / alpha_dual
+// Box bounds are dense per variable (include/srbd_qp.h), so bound i of u_k /
+// x_k lives on lane i next to u_k[i] / x_k[i]: every constraint operation is
+// lane-local and the barrier Hessian only touches the diagonals of R and Q.
+#include "kernels.h"
+#include "riccati.h"
+
+namespace srbd {
+
+namespace {
+
+constexpr double kThr0 = 0.1;     // minimum initial slack (HPIPM init_var)
+constexpr double kStepTau = 0.995;  // fraction to the boundary
+
+__device__ __forceinline__ double gsum(double v) {
+  v += __shfl_xor(v, 8, kGroup);
+  v += __shfl_xor(v, 4, kGroup);
+  v += __shfl_xor(v, 2, kGroup);
+  v += __shfl_xor(v, 1, kGroup);
+  return v;
+}
+__device__ __forceinline__ double gmax(double v) {
+  v = fmax(v, __shfl_xor(v, 8, kGroup));
+  v = fmax(v, __shfl_xor(v, 4, kGroup));
+  v = fmax(v, __shfl_xor(v, 2, kGroup));
+  v = fmax(v, __shfl_xor(v, 1, kGroup));
+  return v;
+}
+__device__ __forceinline__ double gmin(double v) {
+  v = fmin(v, __shfl_xor(v, 8, kGroup));
+  v = fmin(v, __shfl_xor(v, 4, kGroup));
+  v = fmin(v, __shfl_xor(v, 2, kGroup));
+  v = fmin(v, __shfl_xor(v, 1, kGroup));
+  return v;
+}
+// |v| propagating NaN (max with NaN would drop it)
+__device__ __forceinline__ double nabs(double v) { return v == v ? fabs(v) : __builtin_inf(); }
+
+// One inequality side on one variable (box bound, dense per variable).
+struct Side {
+  double lb, ub;   // bounds
+  double ml, mu;   // 1 if the lower / upper bound is active, else 0
+};
+
+template <bool FULL>
+struct Ctx {
+  int N, nx, nu, lane;
+  bool isv;
+  const double *A, *B, *b, *Q, *S, *R, *q, *r, *x0;
+  const double *lbu, *ubu, *lbum, *ubum, *lbx, *ubx, *lbxm, *ubxm;
+  double *x, *u, *pi;
+  double* ws;
+
+  __device__ size_t nxx() const { return FULL ? 144 : (size_t)nx * nx; }
+  __device__ size_t nxu() const { return FULL ? 144 : (size_t)nx * nu; }
+  __device__ size_t nuu() const { return FULL ? 144 : (size_t)nu * nu; }
+  __device__ double* st(int k) const { return ws + (size_t)k * kIpmStage; }
+
+  // ---- column-owned loads (lane = column), zero padded ----
+  __device__ void col(const double* blk, int rows, int c, bool ok, double (&v)[12]) const {
+    if constexpr (FULL) {
+      load12(blk + c * 12, v);
+    } else {
+      load_col_pad(blk + (size_t)c * rows, rows, ok, v);
+    }
+  }
+  // ---- row-owned loads (lane = row) of a column-major (rows x cols) block ----
+  __device__ void row(const double* blk, int rows, int cols, int rw, bool ok, double (&v)[12]) const {
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      if constexpr (FULL) {
+        v[J] = blk[rw + J * 12];
+      } else {
+        v[J] = (ok && J < cols) ? blk[(size_t)rw + (size_t)J * rows] : 0.0;
+      }
+    });
+  }
+  // element i of a length-n vector (0 beyond n)
+  __device__ double el(const double* v, int n, int i) const {
+    if constexpr (FULL) {
+      return i < 12 ? v[i] : 0.0;
+    } else {
+      return i < n ? v[i] : 0.0;
+    }
+  }
+  __device__ Side side_u(int k, int i) const {
+    Side s{0.0, 0.0, 0.0, 0.0};
+    if (lbu && i < nu && k < N) {
+      const size_t o = (size_t)k * nu + i;
+      s.lb = lbu[o];
+      s.ub = ubu[o];
+      s.ml = lbum ? (lbum[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+      s.mu = ubum ? (ubum[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+    }
+    return s;
+  }
+  __device__ Side side_x(int k, int i) const {
+    Side s{0.0, 0.0, 0.0, 0.0};
+    if (lbx && i < nx && k > 0) {  // stage-0 x bounds dropped (x0 embedding)
+      const size_t o = (size_t)k * nx + i;
+      s.lb = lbx[o];
+      s.ub = ubx[o];
+      s.ml = lbxm ? (lbxm[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+      s.mu = ubxm ? (ubxm[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+    }
+    return s;
+  }
+};
+
+// barrier state of one variable: lam_l, lam_u, t_l, t_u
+struct Bar {
+  double ll, lu, tl, tu;
+};
+__device__ __forceinline__ Bar load_bar(const double* stk, int which, int i) {
+  const double* p = stk + kStLam + which * 48;
+  return Bar{p[i], p[12 + i], p[24 + i], p[36 + i]};
+}
+__device__ __forceinline__ void store_bar(double* stk, int which, int i, const Bar& b) {
+  double* p = stk + kStLam + which * 48;
+  p[i] = b.ll;
+  p[12 + i] = b.lu;
+  p[24 + i] = b.tl;
+  p[36 + i] = b.tu;
+}
+// step of one variable's barrier pair: dt_l, dt_u, dlam_l, dlam_u
+struct BarStep {
+  double dtl, dtu, dll, dlu;
+};
+__device__ __forceinline__ BarStep load_bstep(const double* stk, int which, int i) {
+  const double* p = stk + kStDlt + which * 48;
+  return BarStep{p[i], p[12 + i], p[24 + i], p[36 + i]};
+}
+__device__ __forceinline__ void store_bstep(double* stk, int which, int i, const BarStep& d) {
+  double* p = stk + kStDlt + which * 48;
+  p[i] = d.dtl;
+  p[12 + i] = d.dtu;
+  p[24 + i] = d.dll;
+  p[36 + i] = d.dlu;
+}
+
+// Gamma (Hessian add) and gamma (gradient add) of one variable:
+// Gamma = lam_l/t_l + lam_u/t_u,
+// gamma = (rm_l + lam_l rd_l)/t_l - (rm_u + lam_u rd_u)/t_u, with
+// rm = lam t + extra - sigma_mu (extra = dlam_aff dt_aff in the corrector).
+__device__ __forceinline__ void gamma_of(const Side& s, const Bar& b, double v, double ext_l,
+                                         double ext_u, double smu, double& G, double& g) {
+  G = 0.0;
+  g = 0.0;
+  if (s.ml != 0.0) {
+    const double rd = v - s.lb - b.tl;
+    const double rm = b.ll * b.tl + ext_l - smu;
+    G += b.ll / b.tl;
+    g += (rm + b.ll * rd) / b.tl;
+  }
+  if (s.mu != 0.0) {
+    const double rd = s.ub - v - b.tu;
+    const double rm = b.lu * b.tu + ext_u - smu;
+    G += b.lu / b.tu;
+    g -= (rm + b.lu * rd) / b.tu;
+  }
+}
+
+// dt / dlam of one variable given its primal step dv.
+__device__ __forceinline__ BarStep bar_step(const Side& s, const Bar& b, double v, double dv,
+                                            double ext_l, double ext_u, double smu) {
+  BarStep d{0.0, 0.0, 0.0, 0.0};
+  if (s.ml != 0.0) {
+    const double rd = v - s.lb - b.tl;
+    d.dtl = rd + dv;
+    d.dll = -(b.ll * b.tl + ext_l - smu + b.ll * d.dtl) / b.tl;
+  }
+  if (s.mu != 0.0) {
+    const double rd = s.ub - v - b.tu;
+    d.dtu = rd - dv;
+    d.dlu = -(b.lu * b.tu + ext_u - smu + b.lu * d.dtu) / b.tu;
+  }
+  return d;
+}
+
+__device__ __forceinline__ void ratio(const Side& s, const Bar& b, const BarStep& d, double& ap,
+                                      double& ad) {
+  if (s.ml != 0.0) {
+    if (d.dtl < 0.0) ap = fmin(ap, -b.tl / d.dtl);
+    if (d.dll < 0.0) ad = fmin(ad, -b.ll / d.dll);
+  }
+  if (s.mu != 0.0) {
+    if (d.dtu < 0.0) ap = fmin(ap, -b.tu / d.dtu);
+    if (d.dlu < 0.0) ad = fmin(ad, -b.lu / d.dlu);
+  }
+}
+
+// gather an element-owned value (lane i < 12 holds v_i) into VL's registers
+__device__ __forceinline__ void gather12(double v, double (&out)[12]) {
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    out[I] = bc<I>(v);
+  });
+}
+
+template <bool FULL>
+__global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int qp = gid >> 4;
+  const int lane = threadIdx.x & (kGroup - 1);
+  if (qp >= a.batch) return;
+  const int N = a.N;
+  const int nx = FULL ? 12 : a.nx;
+  const int nu = FULL ? 12 : a.nu;
+  const int col = lane < kMaxDim ? lane : kMaxDim - 1;
+  const int li = lane < kMaxDim ? lane : 0;  // element index used for addressing
+  const bool xel = lane < nx, uel = lane < nu;
+
+  Ctx<FULL> c;
+  c.N = N;
+  c.nx = nx;
+  c.nu = nu;
+  c.lane = lane;
+  c.isv = lane == kVecLane;
+  {
+    const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu, nuu = (size_t)nu * nu;
+    c.A = a.A + (size_t)qp * N * nxx;
+    c.B = a.B + (size_t)qp * N * nxu;
+    c.b = a.b + (size_t)qp * N * nx;
+    c.Q = a.Q + (size_t)qp * (N + 1) * nxx;
+    c.S = a.S + (size_t)qp * N * nxu;
+    c.R = a.R + (size_t)qp * N * nuu;
+    c.q = a.q + (size_t)qp * (N + 1) * nx;
+    c.r = a.r + (size_t)qp * N * nu;
+    c.x0 = a.x0 + (size_t)qp * nx;
+    const size_t su = (size_t)qp * N * nu, sx = (size_t)qp * (N + 1) * nx;
+    c.lbu = a.lbu ? a.lbu + su : nullptr;
+    c.ubu = a.ubu ? a.ubu + su : nullptr;
+    c.lbum = a.lbu_mask ? a.lbu_mask + su : nullptr;
+    c.ubum = a.ubu_mask ? a.ubu_mask + su : nullptr;
+    c.lbx = a.lbx ? a.lbx + sx : nullptr;
+    c.ubx = a.ubx ? a.ubx + sx : nullptr;
+    c.lbxm = a.lbx_mask ? a.lbx_mask + sx : nullptr;
+    c.ubxm = a.ubx_mask ? a.ubx_mask + sx : nullptr;
+    c.x = a.x + sx;
+    c.u = a.u + su;
+    c.pi = a.pi + sx;
+    c.ws = a.ws + (size_t)qp * a.ws_qp;
+  }
+  const double reg = a.reg;
+
+  // =================== init (var_init_scheme 0, relative form) ===================
+  double ncl = 0.0;
+  for (int k = 0; k <= N; ++k) {
+    double* stk = c.st(k);
+    // u_k
+    if (k < N) {
+      double v = (a.warm_start && uel) ? c.u[(size_t)k * nu + li] : 0.0;
+      const Side s = c.side_u(k, lane);
+      Bar bb{0.0, 0.0, 1.0, 1.0};
+      if (s.ml != 0.0 || s.mu != 0.0) {
+        double tl = v - s.lb, tu = s.ub - v;
+        if (s.ml != 0.0 && s.mu != 0.0) {
+          if (tl < kThr0) {
+            if (tu < kThr0) {
+              v = 0.5 * (s.lb + s.ub);
+              tl = tu = kThr0;
+            } else {
+              tl = kThr0;
+              v = s.lb + kThr0;
+              tu = s.ub - v;
+            }
+          } else if (tu < kThr0) {
+            tu = kThr0;
+            v = s.ub - kThr0;
+            tl = v - s.lb;
+          }
+        } else if (s.ml != 0.0) {
+          if (tl < kThr0) {
+            tl = kThr0;
+            v = s.lb + kThr0;
+          }
+        } else if (tu < kThr0) {
+          tu = kThr0;
+          v = s.ub - kThr0;
+        }
+        bb.tl = s.ml != 0.0 ? tl : 1.0;
+        bb.tu = s.mu != 0.0 ? tu : 1.0;
+        bb.ll = s.ml != 0.0 ? a.mu0 / tl : 0.0;
+        bb.lu = s.mu != 0.0 ? a.mu0 / tu : 0.0;
+      }
+      ncl += s.ml + s.mu;
+      if (lane < kMaxDim) store_bar(stk, 0, lane, bb);
+      if (uel) c.u[(size_t)k * nu + lane] = v;
+    }
+    // x_k
+    {
+      double v;
+      if (k == 0) {
+        v = xel ? c.x0[li] : 0.0;
+      } else {
+        v = (a.warm_start && xel) ? c.x[(size_t)k * nx + li] : 0.0;
+      }
+      const Side s = c.side_x(k, lane);
+      Bar bb{0.0, 0.0, 1.0, 1.0};
+      if (s.ml != 0.0 || s.mu != 0.0) {
+        double tl = v - s.lb, tu = s.ub - v;
+        if (s.ml != 0.0 && s.mu != 0.0) {
+          if (tl < kThr0) {
+            if (tu < kThr0) {
+              v = 0.5 * (s.lb + s.ub);
+              tl = tu = kThr0;
+            } else {
+              tl = kThr0;
+              v = s.lb + kThr0;
+              tu = s.ub - v;
+            }
+          } else if (tu < kThr0) {
+            tu = kThr0;
+            v = s.ub - kThr0;
+            tl = v - s.lb;
+          }
+        } else if (s.ml != 0.0) {
+          if (tl < kThr0) {
+            tl = kThr0;
+            v = s.lb + kThr0;
+          }
+        } else if (tu < kThr0) {
+          tu = kThr0;
+          v = s.ub - kThr0;
+        }
+        bb.tl = s.ml != 0.0 ? tl : 1.0;
+        bb.tu = s.mu != 0.0 ? tu : 1.0;
+        bb.ll = s.ml != 0.0 ? a.mu0 / tl : 0.0;
+        bb.lu = s.mu != 0.0 ? a.mu0 / tu : 0.0;
+      }
+      ncl += s.ml + s.mu;
+      if (lane < kMaxDim) store_bar(stk, 1, lane, bb);
+      if (xel) {
+        c.x[(size_t)k * nx + lane] = v;
+        c.pi[(size_t)k * nx + lane] = 0.0;
+      }
+    }
+    if (lane < kMaxDim) {
+      // zero step: the first RU pass applies nothing
+      stk[kStStep + lane] = 0.0;
+      stk[kStStep + 12 + lane] = 0.0;
+      stk[kStStep + 24 + lane] = 0.0;
+      store_bstep(stk, 0, lane, BarStep{0, 0, 0, 0});
+      store_bstep(stk, 1, lane, BarStep{0, 0, 0, 0});
+    }
+  }
+  const double nc = gsum(lane < kMaxDim ? ncl : 0.0);
+  const double nc_inv = nc > 0.0 ? 1.0 / nc : 0.0;
+
+  double alpha_p = 0.0, alpha_d = 0.0;  // step applied by the next RU pass
+  double res_stat = 0.0, res_eq = 0.0, res_ineq = 0.0, res_comp = 0.0, obj = 0.0, mu = 0.0;
+  int iter = 0, status = -1;
+  double last_amin = 1.0;
+
+  for (;;) {
+    // =================== RU: update + residuals ===================
+    double mg = 0.0, mb = 0.0, md = 0.0, mm = 0.0, musum = 0.0, objl = 0.0;
+    double xk = 0.0, pik = 0.0;  // element-owned x_k, pi_k of the current stage
+    for (int k = 0; k <= N; ++k) {
+      double* stk = c.st(k);
+      // current-stage values (updated): x_k / pi_k carried, u_k updated here
+      if (k == 0) {
+        xk = xel ? c.x[li] : 0.0;  // x_0 = x0 (never updated)
+        pik = 0.0;
+      }
+      double uk = 0.0;
+      if (k < N && uel) {
+        uk = c.u[(size_t)k * nu + lane] + alpha_p * stk[kStStep + lane];
+        c.u[(size_t)k * nu + lane] = uk;
+      }
+      // barrier variables of stage k
+      Bar bu{0, 0, 1, 1}, bx{0, 0, 1, 1};
+      const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
+      if (lane < kMaxDim) {
+        bu = load_bar(stk, 0, lane);
+        bx = load_bar(stk, 1, lane);
+        const BarStep du = load_bstep(stk, 0, lane), dx = load_bstep(stk, 1, lane);
+        bu.tl += alpha_p * du.dtl;
+        bu.tu += alpha_p * du.dtu;
+        bu.ll += alpha_d * du.dll;
+        bu.lu += alpha_d * du.dlu;
+        bx.tl += alpha_p * dx.dtl;
+        bx.tu += alpha_p * dx.dtu;
+        bx.ll += alpha_d * dx.dll;
+        bx.lu += alpha_d * dx.dlu;
+        store_bar(stk, 0, lane, bu);
+        store_bar(stk, 1, lane, bx);
+      }
+      // next-stage x_{k+1}, pi_{k+1} (updated, carried to k+1)
+      double xn = 0.0, pin = 0.0;
+      if (k < N && xel) {
+        double* stn = c.st(k + 1);
+        xn = c.x[(size_t)(k + 1) * nx + lane] + alpha_p * stn[kStStep + 12 + lane];
+        pin = c.pi[(size_t)(k + 1) * nx + lane] + alpha_d * stn[kStStep + 24 + lane];
+        c.x[(size_t)(k + 1) * nx + lane] = xn;
+        c.pi[(size_t)(k + 1) * nx + lane] = pin;
+      }
+      // broadcasts of the iterate
+      double bxk[12], buk[12], bpn[12];
+      gather12(xk, bxk);
+      gather12(uk, buk);
+      gather12(pin, bpn);
+      // ---- residuals (element-owned) ----
+      double rgx = 0.0, rgu = 0.0, rb = 0.0;
+      {
+        double Qc[12];
+        c.col(c.Q + (size_t)k * c.nxx(), nx, col, xel, Qc);
+        double qx = 0.0;
+        sfor<0, 12>([&](auto j) {
+          constexpr int J = decltype(j)::value;
+          qx = fmadd(Qc[J], bxk[J], qx);
+        });
+        const double qk = c.el(c.q + (size_t)k * nx, nx, li);
+        rgx = qx + qk - pik;
+        if (k > 0) objl += xk * (0.5 * qx + qk);
+      }
+      if (k < N) {
+        double Rc[12], Sr[12], Sc[12], Bc[12], Ac[12];
+        c.col(c.R + (size_t)k * c.nuu(), nu, col, uel, Rc);
+        c.row(c.S + (size_t)k * c.nxu(), nu, nx, li, uel, Sr);
+        c.col(c.S + (size_t)k * c.nxu(), nu, col, xel, Sc);
+        c.col(c.B + (size_t)k * c.nxu(), nx, col, uel, Bc);
+        c.col(c.A + (size_t)k * c.nxx(), nx, col, xel, Ac);
+        double ru = 0.0, sx_ = 0.0, stu = 0.0, btp = 0.0, atp = 0.0;
+        sfor<0, 12>([&](auto j) {
+          constexpr int J = decltype(j)::value;
+          ru = fmadd(Rc[J], buk[J], ru);
+          sx_ = fmadd(Sr[J], bxk[J], sx_);
+          stu = fmadd(Sc[J], buk[J], stu);
+          btp = fmadd(Bc[J], bpn[J], btp);
+          atp = fmadd(Ac[J], bpn[J], atp);
+        });
+        const double rk = c.el(c.r + (size_t)k * nu, nu, li);
+        rgu = ru + sx_ + rk + btp;
+        rgx += stu + atp;
+        objl += uk * (0.5 * ru + rk + sx_);
+        // res_b = A x + B u + b - x_{k+1} (row-owned A, B)
+        double Ar[12], Br[12];
+        c.row(c.A + (size_t)k * c.nxx(), nx, nx, li, xel, Ar);
+        c.row(c.B + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
+        double ax = 0.0;
+        sfor<0, 12>([&](auto j) {
+          constexpr int J = decltype(j)::value;
+          ax = fmadd(Ar[J], bxk[J], ax);
+          ax = fmadd(Br[J], buk[J], ax);
+        });
+        rb = ax + c.el(c.b + (size_t)k * nx, nx, li) - xn;
+      }
+      // constraint terms
+      if (su.ml != 0.0) {
+        rgu -= bu.ll;
+        const double rd = uk - su.lb - bu.tl, rm = bu.ll * bu.tl;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (su.mu != 0.0) {
+        rgu += bu.lu;
+        const double rd = su.ub - uk - bu.tu, rm = bu.lu * bu.tu;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (sx.ml != 0.0) {
+        rgx -= bx.ll;
+        const double rd = xk - sx.lb - bx.tl, rm = bx.ll * bx.tl;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (sx.mu != 0.0) {
+        rgx += bx.lu;
+        const double rd = sx.ub - xk - bx.tu, rm = bx.lu * bx.tu;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (!xel) rgx = 0.0;
+      if (!uel) rgu = 0.0;
+      if (k < N) {
+        mg = fmax(mg, nabs(rgu));
+        mb = fmax(mb, nabs(xel ? rb : 0.0));
+      }
+      if (k > 0) mg = fmax(mg, nabs(rgx));
+      if (lane < kMaxDim) {
+        stk[kStRes + lane] = rgu;
+        stk[kStRes + 12 + lane] = rgx;
+        stk[kStRes + 24 + lane] = xel ? rb : 0.0;
+      }
+      xk = xn;
+      pik = pin;
+    }
+    res_stat = gmax(lane < kMaxDim ? mg : 0.0);
+    res_eq = gmax(lane < kMaxDim ? mb : 0.0);
+    res_ineq = gmax(lane < kMaxDim ? md : 0.0);
+    res_comp = gmax(lane < kMaxDim ? mm : 0.0);
+    obj = gsum(lane < kMaxDim ? objl : 0.0);
+    mu = gsum(lane < kMaxDim ? musum : 0.0) * nc_inv;
+    // ---- exit test (HPIPM order: converged / iter_max / min step / NaN) ----
+    {
+      const bool isnan_ = !(res_stat == res_stat) || !(res_eq == res_eq) ||
+                          !(res_ineq == res_ineq) || !(res_comp == res_comp) || !(mu == mu) ||
+                          res_stat == __builtin_inf() || res_eq == __builtin_inf();
+      if (isnan_) {
+        status = 3;
+      } else if (res_stat <= a.tol_stat && res_eq <= a.tol_eq && res_ineq <= a.tol_ineq &&
+                 res_comp <= a.tol_comp) {
+        status = 0;
+      } else if (iter >= a.iter_max) {
+        status = 1;
+      } else if (iter > 0 && last_amin < a.alpha_min) {
+        status = 2;
+      }
+      if (status >= 0) break;
+    }
+
+    // =================== B1: factorization + predictor vectors ===================
+    {
+      double P[12];
+      // terminal stage: P_N = Q_N + diag(Gamma_x), p_N = q~_N
+      {
+        double* stN = c.st(N);
+        const Side sx = c.side_x(N, lane);
+        const double xv = xel ? c.x[(size_t)N * nx + lane] : 0.0;
+        double G = 0.0, g = 0.0;
+        if (lane < kMaxDim) gamma_of(sx, load_bar(stN, 1, lane), xv, 0.0, 0.0, 0.0, G, g);
+        const double qt = lane < kMaxDim ? stN[kStRes + 12 + lane] + g : 0.0;
+        double qv[12];
+        gather12(qt, qv);
+        c.col(c.Q + (size_t)N * c.nxx(), nx, col, xel, P);
+        sfor<0, 12>([&](auto i) {
+          constexpr int I = decltype(i)::value;
+          if (lane == I) P[I] += G;
+          if (c.isv) P[I] = qv[I];
+        });
+        if (lane < kMaxDim) store12(stN + kRecP + lane * 12, P);
+        if (c.isv) store12(stN + kRecPv, P);
+      }
+      for (int k = N - 1; k >= 0; --k) {
+        double* stk = c.st(k);
+        const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
+        const double uv = uel ? c.u[(size_t)k * nu + lane] : 0.0;
+        const double xv = xel ? c.x[(size_t)k * nx + lane] : 0.0;
+        double Gu = 0.0, gu = 0.0, Gx = 0.0, gx = 0.0;
+        if (lane < kMaxDim) {
+          gamma_of(su, load_bar(stk, 0, lane), uv, 0.0, 0.0, 0.0, Gu, gu);
+          gamma_of(sx, load_bar(stk, 1, lane), xv, 0.0, 0.0, 0.0, Gx, gx);
+        }
+        const double rt = lane < kMaxDim ? stk[kStRes + lane] + gu : 0.0;
+        const double qt = lane < kMaxDim ? stk[kStRes + 12 + lane] + gx : 0.0;
+        const double bt = lane < kMaxDim ? stk[kStRes + 24 + lane] : 0.0;
+        double bv[12];
+        gather12(bt, bv);
+        double A_[12], B_[12];
+        c.col(c.A + (size_t)k * c.nxx(), nx, col, xel, A_);
+        c.col(c.B + (size_t)k * c.nxu(), nx, col, uel, B_);
+        sfor<0, 12>([&](auto i) {
+          constexpr int I = decltype(i)::value;
+          if (c.isv) {
+            A_[I] = bv[I];
+            B_[I] = 0.0;
+          }
+        });
+        auto loadR = [&](double (&Rc)[12]) {
+          c.col(c.R + (size_t)k * c.nuu(), nu, col, uel, Rc);
+          sfor<0, 12>([&](auto i) {
+            constexpr int I = decltype(i)::value;
+            if (lane == I) Rc[I] += (I < nu) ? Gu : 1.0;  // padded inputs: R = 1
+            if (c.isv) Rc[I] = 0.0;
+          });
+        };
+        auto loadSQ = [&](double (&Sc)[12], double (&Qc)[12]) {
+          c.col(c.S + (size_t)k * c.nxu(), nu, col, xel, Sc);
+          c.col(c.Q + (size_t)k * c.nxx(), nx, col, xel, Qc);
+          sfor<0, 12>([&](auto i) {
+            constexpr int I = decltype(i)::value;
+            const double rI = bc<I>(rt), qI = bc<I>(qt);
+            if (lane == I) Qc[I] += Gx;
+            if (c.isv) {
+              Sc[I] = rI;
+              Qc[I] = qI;
+            }
+          });
+        };
+        StageFactor<double> f;
+        riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
+        if (lane < kMaxDim) {
+          store12(stk + kRecL + lane * 12, f.Lc);
+          store12(stk + kRecK + lane * 12, f.Kc);
+          store12(stk + kRecAcl + lane * 12, A_);
+          store12(stk + kRecP + lane * 12, f.F);
+          stk[kRecRs + lane] = f.rs;
+        }
+        if (c.isv) {
+          store12(stk + kRecKv, f.Kc);
+          store12(stk + kRecBcl, A_);
+          store12(stk + kRecPv, f.F);
+        }
+        sfor<0, 12>([&](auto i) {
+          constexpr int I = decltype(i)::value;
+          P[I] = f.F[I];
+        });
+      }
+    }
+
+    // =================== F1 / M / B2 / F2 ===================
+    double sigma_mu = 0.0;
+    const int npass = a.pred_corr ? 2 : 1;
+    double ap = 1e300, ad = 1e300;
+    for (int pass = 0; pass < npass; ++pass) {
+      const bool corr = pass == 1;
+      if (corr) {
+        // ---- M: alpha_aff, mu_aff, sigma ----
+        const double aa = fmin(1.0, fmin(gmin(ap), gmin(ad)));
+        double mus = 0.0;
+        for (int k = 0; k <= N; ++k) {
+          const double* stk = c.st(k);
+          if (lane < kMaxDim) {
+            const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
+            const Bar bu = load_bar(stk, 0, lane), bx = load_bar(stk, 1, lane);
+            const BarStep du = load_bstep(stk, 0, lane), dx = load_bstep(stk, 1, lane);
+            if (su.ml != 0.0) mus += (bu.ll + aa * du.dll) * (bu.tl + aa * du.dtl);
+            if (su.mu != 0.0) mus += (bu.lu + aa * du.dlu) * (bu.tu + aa * du.dtu);
+            if (sx.ml != 0.0) mus += (bx.ll + aa * dx.dll) * (bx.tl + aa * dx.dtl);
+            if (sx.mu != 0.0) mus += (bx.lu + aa * dx.dlu) * (bx.tu + aa * dx.dtu);
+          }
+        }
+        const double mu_aff = gsum(lane < kMaxDim ? mus : 0.0) * nc_inv;
+        double sg = mu > 0.0 ? mu_aff / mu : 0.0;
+        sg = sg * sg * sg;
+        if (sg > 1.0) sg = 1.0;
+        sigma_mu = sg * mu;
+        // ---- B2: corrector vectors (element-owned recursion) ----
+        double pnext = 0.0;  // p_{k+1}, element-owned
+        {
+          double* stN = c.st(N);
+          const Side sx = c.side_x(N, lane);
+          const double xv = xel ? c.x[(size_t)N * nx + lane] : 0.0;
+          double G = 0.0, g = 0.0;
+          if (lane < kMaxDim) {
+            const BarStep dx = load_bstep(stN, 1, lane);
+            gamma_of(sx, load_bar(stN, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, G, g);
+          }
+          pnext = lane < kMaxDim && xel ? stN[kStRes + 12 + lane] + g : 0.0;
+          if (lane < kMaxDim) stN[kRecPv + lane] = pnext;
+        }
+        for (int k = N - 1; k >= 0; --k) {
+          double* stk = c.st(k);
+          const double* stn = c.st(k + 1);
+          const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
+          const double uv = uel ? c.u[(size_t)k * nu + lane] : 0.0;
+          const double xv = xel ? c.x[(size_t)k * nx + lane] : 0.0;
+          double Gu = 0.0, gu = 0.0, Gx = 0.0, gx = 0.0;
+          if (lane < kMaxDim) {
+            const BarStep du = load_bstep(stk, 0, lane), dx = load_bstep(stk, 1, lane);
+            gamma_of(su, load_bar(stk, 0, lane), uv, du.dll * du.dtl, du.dlu * du.dtu, sigma_mu, Gu, gu);
+            gamma_of(sx, load_bar(stk, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, Gx, gx);
+          }
+          const double rt = lane < kMaxDim && uel ? stk[kStRes + lane] + gu : 0.0;
+          const double qt = lane < kMaxDim && xel ? stk[kStRes + 12 + lane] + gx : 0.0;
+          const double bt = lane < kMaxDim ? stk[kStRes + 24 + lane] : 0.0;
+          // w = P_{k+1} b~ + p_{k+1}
+          double Pc[12], bb[12];
+          load12(stn + kRecP + col * 12, Pc);
+          gather12(bt, bb);
+          double w = pnext;
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            w = fmadd(Pc[J], bb[J], w);
+          });
+          // g = r~ + B'w ; f = q~ + A'w
+          double Bc[12], Ac[12], bw[12];
+          c.col(c.B + (size_t)k * c.nxu(), nx, col, uel, Bc);
+          c.col(c.A + (size_t)k * c.nxx(), nx, col, xel, Ac);
+          gather12(w, bw);
+          double g = rt, f = qt;
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            g = fmadd(Bc[J], bw[J], g);
+            f = fmadd(Ac[J], bw[J], f);
+          });
+          if (lane >= kMaxDim) g = 0.0;
+          // p = f + K'g  (K column-owned: lane j holds K[:, j])
+          double Kc[12], bg[12];
+          load12(stk + kRecK + col * 12, Kc);
+          gather12(g, bg);
+          double pv = f;
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            pv = fmadd(Kc[J], bg[J], pv);
+          });
+          // y = L^-1 g (row-owned L), then z = L^-T y (column-owned L), k = -z
+          double Lr[12], Lc[12];
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            Lr[J] = stk[kRecL + J * 12 + li];
+          });
+          load12(stk + kRecL + col * 12, Lc);
+          const double rs = stk[kRecRs + li];
+          double y = g;
+          sfor<0, 12>([&](auto kk) {
+            constexpr int K = decltype(kk)::value;
+            const double yk = bc<K>(y * rs);
+            if (lane == K) y = yk;
+            if (lane > K) y = fmadd(-Lr[K], yk, y);
+          });
+          sfor_down<0, 12>([&](auto kk) {
+            constexpr int K = decltype(kk)::value;
+            const double zk = bc<K>(y * rs);
+            if (lane == K) y = zk;
+            if (lane < K) y = fmadd(-Lc[K], zk, y);
+          });
+          const double kv = lane < kMaxDim && uel ? -y : 0.0;
+          // bcl = b~ + B k (row-owned B)
+          double Br[12], bk[12];
+          c.row(c.B + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
+          gather12(kv, bk);
+          double bcl = bt;
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            bcl = fmadd(Br[J], bk[J], bcl);
+          });
+          if (lane < kMaxDim) {
+            stk[kRecKv + lane] = kv;
+            stk[kRecBcl + lane] = xel ? bcl : 0.0;
+            stk[kRecPv + lane] = xel ? pv : 0.0;
+          }
+          pnext = xel ? pv : 0.0;
+        }
+      }
+      // ---- forward step (F1 predictor / F2 corrector), row-owned ----
+      ap = 1e300;
+      ad = 1e300;
+      double dxk = 0.0;  // dx_0 = 0 (x0 fixed)
+      for (int k = 0; k <= N; ++k) {
+        double* stk = c.st(k);
+        double bdx[12];
+        gather12(dxk, bdx);
+        double Pc[12];
+        load12(stk + kRecP + col * 12, Pc);
+        double dpi = stk[kRecPv + li];
+        sfor<0, 12>([&](auto j) {
+          constexpr int J = decltype(j)::value;
+          dpi = fmadd(Pc[J], bdx[J], dpi);
+        });
+        double du = 0.0, dxn = 0.0;
+        if (k < N) {
+          double Kr[12], Ar[12];
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            Kr[J] = stk[kRecK + J * 12 + li];
+            Ar[J] = stk[kRecAcl + J * 12 + li];
+          });
+          du = stk[kRecKv + li];
+          dxn = stk[kRecBcl + li];
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            du = fmadd(Kr[J], bdx[J], du);
+            dxn = fmadd(Ar[J], bdx[J], dxn);
+          });
+        }
+        if (!uel || k == N) du = 0.0;
+        if (!xel) {
+          dxn = 0.0;
+          dpi = 0.0;
+        }
+        if (lane < kMaxDim) {
+          const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
+          const Bar bu = load_bar(stk, 0, lane), bx = load_bar(stk, 1, lane);
+          const double uv = (uel && k < N) ? c.u[(size_t)k * nu + lane] : 0.0;
+          const double xv = xel ? c.x[(size_t)k * nx + lane] : 0.0;
+          double eul = 0.0, euu = 0.0, exl = 0.0, exu = 0.0, smu = 0.0;
+          if (corr) {
+            const BarStep pu = load_bstep(stk, 0, lane), px = load_bstep(stk, 1, lane);
+            eul = pu.dll * pu.dtl;
+            euu = pu.dlu * pu.dtu;
+            exl = px.dll * px.dtl;
+            exu = px.dlu * px.dtu;
+            smu = sigma_mu;
+          }
+          const BarStep nu_ = bar_step(su, bu, uv, du, eul, euu, smu);
+          const BarStep nx_ = bar_step(sx, bx, xv, dxk, exl, exu, smu);
+          ratio(su, bu, nu_, ap, ad);
+          ratio(sx, bx, nx_, ap, ad);
+          store_bstep(stk, 0, lane, nu_);
+          store_bstep(stk, 1, lane, nx_);
+          stk[kStStep + lane] = du;
+          stk[kStStep + 12 + lane] = dxk;
+          stk[kStStep + 24 + lane] = k > 0 ? dpi : 0.0;
+        }
+        dxk = dxn;
+      }
+    }
+    // ---- step length ----
+    ap = gmin(lane < kMaxDim ? ap : 1e300);
+    ad = gmin(lane < kMaxDim ? ad : 1e300);
+    if (!a.split_step) {
+      ap = fmin(ap, ad);
+      ad = ap;
+    }
+    alpha_p = fmin(1.0, kStepTau * ap);
+    alpha_d = fmin(1.0, kStepTau * ad);
+    last_amin = fmin(alpha_p, alpha_d);
+    ++iter;
+  }
+
+  // =================== outputs ===================
+  // pi_0 := Q0 x0 + S0'u0 + q0 + A0'(pi_1 + P_1 res_b0): the value of the
+  // stage-0 rebuild (ocp_qp_ipm_solver.cpp:347-373) with p_1 = pi_1 - P_1 x_1.
+  {
+    const double* st0 = c.st(0);
+    const double* st1 = c.st(1);
+    double bx0[12], bu0[12];
+    gather12(xel ? c.x[li] : 0.0, bx0);
+    gather12(uel ? c.u[li] : 0.0, bu0);
+    double P1c[12], brb[12];
+    load12(st1 + kRecP + col * 12, P1c);
+    gather12(lane < kMaxDim ? st0[kStRes + 24 + lane] : 0.0, brb);
+    double t = xel ? c.pi[(size_t)nx + lane] : 0.0;
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      t = fmadd(P1c[J], brb[J], t);
+    });
+    if (!xel) t = 0.0;
+    double bt[12];
+    gather12(t, bt);
+    double Qc[12], Sc[12], Ac[12];
+    c.col(c.Q, nx, col, xel, Qc);
+    c.col(c.S, nu, col, xel, Sc);
+    c.col(c.A, nx, col, xel, Ac);
+    double p0 = c.el(c.q, nx, li);
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      p0 = fmadd(Qc[J], bx0[J], p0);
+      p0 = fmadd(Sc[J], bu0[J], p0);
+      p0 = fmadd(Ac[J], bt[J], p0);
+    });
+    if (xel) c.pi[lane] = p0;
+  }
+  if (a.P || a.p || a.K || a.k) {
+    // Riccati matrices of the last factorization (HPIPM's get_ric_* getters),
+    // vectors by consistency: p_k = pi_k - P_k x_k, k_k = u_k - K_k x_k.
+    const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu;
+    for (int k = 0; k <= N; ++k) {
+      const double* stk = c.st(k);
+      double bxk[12];
+      gather12(xel ? c.x[(size_t)k * nx + li] : 0.0, bxk);
+      double Pc[12];
+      load12(stk + kRecP + col * 12, Pc);
+      if (a.P && xel)
+        sfor<0, 12>([&](auto i) {
+          constexpr int I = decltype(i)::value;
+          if (I < nx) a.P[((size_t)qp * (N + 1) + k) * nxx + (size_t)lane * nx + I] = Pc[I];
+        });
+      if (a.p) {
+        double px = 0.0;
+        sfor<0, 12>([&](auto j) {
+          constexpr int J = decltype(j)::value;
+          px = fmadd(Pc[J], bxk[J], px);
+        });
+        if (xel) a.p[((size_t)qp * (N + 1) + k) * nx + lane] = c.pi[(size_t)k * nx + lane] - px;
+      }
+      if (k < N) {
+        double Kc[12];
+        load12(stk + kRecK + col * 12, Kc);
+        if (a.K && xel)
+          sfor<0, 12>([&](auto i) {
+            constexpr int I = decltype(i)::value;
+            if (I < nu) a.K[((size_t)qp * N + k) * nxu + (size_t)lane * nu + I] = Kc[I];
+          });
+        if (a.k) {
+          double Kr[12];
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            Kr[J] = stk[kRecK + J * 12 + li];
+          });
+          double kx = 0.0;
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            kx = fmadd(Kr[J], bxk[J], kx);
+          });
+          if (uel) a.k[((size_t)qp * N + k) * nu + lane] = c.u[(size_t)k * nu + lane] - kx;
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    if (a.status) a.status[qp] = status;
+    if (a.iter) a.iter[qp] = nc > 0.0 ? iter : 0;
+    if (a.res) {
+      a.res[(size_t)qp * 4 + 0] = res_stat;
+      a.res[(size_t)qp * 4 + 1] = res_eq;
+      a.res[(size_t)qp * 4 + 2] = res_ineq;
+      a.res[(size_t)qp * 4 + 3] = res_comp;
+    }
+    if (a.obj) a.obj[qp] = obj;
+  }
+}
+
+}  // namespace
+
+size_t ws_doubles_ipm(int N) { return (size_t)(N + 1) * kIpmStage; }
+
+hipError_t launch_ipm_box(const ProblemArgs& a, hipStream_t stream) {
+  if (a.batch <= 0) return hipSuccess;
+  const int threads = 256;
+  const long long lanes = (long long)a.batch * kGroup;
+  const int blocks = (int)((lanes + threads - 1) / threads);
+  if (a.nx == 12 && a.nu == 12) {
+    hipLaunchKernelGGL(ipm_box_kernel<true>, dim3(blocks), dim3(threads), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(ipm_box_kernel<false>, dim3(blocks), dim3(threads), 0, stream, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace srbd

@@ -34,7 +34,22 @@ struct ProblemArgs {
   double* ws;
   size_t ws_qp;  // doubles per QP
   double reg;
+  // IPM settings (hpipm-cpp OcpQpIpmSolverSettings semantics)
+  int iter_max, pred_corr, split_step, warm_start;
+  double alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp;
 };
+
+// IPM per-stage workspace layout (doubles), see ipm_box.hip.
+constexpr int kRecL = 0, kRecK = 144, kRecAcl = 288, kRecP = 432, kRecRs = 576, kRecKv = 588,
+              kRecBcl = 600, kRecPv = 612, kRecSize = 624;
+constexpr int kStLam = 624;   // 8 x 12: lam_l,u / lam_u,u / t_l,u / t_u,u / same for x
+constexpr int kStRes = 720;   // 3 x 12: res_g,u / res_g,x / res_b
+constexpr int kStStep = 756;  // 3 x 12: du / dx / dpi
+constexpr int kStDlt = 792;   // 8 x 12: dt_l,u dt_u,u dlam_l,u dlam_u,u (u), same (x)
+constexpr int kIpmStage = 888;
+
+size_t ws_doubles_ipm(int N);
+hipError_t launch_ipm_box(const ProblemArgs& a, hipStream_t stream);
 
 // Workspace doubles per QP needed by the unconstrained solve.
 size_t ws_doubles_unconstr(int N);

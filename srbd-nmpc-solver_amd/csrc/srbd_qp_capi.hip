@@ -122,7 +122,7 @@ static int check_dims(const srbd_qp_dims* d) {
 static bool constrained(const srbd_qp_dims& d) { return d.has_box_u || d.has_box_x || d.ng > 0; }
 
 static size_t ws_doubles_per_qp(const srbd_qp_dims& d) {
-  return srbd::ws_doubles_unconstr(d.N);
+  return constrained(d) ? srbd::ws_doubles_ipm(d.N) : srbd::ws_doubles_unconstr(d.N);
 }
 
 int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srbd_qp_handle* out) {
@@ -131,8 +131,8 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srb
   int rc = check_dims(dims);
   if (rc) return rc;
   if (batch_capacity < 1) return fail(SRBD_QP_EINVAL, "batch_capacity must be >= 1");
-  if (constrained(*dims))
-    return fail(SRBD_QP_EDIM, "inequality-constrained QPs are not supported by this build yet");
+  if (dims->ng > 0)
+    return fail(SRBD_QP_EDIM, "general constraints (ng > 0) are not supported by this build yet");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(SRBD_QP_EDEVICE, "no HIP device available (libsrbd_qp has no CPU fallback)");
@@ -228,12 +228,27 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   a.ws = h->ws;
   a.ws_qp = h->ws_qp;
   a.reg = st->reg_prim;
-  hipError_t e = srbd::launch_riccati_unconstr(a, strm);
-  if (e == hipSuccess && (s->res || s->obj)) {
-    // residuals of an unconstrained solve are not computed by this build:
-    // report zeros only when asked not to compute them.
-    if (s->res) e = hipMemsetAsync(s->res, 0, sizeof(double) * 4 * (size_t)batch, strm);
-    if (e == hipSuccess && s->obj) e = hipMemsetAsync(s->obj, 0, sizeof(double) * (size_t)batch, strm);
+  a.iter_max = st->iter_max;
+  a.pred_corr = st->pred_corr;
+  a.split_step = st->split_step;
+  a.warm_start = st->warm_start;
+  a.alpha_min = st->alpha_min;
+  a.mu0 = st->mu0;
+  a.tol_stat = st->tol_stat;
+  a.tol_eq = st->tol_eq;
+  a.tol_ineq = st->tol_ineq;
+  a.tol_comp = st->tol_comp;
+  hipError_t e;
+  if (constrained(h->dims)) {
+    e = srbd::launch_ipm_box(a, strm);
+  } else {
+    e = srbd::launch_riccati_unconstr(a, strm);
+    if (e == hipSuccess && (s->res || s->obj)) {
+      // an unconstrained solve reports zero residual norms / objective unless
+      // computed (compute_residuals is not implemented for nc == 0 yet)
+      if (s->res) e = hipMemsetAsync(s->res, 0, sizeof(double) * 4 * (size_t)batch, strm);
+      if (e == hipSuccess && s->obj) e = hipMemsetAsync(s->obj, 0, sizeof(double) * (size_t)batch, strm);
+    }
   }
   hipSetDevice(prev);
   if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("kernel launch: ") + hipGetErrorString(e));

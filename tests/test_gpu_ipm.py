@@ -1,0 +1,118 @@
+"""GPU parity of the box-constrained batched IPM kernel (through the C-ABI).
+
+* compareResults (hpipm-cpp/test/ocp_qp_ipm_solver.cpp:170-315): the OSQP
+  golden trajectories sol0..14.txt, warm-started closed loop, isApprox 1e-9.
+* constrained (:112-168): status Success and x[0] == x0, plus parity with the
+  CPU oracle (same algorithm) on x, u, pi and the iteration counts.
+* SRBD box-on-u QPs (BASELINE config 3) against the oracle.
+"""
+import numpy as np
+import pytest
+
+import helpers
+
+pytestmark = pytest.mark.gpu
+
+
+def test_compare_results_osqp_golden(pkg):
+    qp, d, goldens, A, B, b = helpers.quadcopter(pkg.OcpQpBatch)
+    st = dict(d["settings"])
+    N, nx, nu = qp.N, qp.nx, qp.nu
+    x = np.zeros(nx)
+    xw = np.zeros((1, N + 1, nx))
+    uw = np.full((1, N, nu), d["u0"])
+    h = pkg.capi.Handle(N, nx, nu, 0, True, True, capacity=1)
+    for t in range(d["sim_steps"]):
+        out = pkg.capi.solve(qp, x[None], st, x_init=xw, u_init=uw, handle=h)
+        assert out["status"][0] == 0, (t, out["status"][0], out["res"][0])
+        cat = np.concatenate([out["x"][0].ravel(), out["u"][0].ravel()])
+        assert helpers.is_approx(cat, goldens[t], d["rel_prec"]), (
+            t, np.linalg.norm(cat - goldens[t]) / np.linalg.norm(goldens[t]))
+        xw, uw = out["x"], out["u"]
+        x = A @ x + B @ out["u"][0, 0] + b
+
+
+def test_compare_results_batched(pkg, oracle):
+    """The same closed-loop problem, all 15 steps solved as one cold-start batch
+    from the oracle's trajectory of initial states."""
+    qp1, d, goldens, A, B, b = helpers.quadcopter(pkg.OcpQpBatch)
+    x0s = []
+    x = np.zeros(12)
+    for t in range(d["sim_steps"]):
+        x0s.append(x.copy())
+        u0 = goldens[t][(qp1.N + 1) * 12:(qp1.N + 1) * 12 + 4]
+        x = A @ x + B @ u0 + b
+    qp = qp1.subset(np.zeros(15, dtype=int))
+    x0 = np.array(x0s)
+    st = dict(d["settings"], warm_start=0)
+    out = pkg.capi.solve(qp, x0, st)
+    assert np.all(out["status"] == 0), out["status"]
+    for t in range(15):
+        cat = np.concatenate([out["x"][t].ravel(), out["u"][t].ravel()])
+        assert helpers.is_approx(cat, goldens[t], 1e-9), t
+
+
+@pytest.mark.parametrize("dims", [(5, 3), (12, 12), (12, 4)])
+def test_constrained_vs_oracle(pkg, oracle, dims):
+    nx, nu = dims
+    qp, x0 = helpers.random_constrained(24, 15, nx, nu, 0, 17 + nx, pkg.OcpQpBatch)
+    st = dict(iter_max=40, mode="Balance")
+    out = pkg.capi.solve(qp, x0, st, riccati=True)
+    ref = oracle.solve(qp, st, x0=x0)
+    assert np.all(out["status"] == 0), (out["status"], out["res"])
+    assert np.all(ref["status"] == 0)
+    assert np.all(np.abs(out["iter"] - ref["iter"]) <= 1), (out["iter"], ref["iter"])
+    for i in range(qp.batch):
+        assert np.array_equal(out["x"][i, 0], x0[i])  # x[0] == x0 (reference :167)
+        for key in ("x", "u"):
+            assert helpers.is_approx(out[key][i], ref[key][i], 1e-7), (key, i)
+        assert helpers.is_approx(out["pi"][i], ref["pi"][i], 1e-6), ("pi", i)
+        assert np.all(out["res"][i] <= 1e-8)
+
+
+def test_inactive_bounds_equal_unconstrained(pkg):
+    qp, x0 = helpers.random_unconstrained(16, 12, 12, 12, 9, pkg.OcpQpBatch)
+    ref = pkg.capi.solve(qp, x0)
+    qp.lbu = np.full((16, 12, 12), -1e4)
+    qp.ubu = np.full((16, 12, 12), 1e4)
+    out = pkg.capi.solve(qp, x0, dict(iter_max=60, tol_stat=1e-11, tol_eq=1e-11, tol_ineq=1e-11,
+                                      tol_comp=1e-9))
+    assert np.all(out["status"] == 0), out["status"]
+    for i in range(16):
+        assert helpers.is_approx(out["x"][i], ref["x"][i], 1e-8)
+        assert helpers.is_approx(out["u"][i], ref["u"][i], 1e-8)
+
+
+def test_all_masked_is_unconstrained(pkg):
+    qp, x0 = helpers.random_unconstrained(5, 10, 6, 4, 21, pkg.OcpQpBatch)
+    ref = pkg.capi.solve(qp, x0)
+    qp.lbu = np.full((5, 10, 4), -1.0)
+    qp.ubu = np.full((5, 10, 4), 1.0)
+    qp.lbu_mask = np.zeros((5, 10, 4))
+    qp.ubu_mask = np.zeros((5, 10, 4))
+    out = pkg.capi.solve(qp, x0)
+    assert np.all(out["status"] == 0) and np.all(out["iter"] == 0)
+    for i in range(5):
+        assert helpers.is_approx(out["u"][i], ref["u"][i], 1e-9)
+
+
+@pytest.mark.parametrize("settings", [
+    dict(iter_max=30),                                                   # hpipm-cpp defaults
+    dict(iter_max=30, tol_stat=1e-4, tol_eq=1e-4, tol_ineq=1e-4, tol_comp=1e-4, split_step=1),  # NMPC
+])
+def test_srbd_box_u_vs_oracle(pkg, oracle, settings):
+    qp, x0 = pkg.srbd_model.generate_batch(40, N=20, seed=77, constraints="box_u")
+    out = pkg.capi.solve(qp, x0, settings)
+    ref = oracle.solve(qp, settings, x0=x0, riccati=False)
+    assert np.all(out["status"] == 0), out["status"]
+    assert np.all(np.abs(out["iter"] - ref["iter"]) <= 1), (out["iter"], ref["iter"])
+    tol = 1e-7 if settings.get("tol_stat", 1e-8) < 1e-6 else 1e-3
+    for i in range(qp.batch):
+        assert helpers.is_approx(out["u"][i], ref["u"][i], tol), i
+        assert helpers.is_approx(out["x"][i], ref["x"][i], tol), i
+
+
+def test_max_iter_status(pkg):
+    qp, x0 = pkg.srbd_model.generate_batch(8, N=10, seed=5, constraints="box_u")
+    out = pkg.capi.solve(qp, x0, dict(iter_max=2))
+    assert np.all(out["status"] == 1) and np.all(out["iter"] == 2)

@@ -40,6 +40,12 @@ def test_reference_unconstrained_dims(pkg):
 @pytest.mark.parametrize("N", [1, 10, 20, 40])
 def test_full_12x12_fast_path(pkg, N):
     qp, x0 = helpers.random_unconstrained(67, N, 12, 12, 100 + N, pkg.OcpQpBatch)
+    if N > 10:
+        # random 12x12 A has spectral radius ~2: over 20+ stages P grows like
+        # rho^(2N) and pi = P x + p cancels catastrophically in any fp64
+        # implementation (numpy included).  Keep the long horizons well-posed.
+        rho = np.max(np.abs(np.linalg.eigvals(qp.A)), axis=-1)
+        qp.A = qp.A / rho[..., None, None]
     out = pkg.capi.solve(qp, x0, None, riccati=True)
     assert np.all(out["status"] == 0)
     _assert_riccati_matches(qp, x0, out, prec=1e-9, qps=range(0, 67, 11))
