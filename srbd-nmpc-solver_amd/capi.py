@@ -62,6 +62,13 @@ def lib():
     if _lib is None:
         if not LIB_PATH.exists():
             raise SrbdQpError(f"{LIB_PATH} not built; run `make` (or __graft_entry__.build())")
+        # torch bundles its own libamdhip64.so.7 (same soname as /opt/rocm's).
+        # Load torch first so that this library binds to the HIP runtime torch
+        # already uses: one runtime per process, shared device pointers/streams.
+        try:
+            import torch  # noqa: F401
+        except ImportError:  # pragma: no cover - C-only consumers
+            pass
         L = C.CDLL(str(LIB_PATH))
         L.srbd_qp_create.argtypes = [C.POINTER(Dims), C.c_int, C.c_int, C.POINTER(C.c_void_p)]
         L.srbd_qp_create.restype = C.c_int

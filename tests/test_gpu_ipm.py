@@ -66,7 +66,17 @@ def test_constrained_vs_oracle(pkg, oracle, dims):
         assert np.array_equal(out["x"][i, 0], x0[i])  # x[0] == x0 (reference :167)
         for key in ("x", "u"):
             assert helpers.is_approx(out[key][i], ref[key][i], 1e-7), (key, i)
-        assert helpers.is_approx(out["pi"][i], ref["pi"][i], 1e-6), ("pi", i)
+        assert helpers.is_approx(out["pi"][i, 1:], ref["pi"][i, 1:], 1e-6), ("pi", i)
+        # pi_0: the stage-0 rebuild (ocp_qp_ipm_solver.cpp:347-373) is algebraically
+        # the x0-stationarity Q0 x0 + S0'u0 + q0 + A0'(pi_1 + P_1 res_b0); with active
+        # bounds P_1 carries lam/t ~ 1e10 and the literal rebuild (the oracle's) loses
+        # ~|P_1| eps, so check the kernel against the stationarity form directly.
+        A0, B0, b0 = qp.A[i, 0], qp.B[i, 0], qp.b[i, 0]
+        rb0 = A0 @ x0[i] + B0 @ out["u"][i, 0] + b0 - out["x"][i, 1]
+        pi0 = (qp.Q[i, 0] @ x0[i] + qp.S[i, 0].T @ out["u"][i, 0] + qp.q[i, 0]
+               + A0.T @ (out["pi"][i, 1] + out["P"][i, 1] @ rb0))
+        assert helpers.is_approx(out["pi"][i, 0], pi0, 1e-6), ("pi0", i)  # |P_1| eps |res_b0| limited
+        assert helpers.is_approx(out["pi"][i, 0], ref["pi"][i, 0], 1e-3), ("pi0 vs oracle", i)
         assert np.all(out["res"][i] <= 1e-8)
 
 

@@ -64,6 +64,8 @@ def test_padded_dims_vs_oracle(pkg, oracle, dims):
 
 def test_dense_kkt(pkg):
     qp, x0 = helpers.random_unconstrained(5, 20, 12, 12, 77, pkg.OcpQpBatch)
+    rho = np.max(np.abs(np.linalg.eigvals(qp.A)), axis=-1)  # well-posed long horizon
+    qp.A = qp.A / rho[..., None, None]
     out = pkg.capi.solve(qp, x0)
     for i in range(qp.batch):
         x, u, pi = helpers.dense_kkt(qp, x0[i], i)
