@@ -80,6 +80,64 @@ __device__ __forceinline__ void launder(T (&v)[12]) {
   launder_impl(v, std::make_integer_sequence<int, 12>{});
 }
 
+// ---------------------------------------------------------------------------
+// Fused broadcast-FMA blocks: v_fmac_f64_dpp with row_newbcast, i.e. the
+// broadcast rides on the FMA's src0 operand for free (hipcc does not combine
+// v_mov_b64_dpp into v_fmac_f64 by itself).  Each block is one asm statement
+// of 12 independent FMAs led by `s_nop 1`: the 2 wait states a DPP read needs
+// after a VALU write of its source VGPR (the only hazard here -- inside a
+// block no DPP source is written).
+//
+//   fma_bcast_src<S>(C, X, y):   C[i] += bc<S>(X[i]) * y     (i = 0..11)
+//   fma_bcast_lane(C, x, Y):     C[i] += bc<i>(x)    * y_i   -> see below
+// ---------------------------------------------------------------------------
+#define SRBD_FMAC_DPP(D, S0, S1, LANE) "v_fmac_f64_dpp " D ", " S0 ", " S1 " row_newbcast:" #LANE " row_mask:0xf bank_mask:0xf\n\t"
+
+// C[i] += bc<SRC>(X[i]) * y for i = 0..11
+template <int SRC>
+__device__ __forceinline__ void fma_bcast_src(double (&C)[12], const double (&X)[12], double y) {
+  static_assert(SRC >= 0 && SRC < kGroup, "row_newbcast source lane");
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %12, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %13, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %2, %14, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %3, %15, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %4, %16, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %5, %17, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %6, %18, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %7, %19, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %8, %20, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %9, %21, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %10, %22, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %11, %23, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf"
+      : "+v"(C[0]), "+v"(C[1]), "+v"(C[2]), "+v"(C[3]), "+v"(C[4]), "+v"(C[5]), "+v"(C[6]),
+        "+v"(C[7]), "+v"(C[8]), "+v"(C[9]), "+v"(C[10]), "+v"(C[11])
+      : "v"(X[0]), "v"(X[1]), "v"(X[2]), "v"(X[3]), "v"(X[4]), "v"(X[5]), "v"(X[6]), "v"(X[7]),
+        "v"(X[8]), "v"(X[9]), "v"(X[10]), "v"(X[11]), "v"(y), "i"(SRC));
+}
+
+// C[i] += bc<i>(x) * y for i = 0..11 (x, y: one register each)
+__device__ __forceinline__ void fma_bcast_lanes(double (&C)[12], double x, double y) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %12, %13 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %12, %13 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %2, %12, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %3, %12, %13 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %4, %12, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %5, %12, %13 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %6, %12, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %7, %12, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %8, %12, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %9, %12, %13 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %10, %12, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %11, %12, %13 row_newbcast:11 row_mask:0xf bank_mask:0xf"
+      : "+v"(C[0]), "+v"(C[1]), "+v"(C[2]), "+v"(C[3]), "+v"(C[4]), "+v"(C[5]), "+v"(C[6]),
+        "+v"(C[7]), "+v"(C[8]), "+v"(C[9]), "+v"(C[10]), "+v"(C[11])
+      : "v"(x), "v"(y));
+}
+
 template <typename T>
 __device__ __forceinline__ T fmadd(T a, T b, T c) {
   return __builtin_fma(a, b, c);

@@ -31,30 +31,50 @@
 // the previous phase (which blows the 256-VGPR budget).
 #define SRBD_PHASE_FENCE() __builtin_amdgcn_sched_barrier(0)
 
+// 1: the dense 12x12 products use the fused v_fmac_f64_dpp asm blocks
+// (qp_group.h); 0: compiler-generated v_mov_b64_dpp + v_fma_f64.
+#ifndef SRBD_FUSED_DPP
+#define SRBD_FUSED_DPP 1
+#endif
+
 namespace srbd {
 
 // C[:,l] = P M[:,l] (+ init): P symmetric & column-owned, M column-owned.
 template <typename T>
 __device__ __forceinline__ void sym_mul_col(const T (&P)[12], const T (&M)[12], T (&C)[12]) {
-  sfor<0, 12>([&](auto kk) {
-    constexpr int K = decltype(kk)::value;
-    sfor<0, 12>([&](auto i) {
-      constexpr int I = decltype(i)::value;
-      C[I] = fmadd(bc<K>(P[I]), M[K], C[I]);
+  if constexpr (std::is_same_v<T, double> && SRBD_FUSED_DPP) {
+    sfor<0, 12>([&](auto kk) {
+      constexpr int K = decltype(kk)::value;
+      fma_bcast_src<K>(C, P, M[K]);
     });
-  });
+  } else {
+    sfor<0, 12>([&](auto kk) {
+      constexpr int K = decltype(kk)::value;
+      sfor<0, 12>([&](auto i) {
+        constexpr int I = decltype(i)::value;
+        C[I] = fmadd(bc<K>(P[I]), M[K], C[I]);
+      });
+    });
+  }
 }
 
 // C[i][l] += X[:,i]' Y[:,l] for i < 12 (X, Y column-owned)
 template <typename T>
 __device__ __forceinline__ void tmul_acc(const T (&X)[12], const T (&Y)[12], T (&C)[12]) {
-  sfor<0, 12>([&](auto i) {
-    constexpr int I = decltype(i)::value;
+  if constexpr (std::is_same_v<T, double> && SRBD_FUSED_DPP) {
     sfor<0, 12>([&](auto kk) {
       constexpr int K = decltype(kk)::value;
-      C[I] = fmadd(bc<I>(X[K]), Y[K], C[I]);
+      fma_bcast_lanes(C, X[K], Y[K]);
     });
-  });
+  } else {
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      sfor<0, 12>([&](auto kk) {
+        constexpr int K = decltype(kk)::value;
+        C[I] = fmadd(bc<I>(X[K]), Y[K], C[I]);
+      });
+    });
+  }
 }
 
 // Right-looking Cholesky of the column-owned symmetric G (lane l holds
@@ -179,23 +199,15 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
   }
   SRBD_PHASE_FENCE();
   // ---- P_k = F - Y'Y (VL: p_k = f - Y'y)
-  sfor<0, 12>([&](auto i) {
-    constexpr int I = decltype(i)::value;
-    sfor<0, 12>([&](auto kk) {
-      constexpr int K = decltype(kk)::value;
-      o.F[I] = fmadd(-bc<I>(o.H[K]), o.H[K], o.F[I]);
-    });
-  });
+  {
+    T Hn[12];
+    sfor<0, 12>([&](auto i) { Hn[decltype(i)::value] = -o.H[decltype(i)::value]; });
+    tmul_acc(o.H, Hn, o.F);
+  }
   SRBD_PHASE_FENCE();
   // ---- Acl = A + B K (VL: bcl = b + B k)
   launder(B_);
-  sfor<0, 12>([&](auto i) {
-    constexpr int I = decltype(i)::value;
-    sfor<0, 12>([&](auto m) {
-      constexpr int M = decltype(m)::value;
-      A_[I] = fmadd(bc<M>(B_[I]), o.Kc[M], A_[I]);
-    });
-  });
+  sym_mul_col(B_, o.Kc, A_);  // A[i][l] += B[i][m] K[m][l]: bc<m>(B_[i]) * Kc[m]
 }
 
 }  // namespace srbd
