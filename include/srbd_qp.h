@@ -49,6 +49,7 @@
  *     x [batch][N+1][nx]  u [batch][N][nu]  pi [batch][N+1][nx]   (required)
  *     P [batch][N+1][nx*nx]  p [batch][N+1][nx]  K [batch][N][nu*nx]  k [batch][N][nu]
  *     status [batch] (HpipmStatus codes)  iter [batch]  res [batch][4]  obj [batch]
+ *     stat [batch][iter_max+2][18]
  *   Conventions (ocp_qp_ipm_solver.cpp:337-373, test/ocp_qp_ipm_solver.cpp:60-109):
  *     x[0] = x0; pi[k] is the multiplier of x[k] = A x[k-1] + ... (hpipm pi[k-1]),
  *     pi[k] = P[k] x[k] + p[k]; u[k] = K[k] x[k] + k[k]; stage 0 as rebuilt.
@@ -66,7 +67,7 @@
 extern "C" {
 #endif
 
-#define SRBD_QP_ABI_VERSION 1
+#define SRBD_QP_ABI_VERSION 2
 #define SRBD_QP_MAX_NX 12
 #define SRBD_QP_MAX_NU 12
 #define SRBD_QP_MAX_NG 64
@@ -134,6 +135,13 @@ typedef struct srbd_qp_solution_f64 {
   int *status, *iter;      /* optional                                     */
   double *res;             /* optional [batch][4] max |res_stat|,|res_eq|,|res_ineq|,|res_comp| */
   double *obj;             /* optional [batch]                              */
+  double *stat;            /* optional [batch][iter_max+2][18]: per-iteration
+                            * statistics in HPIPM's ws->stat row layout, the
+                            * rows hpipm-cpp copies into OcpQpIpmSolverStatistics
+                            * (ocp_qp_ipm_solver.cpp:381-403): alpha_aff, mu_aff,
+                            * sigma, alpha_prim, alpha_dual, mu, res_stat, res_eq,
+                            * res_ineq, res_comp, obj, then 7 columns that stay 0
+                            * (no LQ factorization / iterative refinement).    */
 } srbd_qp_solution_f64;
 
 typedef struct srbd_qp_handle_s* srbd_qp_handle;

@@ -40,7 +40,7 @@ DATA_FIELDS = ("A", "B", "b", "Q", "S", "R", "q", "r",
                "lbu", "ubu", "lbu_mask", "ubu_mask",
                "lbx", "ubx", "lbx_mask", "ubx_mask",
                "C", "D", "lg", "ug", "lg_mask", "ug_mask", "x0")
-SOL_FIELDS = ("x", "u", "pi", "P", "p", "K", "k", "status", "iter", "res", "obj")
+SOL_FIELDS = ("x", "u", "pi", "P", "p", "K", "k", "status", "iter", "res", "obj", "stat")
 
 
 class Data(C.Structure):
@@ -185,7 +185,7 @@ def _tensor_ptr(t) -> int:
 
 
 def device_buffers(qp, x0: np.ndarray, device="cuda:0", want_riccati: bool = False,
-                   x_init=None, u_init=None):
+                   x_init=None, u_init=None, stat_rows: int = 0):
     """Upload an OcpQpBatch (+x0) to device tensors in the C-ABI layout.
 
     Returns (data_tensors, sol_tensors, Data, Solution)."""
@@ -207,6 +207,8 @@ def device_buffers(qp, x0: np.ndarray, device="cuda:0", want_riccati: bool = Fal
         "res": torch.zeros(nb, 4, **f64),
         "obj": torch.zeros(nb, **f64),
     }
+    if stat_rows:
+        st["stat"] = torch.zeros(nb, stat_rows, 18, **f64)  # HPIPM ws->stat rows
     if want_riccati:
         st["P"] = torch.zeros(nb, N + 1, nx, nx, **f64)  # col-major blocks
         st["p"] = torch.zeros(nb, N + 1, nx, **f64)
@@ -218,16 +220,22 @@ def device_buffers(qp, x0: np.ndarray, device="cuda:0", want_riccati: bool = Fal
 
 
 def solve(qp, x0, settings: Optional[Dict] = None, device: str = "cuda:0", riccati: bool = False,
-          x_init=None, u_init=None, handle: Optional[Handle] = None) -> Dict[str, np.ndarray]:
-    """Solve an OcpQpBatch on the GPU through the C-ABI; returns numpy results."""
+          x_init=None, u_init=None, handle: Optional[Handle] = None,
+          stats: bool = False) -> Dict[str, np.ndarray]:
+    """Solve an OcpQpBatch on the GPU through the C-ABI; returns numpy results.
+
+    stats=True also returns "stat" [batch][iter_max+2][18], the per-iteration
+    statistics rows (alpha_aff, mu_aff, sigma, alpha_prim, alpha_dual, mu,
+    res_stat, res_eq, res_ineq, res_comp, obj, 0...)."""
     import torch
     if not torch.cuda.is_available():
         raise SrbdQpError("no GPU available: libsrbd_qp has no CPU fallback")
     dev_index = torch.device(device).index or 0
     h = handle or Handle(qp.N, qp.nx, qp.nu, qp.ng, qp.has_box_u, qp.has_box_x,
                          capacity=qp.batch, device=dev_index)
-    dt, st, data, sol = device_buffers(qp, x0, device, riccati, x_init, u_init)
     s = settings_struct(settings)
+    dt, st, data, sol = device_buffers(qp, x0, device, riccati, x_init, u_init,
+                                       stat_rows=(s.iter_max + 2) if stats else 0)
     h.solve_device(qp.batch, s, data, sol)
     h.synchronize()
     out = {k: v.cpu().numpy() for k, v in st.items()}

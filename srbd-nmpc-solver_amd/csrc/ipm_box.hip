@@ -520,6 +520,17 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
     res_comp = gmax(lane < kMaxDim ? mm : 0.0);
     obj = gsum(lane < kMaxDim ? objl : 0.0);
     mu = gsum(lane < kMaxDim ? musum : 0.0) * nc_inv;
+    double* stat_row = a.stat && lane == 0
+                           ? a.stat + ((size_t)qp * (a.iter_max + 2) + iter) * kStatCols
+                           : nullptr;
+    if (stat_row) {
+      stat_row[5] = mu;
+      stat_row[6] = res_stat;
+      stat_row[7] = res_eq;
+      stat_row[8] = res_ineq;
+      stat_row[9] = res_comp;
+      stat_row[10] = obj;
+    }
     // ---- exit test (HPIPM order: converged / iter_max / min step / NaN) ----
     {
       const bool isnan_ = !(res_stat == res_stat) || !(res_eq == res_eq) ||
@@ -628,7 +639,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
     }
 
     // =================== F1 / M / B2 / F2 ===================
-    double sigma_mu = 0.0;
+    double sigma_mu = 0.0, alpha_aff = 0.0, mu_aff = 0.0, sigma = 0.0;
     const int npass = a.pred_corr ? 2 : 1;
     double ap = 1e300, ad = 1e300;
     for (int pass = 0; pass < npass; ++pass) {
@@ -636,6 +647,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
       if (corr) {
         // ---- M: alpha_aff, mu_aff, sigma ----
         const double aa = fmin(1.0, fmin(gmin(ap), gmin(ad)));
+        alpha_aff = aa;
         double mus = 0.0;
         for (int k = 0; k <= N; ++k) {
           const double* stk = c.st(k);
@@ -649,10 +661,11 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
             if (sx.mu != 0.0) mus += (bx.lu + aa * dx.dlu) * (bx.tu + aa * dx.dtu);
           }
         }
-        const double mu_aff = gsum(lane < kMaxDim ? mus : 0.0) * nc_inv;
+        mu_aff = gsum(lane < kMaxDim ? mus : 0.0) * nc_inv;
         double sg = mu > 0.0 ? mu_aff / mu : 0.0;
         sg = sg * sg * sg;
         if (sg > 1.0) sg = 1.0;
+        sigma = sg;
         sigma_mu = sg * mu;
         // ---- B2: corrector vectors (element-owned recursion) ----
         double pnext = 0.0;  // p_{k+1}, element-owned
@@ -825,6 +838,14 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
     alpha_p = fmin(1.0, kStepTau * ap);
     alpha_d = fmin(1.0, kStepTau * ad);
     last_amin = fmin(alpha_p, alpha_d);
+    if (stat_row) {
+      double* next = stat_row + kStatCols;  // HPIPM stores step kk in row kk+1
+      next[0] = alpha_aff;
+      next[1] = mu_aff;
+      next[2] = sigma;
+      next[3] = alpha_p;
+      next[4] = alpha_d;
+    }
     ++iter;
   }
 

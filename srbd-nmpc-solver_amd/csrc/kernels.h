@@ -30,6 +30,7 @@ struct ProblemArgs {
   double *x, *u, *pi, *P, *p, *K, *k;
   int *status, *iter;
   double *res, *obj;
+  double* stat;  // [batch][iter_max+2][kStatCols] or null
   // workspace
   double* ws;
   size_t ws_qp;  // doubles per QP
@@ -38,6 +39,8 @@ struct ProblemArgs {
   int iter_max, pred_corr, split_step, warm_start;
   double alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp;
 };
+
+constexpr int kStatCols = 18;  // HPIPM ws->stat row width
 
 // IPM per-stage workspace layout (doubles), see ipm_box.hip.
 constexpr int kRecL = 0, kRecK = 144, kRecAcl = 288, kRecP = 432, kRecRs = 576, kRecKv = 588,

@@ -225,6 +225,7 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   a.x = s->x; a.u = s->u; a.pi = s->pi;
   a.P = s->P; a.p = s->p; a.K = s->K; a.k = s->k;
   a.status = s->status; a.iter = s->iter; a.res = s->res; a.obj = s->obj;
+  a.stat = s->stat;
   a.ws = h->ws;
   a.ws_qp = h->ws_qp;
   a.reg = st->reg_prim;
@@ -238,8 +239,12 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   a.tol_eq = st->tol_eq;
   a.tol_ineq = st->tol_ineq;
   a.tol_comp = st->tol_comp;
-  hipError_t e;
-  if (constrained(h->dims)) {
+  hipError_t e = hipSuccess;
+  if (s->stat)
+    e = hipMemsetAsync(s->stat, 0,
+                       sizeof(double) * srbd::kStatCols * (size_t)(st->iter_max + 2) * (size_t)batch, strm);
+  if (e != hipSuccess) {
+  } else if (constrained(h->dims)) {
     e = srbd::launch_ipm_box(a, strm);
   } else {
     e = srbd::launch_riccati_unconstr(a, strm);
@@ -316,6 +321,7 @@ int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* 
          oK = addo(s->K, B * N * nu * nx * D), ok = addo(s->k, B * N * nu * D);
   size_t ost = addo(s->status, B * sizeof(int)), oit = addo(s->iter, B * sizeof(int));
   size_t ores = addo(s->res, B * 4 * D), oobj = addo(s->obj, B * D);
+  size_t ostat = addo(s->stat, B * srbd::kStatCols * (size_t)(st->iter_max + 2) * D);
 
   int prev = 0;
   hipGetDevice(&prev);
@@ -355,6 +361,7 @@ int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* 
   srbd_qp_solution_f64 ss{};
   ss.x = dp(ox); ss.u = dp(ou); ss.pi = dp(opi); ss.P = dp(oP); ss.p = dp(op); ss.K = dp(oK);
   ss.k = dp(ok); ss.status = ip(ost); ss.iter = ip(oit); ss.res = dp(ores); ss.obj = dp(oobj);
+  ss.stat = dp(ostat);
   hipSetDevice(prev);
   rc = srbd_qp_solve_f64(h, batch, st, &dd, &ss, nullptr);
   if (rc) return rc;

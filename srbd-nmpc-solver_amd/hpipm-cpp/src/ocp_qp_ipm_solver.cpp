@@ -1,0 +1,448 @@
+// hpipm::OcpQpIpmSolver over the MI355X C-ABI (include/srbd_qp.h).
+//
+// The reference (hpipm-cpp/src/ocp_qp_ipm_solver.cpp:181-414) hands per-stage
+// Eigen pointers to HPIPM, calls d_ocp_qp_ipm_solve, reads the solution and
+// Riccati factors back and rebuilds stage 0 on the host.  Here the stages of
+// every QP of the batch are packed into the C-ABI's batch/stage-major
+// buffers, one srbd_qp_solve_host_f64 call runs the whole batch on the GPU
+// (x0 elimination and the stage-0 rebuild happen inside the kernel), and the
+// results are unpacked into OcpQpSolution / OcpQpIpmSolverStatistics.
+#include "hpipm-cpp/ocp_qp_ipm_solver.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "srbd_qp.h"
+
+namespace hpipm {
+
+std::string to_string(const HpipmStatus& hpipm_status) {
+  switch (hpipm_status) {
+    case HpipmStatus::Success:
+      return "HpipmStatus::Success";
+    case HpipmStatus::MaxIterReached:
+      return "HpipmStatus::MaxIterReached";
+    case HpipmStatus::MinStepLengthReached:
+      return "HpipmStatus::MinStepLengthReached";
+    case HpipmStatus::NaNDetected:
+      return "HpipmStatus::NaNDetected";
+    default:
+      return "HpipmStatus::UnknownFailure";
+  }
+}
+
+std::ostream& operator<<(std::ostream& os, const HpipmStatus& hpipm_status) {
+  return os << to_string(hpipm_status);
+}
+
+namespace {
+
+[[noreturn]] void abi_error(const char* what) {
+  throw std::runtime_error(std::string(what) + ": " + srbd_qp_last_error());
+}
+
+void copy_block(std::vector<double>& dst, size_t off, const double* src, size_t n) {
+  if (n) std::memcpy(dst.data() + off, src, n * sizeof(double));
+}
+
+// Uniform stage dimensions of one problem (the C-ABI's model).
+struct Shape {
+  int N = 0, nx = 0, nu = 0, ng = 0;
+  bool box_u = false, box_x = false;
+  bool operator==(const Shape& o) const {
+    return N == o.N && nx == o.nx && nu == o.nu && ng == o.ng && box_u == o.box_u &&
+           box_x == o.box_x;
+  }
+  bool operator!=(const Shape& o) const { return !(*this == o); }
+};
+
+Shape shape_of(const OcpQpDim& d) {
+  Shape s;
+  s.N = static_cast<int>(d.N);
+  s.nx = d.nx[0];
+  s.nu = d.N > 0 ? d.nu[0] : 0;
+  for (unsigned int i = 0; i <= d.N; ++i) {
+    if (d.nx[i] != s.nx)
+      throw std::runtime_error("OcpQpIpmSolver: nx must be uniform over the stages (nx[" +
+                               std::to_string(i) + "] = " + std::to_string(d.nx[i]) +
+                               ", nx[0] = " + std::to_string(s.nx) + ")");
+    if (i < d.N && d.nu[i] != s.nu)
+      throw std::runtime_error("OcpQpIpmSolver: nu must be uniform over the stages (nu[" +
+                               std::to_string(i) + "] = " + std::to_string(d.nu[i]) +
+                               ", nu[0] = " + std::to_string(s.nu) + ")");
+    if (d.nsbx[i] != 0 || d.nsbu[i] != 0 || d.nsg[i] != 0)
+      throw std::runtime_error("OcpQpIpmSolver: soft constraints are not supported");
+    s.ng = std::max(s.ng, d.ng[i]);
+    if (i < d.N && d.nbu[i] > 0) s.box_u = true;
+    if (i > 0 && d.nbx[i] > 0) s.box_x = true;  // stage-0 x bounds: eliminated with x0
+  }
+  return s;
+}
+
+}  // namespace
+
+struct OcpQpIpmSolver::Impl {
+  OcpQpIpmSolverSettings settings;
+  OcpQpIpmSolverStatistics stats;
+  std::vector<OcpQpIpmSolverStatistics> batch_stats;
+  OcpQpDim dim;
+  int device = 0;
+  srbd_qp_handle handle = nullptr;
+  Shape shape;
+  int capacity = 0;
+  // host staging (batch/stage-major, column-major blocks)
+  std::vector<double> A, B, b, Q, S, R, q, r, x0;
+  std::vector<double> lbu, ubu, lbu_m, ubu_m, lbx, ubx, lbx_m, ubx_m;
+  std::vector<double> C, D, lg, ug, lg_m, ug_m;
+  std::vector<double> x, u, pi, P, p, K, k, res, obj, stat;
+  std::vector<int> status, iter;
+
+  ~Impl() { release(); }
+  void release() {
+    if (handle) srbd_qp_destroy(handle);
+    handle = nullptr;
+    capacity = 0;
+  }
+
+  void ensure_handle(const Shape& s, int batch) {
+    if (handle && s == shape && batch <= capacity) return;
+    release();
+    srbd_qp_dims d{s.N, s.nx, s.nu, s.ng, s.box_u ? 1 : 0, s.box_x ? 1 : 0};
+    if (srbd_qp_create(&d, std::max(batch, 1), device, &handle) != SRBD_QP_OK) {
+      handle = nullptr;
+      abi_error("OcpQpIpmSolver::resize");
+    }
+    shape = s;
+    capacity = std::max(batch, 1);
+  }
+
+  srbd_qp_settings abi_settings() const {
+    srbd_qp_settings s;
+    srbd_qp_default_settings(&s);
+    s.mode = static_cast<int>(settings.mode);
+    s.iter_max = settings.iter_max;
+    s.alpha_min = settings.alpha_min;
+    s.mu0 = settings.mu0;
+    s.tol_stat = settings.tol_stat;
+    s.tol_eq = settings.tol_eq;
+    s.tol_ineq = settings.tol_ineq;
+    s.tol_comp = settings.tol_comp;
+    s.reg_prim = settings.reg_prim;
+    s.warm_start = settings.warm_start;
+    s.pred_corr = settings.pred_corr;
+    s.ric_alg = settings.ric_alg;
+    s.split_step = settings.split_step;
+    return s;
+  }
+
+  void pack(const std::vector<VectorXd>& x0s, const std::vector<std::vector<OcpQp>>& qps,
+            const std::vector<std::vector<OcpQpSolution>>* warm);
+  std::vector<HpipmStatus> unpack(std::vector<std::vector<OcpQpSolution>>& sols);
+};
+
+void OcpQpIpmSolver::Impl::pack(const std::vector<VectorXd>& x0s,
+                                const std::vector<std::vector<OcpQp>>& qps,
+                                const std::vector<std::vector<OcpQpSolution>>* warm) {
+  const size_t nb = qps.size(), N = shape.N, nx = shape.nx, nu = shape.nu, ng = shape.ng;
+  auto sized = [](std::vector<double>& v, size_t n) { v.assign(n, 0.0); };
+  sized(A, nb * N * nx * nx);
+  sized(B, nb * N * nx * nu);
+  sized(b, nb * N * nx);
+  sized(Q, nb * (N + 1) * nx * nx);
+  sized(S, nb * N * nu * nx);
+  sized(R, nb * N * nu * nu);
+  sized(q, nb * (N + 1) * nx);
+  sized(r, nb * N * nu);
+  sized(x0, nb * nx);
+  if (shape.box_u) {
+    for (auto* v : {&lbu, &ubu, &lbu_m, &ubu_m}) sized(*v, nb * N * nu);
+  }
+  if (shape.box_x) {
+    for (auto* v : {&lbx, &ubx, &lbx_m, &ubx_m}) sized(*v, nb * (N + 1) * nx);
+  }
+  if (ng) {
+    sized(C, nb * (N + 1) * ng * nx);
+    sized(D, nb * N * ng * nu);
+    for (auto* v : {&lg, &ug, &lg_m, &ug_m}) sized(*v, nb * (N + 1) * ng);
+  }
+  for (size_t bi = 0; bi < nb; ++bi) {
+    const std::vector<OcpQp>& qp = qps[bi];
+    if (static_cast<size_t>(x0s[bi].size()) != nx)
+      throw std::runtime_error("x0.size() must be " + std::to_string(nx));
+    copy_block(x0, bi * nx, x0s[bi].data(), nx);
+    for (size_t k = 0; k <= N; ++k) {
+      const OcpQp& s = qp[k];
+      const size_t sk = bi * (N + 1) + k;  // stage index, N+1 stages
+      copy_block(Q, sk * nx * nx, s.Q.data(), nx * nx);
+      copy_block(q, sk * nx, s.q.data(), nx);
+      if (k < N) {
+        const size_t si = bi * N + k;  // stage index, N stages
+        copy_block(A, si * nx * nx, s.A.data(), nx * nx);
+        copy_block(B, si * nx * nu, s.B.data(), nx * nu);
+        copy_block(b, si * nx, s.b.data(), nx);
+        copy_block(S, si * nu * nx, s.S.data(), nu * nx);
+        copy_block(R, si * nu * nu, s.R.data(), nu * nu);
+        copy_block(r, si * nu, s.r.data(), nu);
+        if (shape.box_u) {
+          // index form -> dense per-variable bounds + masks (include/srbd_qp.h)
+          for (size_t j = 0; j < s.idxbu.size(); ++j) {
+            const int v = s.idxbu[j];
+            if (v < 0 || static_cast<size_t>(v) >= nu)
+              throw std::runtime_error("ocp_qp[" + std::to_string(k) + "].idxbu[" +
+                                       std::to_string(j) + "] out of range");
+            const size_t o = si * nu + v;
+            lbu[o] = s.lbu[j];
+            ubu[o] = s.ubu[j];
+            lbu_m[o] = s.lbu_mask.size() ? s.lbu_mask[j] : 1.0;
+            ubu_m[o] = s.ubu_mask.size() ? s.ubu_mask[j] : 1.0;
+          }
+        }
+        if (ng && s.D.size()) {
+          // pad to ng rows: column-major ng x nu block, extra rows stay 0
+          const size_t rows = s.D.rows();
+          for (size_t c = 0; c < nu; ++c)
+            for (size_t rr = 0; rr < rows; ++rr)
+              D[si * ng * nu + c * ng + rr] = s.D.data()[c * rows + rr];
+        }
+      }
+      if (shape.box_x && k > 0) {
+        for (size_t j = 0; j < s.idxbx.size(); ++j) {
+          const int v = s.idxbx[j];
+          if (v < 0 || static_cast<size_t>(v) >= nx)
+            throw std::runtime_error("ocp_qp[" + std::to_string(k) + "].idxbx[" +
+                                     std::to_string(j) + "] out of range");
+          const size_t o = sk * nx + v;
+          lbx[o] = s.lbx[j];
+          ubx[o] = s.ubx[j];
+          lbx_m[o] = s.lbx_mask.size() ? s.lbx_mask[j] : 1.0;
+          ubx_m[o] = s.ubx_mask.size() ? s.ubx_mask[j] : 1.0;
+        }
+      }
+      if (ng) {
+        const size_t rows = s.lg.size();
+        if (rows && s.C.size()) {
+          for (size_t c = 0; c < nx; ++c)
+            for (size_t rr = 0; rr < rows; ++rr)
+              C[sk * ng * nx + c * ng + rr] = s.C.data()[c * rows + rr];
+        }
+        for (size_t rr = 0; rr < rows; ++rr) {
+          const size_t o = sk * ng + rr;
+          lg[o] = s.lg[rr];
+          ug[o] = s.ug[rr];
+          lg_m[o] = s.lg_mask.size() ? s.lg_mask[rr] : 1.0;
+          ug_m[o] = s.ug_mask.size() ? s.ug_mask[rr] : 1.0;
+        }
+      }
+    }
+  }
+  // outputs (x/u double as the warm start when settings.warm_start)
+  sized(x, nb * (N + 1) * nx);
+  sized(u, nb * N * nu);
+  sized(pi, nb * (N + 1) * nx);
+  sized(P, nb * (N + 1) * nx * nx);
+  sized(p, nb * (N + 1) * nx);
+  sized(K, nb * N * nu * nx);
+  sized(k, nb * N * nu);
+  sized(res, nb * 4);
+  sized(obj, nb);
+  sized(stat, nb * (settings.iter_max + 2) * 18);
+  status.assign(nb, -1);
+  iter.assign(nb, 0);
+  if (warm) {
+    for (size_t bi = 0; bi < nb; ++bi) {
+      const std::vector<OcpQpSolution>& w = (*warm)[bi];
+      for (size_t kk = 0; kk < N; ++kk) {
+        copy_block(x, (bi * (N + 1) + kk + 1) * nx, w[kk + 1].x.data(), nx);
+        copy_block(u, (bi * N + kk) * nu, w[kk].u.data(), nu);
+      }
+    }
+  }
+}
+
+std::vector<HpipmStatus> OcpQpIpmSolver::Impl::unpack(
+    std::vector<std::vector<OcpQpSolution>>& sols) {
+  const size_t nb = sols.size(), N = shape.N, nx = shape.nx, nu = shape.nu;
+  const size_t rows = static_cast<size_t>(settings.iter_max) + 2;
+  std::vector<HpipmStatus> out(nb);
+  batch_stats.resize(nb);
+  for (size_t bi = 0; bi < nb; ++bi) {
+    std::vector<OcpQpSolution>& sol = sols[bi];
+    for (size_t kk = 0; kk <= N; ++kk) {
+      OcpQpSolution& s = sol[kk];
+      const size_t sk = bi * (N + 1) + kk;
+      s.x.resize(nx);
+      s.pi.resize(nx);
+      s.P.resize(nx, nx);
+      s.p.resize(nx);
+      std::memcpy(s.x.data(), x.data() + sk * nx, nx * sizeof(double));
+      std::memcpy(s.pi.data(), pi.data() + sk * nx, nx * sizeof(double));
+      std::memcpy(s.P.data(), P.data() + sk * nx * nx, nx * nx * sizeof(double));
+      std::memcpy(s.p.data(), p.data() + sk * nx, nx * sizeof(double));
+      if (kk < N) {
+        const size_t si = bi * N + kk;
+        s.u.resize(nu);
+        s.K.resize(nu, nx);
+        s.k.resize(nu);
+        std::memcpy(s.u.data(), u.data() + si * nu, nu * sizeof(double));
+        std::memcpy(s.K.data(), K.data() + si * nu * nx, nu * nx * sizeof(double));
+        std::memcpy(s.k.data(), k.data() + si * nu, nu * sizeof(double));
+      } else {
+        s.k.resize(0);  // nu[N] = 0 (ocp_qp_ipm_solver.cpp:221-223)
+      }
+    }
+    OcpQpIpmSolverStatistics& st = batch_stats[bi];
+    st.iter = iter[bi];
+    st.max_res_stat = res[bi * 4 + 0];
+    st.max_res_eq = res[bi * 4 + 1];
+    st.max_res_ineq = res[bi * 4 + 2];
+    st.max_res_comp = res[bi * 4 + 3];
+    st.clear();
+    const size_t nrow = std::min(rows, static_cast<size_t>(st.iter) + 2);
+    st.reserve(nrow);
+    std::vector<double>* cols[] = {
+        &st.alpha_aff, &st.mu_aff, &st.sigma, &st.alpha_prim, &st.alpha_dual, &st.mu,
+        &st.res_stat, &st.res_eq, &st.res_ineq, &st.res_comp, &st.obj, &st.lq_fact,
+        &st.itref_pred, &st.itref_corr, &st.lin_res_stat, &st.lin_res_eq, &st.lin_res_ineq,
+        &st.lin_res_comp};
+    for (size_t i = 0; i < nrow; ++i)
+      for (size_t c = 0; c < 18; ++c) cols[c]->push_back(stat[(bi * rows + i) * 18 + c]);
+    const int code = status[bi];
+    out[bi] = (code >= 0 && code <= 3) ? static_cast<HpipmStatus>(code) : HpipmStatus::UnknownFailure;
+  }
+  if (nb) stats = batch_stats[0];
+  return out;
+}
+
+OcpQpIpmSolver::OcpQpIpmSolver(const std::vector<OcpQp>& ocp_qp,
+                               const OcpQpIpmSolverSettings& solver_settings)
+    : impl_(new Impl()) {
+  setSolverSettings(solver_settings);
+  resize(ocp_qp);
+}
+
+OcpQpIpmSolver::OcpQpIpmSolver(const OcpQpIpmSolverSettings& solver_settings) : impl_(new Impl()) {
+  setSolverSettings(solver_settings);
+}
+
+OcpQpIpmSolver::~OcpQpIpmSolver() = default;
+OcpQpIpmSolver::OcpQpIpmSolver(OcpQpIpmSolver&&) noexcept = default;
+OcpQpIpmSolver& OcpQpIpmSolver::operator=(OcpQpIpmSolver&&) noexcept = default;
+
+void OcpQpIpmSolver::setSolverSettings(const OcpQpIpmSolverSettings& solver_settings) {
+  solver_settings.checkSettings();
+  impl_->settings = solver_settings;
+}
+
+void OcpQpIpmSolver::resize(const std::vector<OcpQp>& ocp_qp) {
+  impl_->dim.resize(ocp_qp);
+  impl_->ensure_handle(shape_of(impl_->dim), std::max(impl_->capacity, 1));
+}
+
+HpipmStatus OcpQpIpmSolver::solve(const VectorXd& x0, std::vector<OcpQp>& ocp_qp,
+                                  std::vector<OcpQpSolution>& qp_sol) {
+  std::vector<VectorXd> x0s{x0};
+  std::vector<std::vector<OcpQp>> qps(1);
+  qps[0].swap(ocp_qp);
+  std::vector<std::vector<OcpQpSolution>> sols(1);
+  sols[0].swap(qp_sol);
+  struct Restore {  // hand the caller's vectors back even when solveBatch throws
+    std::vector<OcpQp>& a;
+    std::vector<OcpQpSolution>& b;
+    std::vector<std::vector<OcpQp>>& qa;
+    std::vector<std::vector<OcpQpSolution>>& qb;
+    ~Restore() {
+      a.swap(qa[0]);
+      b.swap(qb[0]);
+    }
+  } restore{ocp_qp, qp_sol, qps, sols};
+  return solveBatch(x0s, qps, sols)[0];
+}
+
+std::vector<HpipmStatus> OcpQpIpmSolver::solveBatch(
+    const std::vector<VectorXd>& x0, std::vector<std::vector<OcpQp>>& ocp_qp,
+    std::vector<std::vector<OcpQpSolution>>& qp_sol) {
+  Impl& m = *impl_;
+  if (ocp_qp.empty()) throw std::runtime_error("ocp_qp must hold at least one QP");
+  if (x0.size() != ocp_qp.size())
+    throw std::runtime_error("x0.size() must be " + std::to_string(ocp_qp.size()));
+  // dimensions: the first QP sets them, every other QP must match
+  m.dim.resize(ocp_qp[0]);
+  const Shape s0 = shape_of(m.dim);
+  Shape s = s0;
+  for (size_t bi = 1; bi < ocp_qp.size(); ++bi) {
+    OcpQpDim d(ocp_qp[bi]);
+    Shape si = shape_of(d);
+    if (si.N != s0.N || si.nx != s0.nx || si.nu != s0.nu)
+      throw std::runtime_error("ocp_qp[" + std::to_string(bi) +
+                               "]: every QP of a batch must have the same N, nx, nu");
+    s.ng = std::max(s.ng, si.ng);
+    s.box_u = s.box_u || si.box_u;
+    s.box_x = s.box_x || si.box_x;
+  }
+  const int nb = static_cast<int>(ocp_qp.size());
+  m.ensure_handle(s, nb);
+  // solution containers (ocp_qp_ipm_solver.cpp:186-223)
+  if (qp_sol.size() != ocp_qp.size()) qp_sol.resize(ocp_qp.size());
+  for (size_t bi = 0; bi < qp_sol.size(); ++bi) {
+    std::vector<OcpQpSolution>& sol = qp_sol[bi];
+    if (sol.size() != static_cast<size_t>(s.N) + 1) sol.resize(s.N + 1);
+    if (m.settings.warm_start) {
+      for (int i = 0; i <= s.N; ++i)
+        if (sol[i].x.size() != s.nx)
+          throw std::runtime_error("qp_sol[" + std::to_string(i) + "].x.size() must be " +
+                                   std::to_string(s.nx));
+      for (int i = 0; i < s.N; ++i)
+        if (sol[i].u.size() != s.nu)
+          throw std::runtime_error("qp_sol[" + std::to_string(i) + "].u.size() must be " +
+                                   std::to_string(s.nu));
+    }
+  }
+  m.pack(x0, ocp_qp, m.settings.warm_start ? &qp_sol : nullptr);
+  auto ptr = [](std::vector<double>& v) -> double* { return v.empty() ? nullptr : v.data(); };
+  srbd_qp_data_f64 d{};
+  d.A = m.A.data(); d.B = m.B.data(); d.b = m.b.data();
+  d.Q = m.Q.data(); d.S = m.S.data(); d.R = m.R.data();
+  d.q = m.q.data(); d.r = m.r.data(); d.x0 = m.x0.data();
+  if (s.box_u) {
+    d.lbu = ptr(m.lbu); d.ubu = ptr(m.ubu); d.lbu_mask = ptr(m.lbu_m); d.ubu_mask = ptr(m.ubu_m);
+  }
+  if (s.box_x) {
+    d.lbx = ptr(m.lbx); d.ubx = ptr(m.ubx); d.lbx_mask = ptr(m.lbx_m); d.ubx_mask = ptr(m.ubx_m);
+  }
+  if (s.ng) {
+    d.C = ptr(m.C); d.D = ptr(m.D); d.lg = ptr(m.lg); d.ug = ptr(m.ug);
+    d.lg_mask = ptr(m.lg_m); d.ug_mask = ptr(m.ug_m);
+  }
+  srbd_qp_solution_f64 o{};
+  o.x = m.x.data(); o.u = m.u.data(); o.pi = m.pi.data();
+  o.P = m.P.data(); o.p = m.p.data(); o.K = m.K.data(); o.k = m.k.data();
+  o.status = m.status.data(); o.iter = m.iter.data(); o.res = m.res.data(); o.obj = m.obj.data();
+  o.stat = m.stat.data();
+  const srbd_qp_settings st = m.abi_settings();
+  if (srbd_qp_solve_host_f64(m.handle, nb, &st, &d, &o) != SRBD_QP_OK)
+    abi_error("OcpQpIpmSolver::solve");
+  return m.unpack(qp_sol);
+}
+
+const OcpQpIpmSolverSettings& OcpQpIpmSolver::getIpmSolverSettings() const {
+  return impl_->settings;
+}
+
+const OcpQpIpmSolverStatistics& OcpQpIpmSolver::getSolverStatistics() const {
+  return impl_->stats;
+}
+
+const std::vector<OcpQpIpmSolverStatistics>& OcpQpIpmSolver::getBatchStatistics() const {
+  return impl_->batch_stats;
+}
+
+void OcpQpIpmSolver::setDevice(int device) {
+  if (device != impl_->device) impl_->release();
+  impl_->device = device;
+}
+
+int OcpQpIpmSolver::device() const { return impl_->device; }
+
+}  // namespace hpipm

@@ -126,3 +126,23 @@ def test_max_iter_status(pkg):
     qp, x0 = pkg.srbd_model.generate_batch(8, N=10, seed=5, constraints="box_u")
     out = pkg.capi.solve(qp, x0, dict(iter_max=2))
     assert np.all(out["status"] == 1) and np.all(out["iter"] == 2)
+
+
+def test_iteration_statistics(pkg, oracle):
+    """Per-iteration stat rows (HPIPM ws->stat layout): row 0 holds the initial
+    residuals, row i+1 the step of iteration i; the last filled row matches the
+    final residual norms, mu decreases, step lengths lie in (0, 1]."""
+    qp, x0 = pkg.srbd_model.generate_batch(16, N=20, seed=3, constraints="box_u")
+    st = dict(iter_max=30)
+    out = pkg.capi.solve(qp, x0, st, stats=True)
+    assert out["stat"].shape == (16, 32, 18)
+    for i in range(16):
+        it = int(out["iter"][i])
+        S = out["stat"][i]
+        assert it > 0
+        np.testing.assert_array_equal(S[it, 6:10], out["res"][i])
+        assert S[it, 10] == out["obj"][i]
+        assert np.all(S[1:it + 1, 3] > 0) and np.all(S[1:it + 1, 3] <= 1)   # alpha_prim
+        assert np.all(S[1:it + 1, 2] >= 0) and np.all(S[1:it + 1, 2] <= 1)  # sigma
+        assert S[it, 5] < S[0, 5]                                           # mu decreased
+        assert np.all(S[it + 1:] == 0) and np.all(S[:, 11:] == 0)

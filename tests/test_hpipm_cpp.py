@@ -1,0 +1,38 @@
+"""The hpipm-cpp C++ interface (srbd-nmpc-solver_amd/hpipm-cpp) through its
+compiled test program build/hpipm_cpp_test, a port of the reference's
+hpipm-cpp/test/ocp_qp_ipm_solver.cpp (unconstrained, constrained,
+compareResults) plus interface checks.
+
+CPU: dimension / settings error behaviour (no device work).
+GPU: the solver cases, every solve a kernel launch through libsrbd_qp.so."""
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+EXE = ROOT / "build" / "hpipm_cpp_test"
+GOLDEN = ROOT / "tests" / "golden"
+
+GPU_CASES = ["unconstrained", "constrained_box", "compareResults", "batch_matches_single"]
+
+
+def _run(args, timeout):
+    if not EXE.exists():
+        pytest.fail(f"{EXE} not built (run `make` or __graft_entry__.build())")
+    r = subprocess.run([str(EXE), "--golden", str(GOLDEN)] + args, capture_output=True,
+                       text=True, timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    return r.stdout
+
+
+def test_interface_errors_cpu():
+    out = _run(["--cpu-only"], 60)
+    assert "0 failed" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", GPU_CASES)
+def test_solver_cases_gpu(case):
+    out = _run([case], 300)
+    assert "1 cases, 0 failed" in out
