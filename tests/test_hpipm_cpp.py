@@ -14,7 +14,8 @@ ROOT = Path(__file__).resolve().parents[1]
 EXE = ROOT / "build" / "hpipm_cpp_test"
 GOLDEN = ROOT / "tests" / "golden"
 
-GPU_CASES = ["unconstrained", "constrained_box", "compareResults", "batch_matches_single"]
+GPU_CASES = ["unconstrained", "constrained_box", "constrained", "compareResults",
+             "batch_matches_single"]
 
 
 def _run(args, timeout):
