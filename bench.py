@@ -81,8 +81,9 @@ def make_shard(pkg, N, constraints, batch, rank, seed, pool):
     """Distinct QPs for this rank: a pool of `pool` QPs generated from
     seed + global index, tiled to `batch` (addresses distinct, data repeats)."""
     pool = min(pool, batch)
+    first, _ = pkg.dist.shard_range(rank, batch)
     qp, x0 = pkg.srbd_model.generate_batch(pool, N=N, seed=seed, constraints=constraints,
-                                           first=rank * batch)
+                                           first=first)
     return qp, x0
 
 
@@ -175,10 +176,7 @@ def main():
         dist.barrier()
     t_wall = time.perf_counter() - t_start
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    t_tensor = torch.tensor([t_wall], dtype=torch.float64, device=device)
-    if distributed:
-        dist.all_reduce(t_tensor, op=dist.ReduceOp.MAX)
-    t_max = float(t_tensor.item())
+    t_max = pkg.dist.max_over_ranks(t_wall, device)
     status = sol_t["status"].cpu().numpy()
     iters = sol_t["iter"].cpu().numpy()
     n_ok = int((status == 0).sum())
@@ -188,15 +186,13 @@ def main():
     # ---- solution gather to rank 0 over RCCL (BASELINE config 4) ----
     gather_ms = None
     if distributed and not args.no_gather:
-        payload = torch.cat([sol_t["x"].reshape(batch, -1), sol_t["u"].reshape(batch, -1),
-                             sol_t["pi"].reshape(batch, -1)], dim=1).contiguous()
-        bufs = [torch.empty_like(payload) for _ in range(world)] if rank == 0 else None
+        payload = pkg.dist.solution_payload(sol_t["x"], sol_t["u"], sol_t["pi"])
         dist.barrier()
         torch.cuda.synchronize()
         tg = time.perf_counter()
         reps = 5
         for _ in range(reps):
-            dist.gather(payload, bufs, dst=0)
+            pkg.dist.gather_to_root(payload, world, rank)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) / reps * 1e3
 

@@ -8,7 +8,11 @@ Python package is the host-side mirror used by tests and bench.py:
 
 * :class:`OcpQpBatch` -- batched ``hpipm::OcpQp`` in the C-ABI layout.
 * :mod:`.capi` -- ctypes binding of libsrbd_qp.so (device pointers from torch).
-* :class:`OcpQpIpmSolver` -- Python mirror of the reference solver facade.
+* :mod:`.srbd_model` -- seeded SRBD QP generator (the reference's linearisation).
+* :mod:`.dist` -- rank sharding / solution gather of the multi-GPU bench.
+
+The reference's C++ interface (``hpipm::OcpQpIpmSolver`` & co.) is rebuilt in
+``hpipm-cpp/`` (libhpipm-cpp.so) on top of the same C-ABI.
 
 There is no CPU fallback: every solve runs the HIP kernels and raises if the
 library or a GPU is missing.
@@ -20,10 +24,7 @@ __version__ = "0.1.0"
 
 def __getattr__(name):
     # lazy: importing the package must work on a CPU-only host (tests, build()).
-    if name in ("capi", "srbd_model", "solver"):
+    if name in ("capi", "srbd_model", "dist"):
         import importlib
         return importlib.import_module(f"{__name__}.{name}")
-    if name in ("OcpQpIpmSolver", "OcpQpIpmSolverSettings", "HpipmMode", "HpipmStatus", "solve_batch"):
-        from . import solver
-        return getattr(solver, name)
     raise AttributeError(name)
