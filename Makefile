@@ -44,8 +44,14 @@ $(LIB): $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
 oracle:
 	$(MAKE) -s -C oracle
 
+# A/B builds of the HIP library: make variant NAME=x VFLAGS="-DFOO=0"
+variant:
+	@mkdir -p build/variants/$(NAME)
+	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $$f -o build/variants/$(NAME)/$$(basename $$f .hip).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/$(NAME)/libsrbd_qp.so build/variants/$(NAME)/*.o
+
 clean:
 	rm -rf build $(LIB)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean variant

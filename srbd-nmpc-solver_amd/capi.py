@@ -14,7 +14,9 @@ from typing import Dict, Optional
 import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "libsrbd_qp.so"
+# SRBD_QP_LIB: an alternative build of the same library (A/B experiments,
+# scripts/dev/ab_variants.py); default the in-tree product build
+LIB_PATH = Path(os.environ.get("SRBD_QP_LIB") or (PKG_DIR / "libsrbd_qp.so"))
 
 _dp = C.c_void_p
 

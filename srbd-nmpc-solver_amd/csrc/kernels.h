@@ -9,15 +9,23 @@
 namespace srbd {
 
 // Forward-pass record of one stage, written by the backward sweep and read
-// back (row-owned) by the forward sweep.  Row-major blocks so that lane i of
-// the forward pass loads row i as 96 contiguous bytes.
+// back (row-owned) by the forward sweep.  K and Acl are row-major so that lane
+// i of the forward pass loads row i as 96 contiguous bytes; the symmetric P is
+// packed (lower triangle by columns, 78 values: see packed_off).
 constexpr int kWsK = 0;      // K   [12][12] row-major (u-row i)
 constexpr int kWsAcl = 144;  // Acl [12][12] row-major
-constexpr int kWsP = 288;    // P   [12][12] (symmetric)
-constexpr int kWsk = 432;    // k   [12]
-constexpr int kWsbcl = 444;  // bcl [12]
-constexpr int kWsp = 456;    // p   [12]
-constexpr int kWsStage = 480;  // doubles per stage record (16-byte multiple)
+constexpr int kWsP = 288;    // P   packed lower triangle, 78
+constexpr int kWsk = 366;    // k   [12]
+constexpr int kWsbcl = 378;  // bcl [12]
+constexpr int kWsp = 390;    // p   [12]
+constexpr int kWsStage = 402;  // doubles per stage record (16-byte multiple)
+
+// offset of P[i][j] (i >= j) in the packed lower triangle: column j starts at
+// j*12 - j*(j-1)/2
+__host__ __device__ constexpr int packed_col(int j) { return j * 12 - j * (j - 1) / 2; }
+__host__ __device__ constexpr int packed_off(int i, int j) {
+  return i >= j ? packed_col(j) + (i - j) : packed_col(i) + (j - i);
+}
 
 struct ProblemArgs {
   int batch, N, nx, nu, ng;

@@ -20,6 +20,10 @@
 #include "kernels.h"
 #include "riccati.h"
 
+#ifndef SRBD_WS_STAGE_MAJOR
+#define SRBD_WS_STAGE_MAJOR 1
+#endif
+
 namespace srbd {
 
 namespace {
@@ -29,6 +33,24 @@ __device__ __forceinline__ void store_n(double* out, int n, const double (&v)[12
   sfor<0, 12>([&](auto i) {
     constexpr int I = decltype(i)::value;
     if (I < n) out[I] = v[I];
+  });
+}
+
+// lane j < 12 stores column j of the symmetric P (v[i] = P[i][j]) into the
+// packed lower triangle: entries i >= j only
+__device__ __forceinline__ void store_packed_col(double* pk, int lane, const double (&v)[12]) {
+  const int cj = packed_col(lane) - lane;
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    if (I >= lane) pk[cj + I] = v[I];
+  });
+}
+// row r of the symmetric P from the packed lower triangle
+__device__ __forceinline__ void load_packed_row(const double* pk, int r, double (&v)[12]) {
+  const int cr = packed_col(r) - r;
+  sfor<0, 12>([&](auto j) {
+    constexpr int J = decltype(j)::value;
+    v[J] = J <= r ? pk[packed_col(J) + r - J] : pk[cr + J];
   });
 }
 
@@ -60,15 +82,28 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgs a) {
   const double reg = a.reg;
 
   const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu, nuu = (size_t)nu * nu;
-  const double* Aq = a.A + (size_t)qp * N * nxx;
-  const double* Bq = a.B + (size_t)qp * N * nxu;
-  const double* bq = a.b + (size_t)qp * N * nx;
-  const double* Qq = a.Q + (size_t)qp * (N + 1) * nxx;
-  const double* Sq = a.S + (size_t)qp * N * nxu;
-  const double* Rq = a.R + (size_t)qp * N * nuu;
-  const double* qq = a.q + (size_t)qp * (N + 1) * nx;
-  const double* rq = a.r + (size_t)qp * N * nu;
-  double* ws = a.ws + (size_t)qp * a.ws_qp;
+#ifdef SRBD_DIAG_SHARED_INPUT  // diagnostic build only: every QP reads QP (qp & 63)'s data
+  const int qin = qp & 63;
+#else
+  const int qin = qp;
+#endif
+  const double* Aq = a.A + (size_t)qin * N * nxx;
+  const double* Bq = a.B + (size_t)qin * N * nxu;
+  const double* bq = a.b + (size_t)qin * N * nx;
+  const double* Qq = a.Q + (size_t)qin * (N + 1) * nxx;
+  const double* Sq = a.S + (size_t)qin * N * nxu;
+  const double* Rq = a.R + (size_t)qin * N * nuu;
+  const double* qq = a.q + (size_t)qin * (N + 1) * nx;
+  const double* rq = a.r + (size_t)qin * N * nu;
+  // forward records, stage-major: stage k of QP q at ws[(k * batch + q) * kWsStage], so the
+  // four QPs of a wavefront write / read one contiguous 15 KB block per stage
+  auto rec_at = [&](int k) -> double* {
+#if SRBD_WS_STAGE_MAJOR
+    return a.ws + ((size_t)k * a.batch + qp) * kWsStage;
+#else
+    return a.ws + (size_t)qp * a.ws_qp + (size_t)k * kWsStage;
+#endif
+  };
 
   StageLoader<FULL> ld{nx, nu};
   const bool xcol = lane < nx;  // lane owns a real state column
@@ -82,8 +117,8 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgs a) {
     ld.col(Qq + (size_t)N * nxx, nx, nx, col, xcol, P);
   }
   {
-    double* rec = ws + (size_t)N * kWsStage;
-    if (lane < kMaxDim) store12(rec + kWsP + lane * 12, P);
+    double* rec = rec_at(N);
+    if (lane < kMaxDim) store_packed_col(rec + kWsP, lane, P);
     if (isv) store12(rec + kWsp, P);
     if (a.P && xcol) store_n(a.P + ((size_t)qp * (N + 1) + N) * nxx + (size_t)lane * nx, nx, P);
     if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + N) * nx, nx, P);
@@ -126,14 +161,18 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgs a) {
     StageFactor<double> f;
     riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
 
-    double* rec = ws + (size_t)k * kWsStage;
+    double* rec = rec_at(k);
+#ifdef SRBD_DIAG_NO_RECORD  // diagnostic build only: no record traffic
+    if (k == -7) {
+#else
     if (lane < kMaxDim) {
+#endif
       sfor<0, 12>([&](auto m) {
         constexpr int M = decltype(m)::value;
         rec[kWsK + M * 12 + lane] = f.Kc[M];
         rec[kWsAcl + M * 12 + lane] = A_[M];
       });
-      store12(rec + kWsP + lane * 12, f.F);
+      store_packed_col(rec + kWsP, lane, f.F);
     }
     if (isv) {
       store12(rec + kWsk, f.Kc);
@@ -151,18 +190,35 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgs a) {
   }
 
   // ---------------- forward sweep (row-owned) ----------------
+  // The record rows of stage k+1 are loaded while stage k computes (the loads
+  // do not depend on x), so each stage pays one memory latency less.
   const int row = lane < kMaxDim ? lane : kMaxDim - 1;
   double xv = (lane < nx) ? a.x0[(size_t)qp * nx + lane] : 0.0;
   bool bad = false;
   double* xo = a.x + (size_t)qp * (N + 1) * nx;
   double* uo = a.u + (size_t)qp * N * nu;
   double* po = a.pi + (size_t)qp * (N + 1) * nx;
+  double Pr[12], Kr[12], Ar[12], pv, kv, bv;
+  auto load_rows = [&](int k, double (&P_)[12], double (&K_)[12], double (&A__)[12], double& p_,
+                       double& k_, double& b_) {
+    const double* rec = rec_at(k);
+    load_packed_row(rec + kWsP, row, P_);
+    p_ = rec[kWsp + row];
+    if (k < N) {
+      load12(rec + kWsK + row * 12, K_);
+      load12(rec + kWsAcl + row * 12, A__);
+      k_ = rec[kWsk + row];
+      b_ = rec[kWsbcl + row];
+    }
+  };
+  load_rows(0, Pr, Kr, Ar, pv, kv, bv);
+#ifdef SRBD_DIAG_NO_FWD  // diagnostic build only
+  if (N > 0) return;
+#endif
 #pragma unroll 1
   for (int k = 0; k <= N; ++k) {
-    const double* rec = ws + (size_t)k * kWsStage;
-    double Pr[12];
-    load12(rec + kWsP + row * 12, Pr);
-    const double pv = rec[kWsp + row];
+    double Pn[12], Kn[12], An[12], pvn = 0.0, kvn = 0.0, bvn = 0.0;
+    if (k < N) load_rows(k + 1, Pn, Kn, An, pvn, kvn, bvn);
     double bx[12];
     sfor<0, 12>([&](auto j) {
       constexpr int J = decltype(j)::value;
@@ -178,11 +234,7 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgs a) {
       po[(size_t)k * nx + lane] = pp;
     }
     if (k == N) break;
-    double Kr[12], Ar[12];
-    load12(rec + kWsK + row * 12, Kr);
-    load12(rec + kWsAcl + row * 12, Ar);
-    double uu = rec[kWsk + row];
-    double xn = rec[kWsbcl + row];
+    double uu = kv, xn = bv;
     sfor<0, 12>([&](auto j) {
       constexpr int J = decltype(j)::value;
       uu = fmadd(Kr[J], bx[J], uu);
@@ -191,6 +243,15 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgs a) {
     if (lane < nu) uo[(size_t)k * nu + lane] = uu;
     bad |= (lane < nu && !(uu == uu)) || (lane < nx && !(xn == xn));
     xv = xn;
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      Pr[J] = Pn[J];
+      Kr[J] = Kn[J];
+      Ar[J] = An[J];
+    });
+    pv = pvn;
+    kv = kvn;
+    bv = bvn;
   }
   if (a.status || a.iter) {
     const unsigned long long m = __ballot(bad);
