@@ -289,6 +289,19 @@ __device__ __forceinline__ void ratio(const Side& s, const Bar& b, const BarStep
   }
 }
 
+// predictor sums for mu_aff: s1 += lam dt + t dlam, s2 += dlam dt (active sides)
+__device__ __forceinline__ void aff_sums(const Side& s, const Bar& b, const BarStep& d, double& s1,
+                                         double& s2) {
+  if (s.ml != 0.0) {
+    s1 += b.ll * d.dtl + b.tl * d.dll;
+    s2 += d.dll * d.dtl;
+  }
+  if (s.mu != 0.0) {
+    s1 += b.lu * d.dtu + b.tu * d.dlu;
+    s2 += d.dlu * d.dtu;
+  }
+}
+
 // gather an element-owned value (lane i < 12 holds v_i) into VL's registers
 __device__ __forceinline__ void gather12(double v, double (&out)[12]) {
   sfor<0, 12>([&](auto i) {
@@ -548,23 +561,36 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
   int iter = 0, status = -1;
   double last_amin = 1.0;
 
+  int par = 0;  // parity of the record the current iteration's factorization writes
   for (;;) {
-    // =================== RU: update + residuals ===================
+    // =========== RB (k = N..0): update + residuals + Gamma/gamma + factorization ===========
+    // One backward sweep per iteration: stage k applies the previous step to its
+    // variables, forms its residuals (x_{k+1}, pi_{k+1} were updated by stage k+1),
+    // and factorizes its barrier-augmented block right away, so the QP data is
+    // streamed once per iteration.  If the exit test after the sweep fires, this
+    // sweep's factorization is simply not used (outputs read the other parity).
     double mg = 0.0, mb = 0.0, md = 0.0, mm = 0.0, musum = 0.0, objl = 0.0;
-    double xk = 0.0, pik = 0.0;  // element-owned x_k, pi_k of the current stage
-    for (int k = 0; k <= N; ++k) {
+    double xn = 0.0, pin = 0.0;  // updated x_{k+1}, pi_{k+1} (element-owned), from stage k+1
+    double P[12];
+    for (int k = N; k >= 0; --k) {
       double* stk = c.st(k);
-      // current-stage values (updated): x_k / pi_k carried, u_k updated here
-      if (k == 0) {
-        xk = xel ? c.x[li] : 0.0;  // x_0 = x0 (never updated)
-        pik = 0.0;
-      }
-      double uk = 0.0;
+      double* rec = stk + par * kRecSize;
+      // ---- apply the previous step to stage k ----
+      double uk = 0.0, xk = 0.0, pik = 0.0;
       if (k < N && uel) {
         uk = c.u[(size_t)k * nu + lane] + alpha_p * stk[kStStep + lane];
         c.u[(size_t)k * nu + lane] = uk;
       }
-      // barrier variables of stage k
+      if (xel) {
+        if (k == 0) {
+          xk = c.x[li];  // x_0 = x0 (never updated); pi_0 is not an iterate
+        } else {
+          xk = c.x[(size_t)k * nx + lane] + alpha_p * stk[kStStep + 12 + lane];
+          pik = c.pi[(size_t)k * nx + lane] + alpha_d * stk[kStStep + 24 + lane];
+          c.x[(size_t)k * nx + lane] = xk;
+          c.pi[(size_t)k * nx + lane] = pik;
+        }
+      }
       Bar bu{0, 0, 1, 1}, bx{0, 0, 1, 1};
       const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
       if (lane < kMaxDim) {
@@ -582,67 +608,114 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         store_bar(stk, 0, lane, bu);
         store_bar(stk, 1, lane, bx);
       }
-      // next-stage x_{k+1}, pi_{k+1} (updated, carried to k+1)
-      double xn = 0.0, pin = 0.0;
-      if (k < N && xel) {
-        double* stn = c.st(k + 1);
-        xn = c.x[(size_t)(k + 1) * nx + lane] + alpha_p * stn[kStStep + 12 + lane];
-        pin = c.pi[(size_t)(k + 1) * nx + lane] + alpha_d * stn[kStStep + 24 + lane];
-        c.x[(size_t)(k + 1) * nx + lane] = xn;
-        c.pi[(size_t)(k + 1) * nx + lane] = pin;
-      }
-      // broadcasts of the iterate
-      double bxk[12], buk[12], bpn[12];
-      gather12(xk, bxk);
-      gather12(uk, buk);
-      gather12(pin, bpn);
-      // ---- residuals (element-owned) ----
+      // ---- residuals of stage k (element-owned) ----
       double rgx = 0.0, rgu = 0.0, rb = 0.0;
       {
-        double Qc[12];
-        c.col(c.Q + (size_t)k * c.nxx(), nx, col, xel, Qc);
-        double qx = 0.0;
-        sfor<0, 12>([&](auto j) {
-          constexpr int J = decltype(j)::value;
-          qx = fmadd(Qc[J], bxk[J], qx);
-        });
-        const double qk = c.el(c.q + (size_t)k * nx, nx, li);
-        rgx = qx + qk - pik;
-        if (k > 0) objl += xk * (0.5 * qx + qk);
+        double bxk[12], buk[12], bpn[12];
+        gather12(xk, bxk);
+        gather12(uk, buk);
+        gather12(pin, bpn);
+        {
+          double Qc[12];
+          c.col(c.Q + (size_t)k * c.nxx(), nx, col, xel, Qc);
+          const double qx = dot12(Qc, bxk, 0.0);
+          const double qk = c.el(c.q + (size_t)k * nx, nx, li);
+          rgx = qx + qk - pik;
+          if (k > 0) objl += xk * (0.5 * qx + qk);
+        }
+        if (k < N) {
+          // one block at a time (fenced) so that at most two 12-arrays are in flight
+          double ru, sx_, stu, btp, atp;
+          {
+            double M[12];
+            c.col(c.R + (size_t)k * c.nuu(), nu, col, uel, M);
+            ru = dot12(M, buk, 0.0);
+          }
+          SRBD_PHASE_FENCE();
+          {
+            double M[12];
+            c.row(c.S + (size_t)k * c.nxu(), nu, nx, li, uel, M);
+            sx_ = dot12(M, bxk, 0.0);
+          }
+          SRBD_PHASE_FENCE();
+          {
+            double M[12];
+            c.col(c.S + (size_t)k * c.nxu(), nu, col, xel, M);
+            stu = dot12(M, buk, 0.0);
+          }
+          SRBD_PHASE_FENCE();
+          {
+            double M[12];
+            c.col(c.B + (size_t)k * c.nxu(), nx, col, uel, M);
+            btp = dot12(M, bpn, 0.0);
+          }
+          SRBD_PHASE_FENCE();
+          {
+            double M[12];
+            c.col(c.A + (size_t)k * c.nxx(), nx, col, xel, M);
+            atp = dot12(M, bpn, 0.0);
+          }
+          SRBD_PHASE_FENCE();
+          const double rk = c.el(c.r + (size_t)k * nu, nu, li);
+          rgu = ru + sx_ + rk + btp;
+          rgx += stu + atp;
+          objl += uk * (0.5 * ru + rk + sx_);
+          // res_b = A x + B u + b - x_{k+1} (row-owned A, B)
+          double ax;
+          {
+            double M[12];
+            c.row(c.A + (size_t)k * c.nxx(), nx, nx, li, xel, M);
+            ax = dot12(M, bxk, 0.0);
+          }
+          SRBD_PHASE_FENCE();
+          {
+            double M[12];
+            c.row(c.B + (size_t)k * c.nxu(), nx, nu, li, xel, M);
+            ax = dot12(M, buk, ax);
+          }
+          SRBD_PHASE_FENCE();
+          rb = ax + c.el(c.b + (size_t)k * nx, nx, li) - xn;
+        }
+        if constexpr (GEN) {
+          // general rows: apply the step, residuals, res_g += C'(lam_u - lam_l), D'(..)
+          for (int ch = 0; ch < c.nch; ++ch) {
+            double* g = c.gs(k, ch);
+            const Side sg = c.side_g(k, ch, lane);
+            Bar bg{0, 0, 1, 1};
+            if (lane < kMaxDim) {
+              bg = load_gbar(g, lane);
+              const BarStep d = load_gstep(g, lane);
+              bg.tl += alpha_p * d.dtl;
+              bg.tu += alpha_p * d.dtu;
+              bg.ll += alpha_d * d.dll;
+              bg.lu += alpha_d * d.dlu;
+              store_gbar(g, lane, bg);
+            }
+            double Cr[12], Dr[12];
+            c.g_row(k, ch, lane, Cr, Dr);
+            const double v = dot12(Dr, buk, dot12(Cr, bxk, 0.0));
+            if (lane < kMaxDim) g[kGenVal + lane] = v;
+            if (sg.ml != 0.0) {
+              const double rd = v - sg.lb - bg.tl, rm = bg.ll * bg.tl;
+              md = fmax(md, nabs(rd));
+              mm = fmax(mm, nabs(rm));
+              musum += rm;
+            }
+            if (sg.mu != 0.0) {
+              const double rd = sg.ub - v - bg.tu, rm = bg.lu * bg.tu;
+              md = fmax(md, nabs(rd));
+              mm = fmax(mm, nabs(rm));
+              musum += rm;
+            }
+            double bdl[12], Cc[12], Dc[12];
+            gather12(lane < kMaxDim ? bg.lu - bg.ll : 0.0, bdl);
+            c.g_col(k, ch, col, Cc, Dc);
+            rgx = dot12(Cc, bdl, rgx);
+            rgu = dot12(Dc, bdl, rgu);
+          }
+        }
       }
-      if (k < N) {
-        double Rc[12], Sr[12], Sc[12], Bc[12], Ac[12];
-        c.col(c.R + (size_t)k * c.nuu(), nu, col, uel, Rc);
-        c.row(c.S + (size_t)k * c.nxu(), nu, nx, li, uel, Sr);
-        c.col(c.S + (size_t)k * c.nxu(), nu, col, xel, Sc);
-        c.col(c.B + (size_t)k * c.nxu(), nx, col, uel, Bc);
-        c.col(c.A + (size_t)k * c.nxx(), nx, col, xel, Ac);
-        double ru = 0.0, sx_ = 0.0, stu = 0.0, btp = 0.0, atp = 0.0;
-        sfor<0, 12>([&](auto j) {
-          constexpr int J = decltype(j)::value;
-          ru = fmadd(Rc[J], buk[J], ru);
-          sx_ = fmadd(Sr[J], bxk[J], sx_);
-          stu = fmadd(Sc[J], buk[J], stu);
-          btp = fmadd(Bc[J], bpn[J], btp);
-          atp = fmadd(Ac[J], bpn[J], atp);
-        });
-        const double rk = c.el(c.r + (size_t)k * nu, nu, li);
-        rgu = ru + sx_ + rk + btp;
-        rgx += stu + atp;
-        objl += uk * (0.5 * ru + rk + sx_);
-        // res_b = A x + B u + b - x_{k+1} (row-owned A, B)
-        double Ar[12], Br[12];
-        c.row(c.A + (size_t)k * c.nxx(), nx, nx, li, xel, Ar);
-        c.row(c.B + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
-        double ax = 0.0;
-        sfor<0, 12>([&](auto j) {
-          constexpr int J = decltype(j)::value;
-          ax = fmadd(Ar[J], bxk[J], ax);
-          ax = fmadd(Br[J], buk[J], ax);
-        });
-        rb = ax + c.el(c.b + (size_t)k * nx, nx, li) - xn;
-      }
-      // constraint terms
+      // box terms
       if (su.ml != 0.0) {
         rgu -= bu.ll;
         const double rd = uk - su.lb - bu.tl, rm = bu.ll * bu.tl;
@@ -671,44 +744,6 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         mm = fmax(mm, nabs(rm));
         musum += rm;
       }
-      if constexpr (GEN) {
-        // general rows: apply the step, residuals, res_g += C'(lam_u - lam_l), D'(..)
-        for (int ch = 0; ch < c.nch; ++ch) {
-          double* g = c.gs(k, ch);
-          const Side sg = c.side_g(k, ch, lane);
-          Bar bg{0, 0, 1, 1};
-          if (lane < kMaxDim) {
-            bg = load_gbar(g, lane);
-            const BarStep d = load_gstep(g, lane);
-            bg.tl += alpha_p * d.dtl;
-            bg.tu += alpha_p * d.dtu;
-            bg.ll += alpha_d * d.dll;
-            bg.lu += alpha_d * d.dlu;
-            store_gbar(g, lane, bg);
-          }
-          double Cr[12], Dr[12];
-          c.g_row(k, ch, lane, Cr, Dr);
-          const double v = dot12(Dr, buk, dot12(Cr, bxk, 0.0));
-          if (lane < kMaxDim) g[kGenVal + lane] = v;
-          if (sg.ml != 0.0) {
-            const double rd = v - sg.lb - bg.tl, rm = bg.ll * bg.tl;
-            md = fmax(md, nabs(rd));
-            mm = fmax(mm, nabs(rm));
-            musum += rm;
-          }
-          if (sg.mu != 0.0) {
-            const double rd = sg.ub - v - bg.tu, rm = bg.lu * bg.tu;
-            md = fmax(md, nabs(rd));
-            mm = fmax(mm, nabs(rm));
-            musum += rm;
-          }
-          double bdl[12], Cc[12], Dc[12];
-          gather12(lane < kMaxDim ? bg.lu - bg.ll : 0.0, bdl);
-          c.g_col(k, ch, col, Cc, Dc);
-          rgx = dot12(Cc, bdl, rgx);
-          rgu = dot12(Dc, bdl, rgu);
-        }
-      }
       if (!xel) rgx = 0.0;
       if (!uel) rgu = 0.0;
       if (k < N) {
@@ -716,100 +751,45 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         mb = fmax(mb, nabs(xel ? rb : 0.0));
       }
       if (k > 0) mg = fmax(mg, nabs(rgx));
+      if (!xel) rb = 0.0;
       if (lane < kMaxDim) {
         stk[kStRes + lane] = rgu;
         stk[kStRes + 12 + lane] = rgx;
-        stk[kStRes + 24 + lane] = xel ? rb : 0.0;
+        stk[kStRes + 24 + lane] = rb;
       }
-      xk = xn;
-      pik = pin;
-    }
-    res_stat = gmax(lane < kMaxDim ? mg : 0.0);
-    res_eq = gmax(lane < kMaxDim ? mb : 0.0);
-    res_ineq = gmax(lane < kMaxDim ? md : 0.0);
-    res_comp = gmax(lane < kMaxDim ? mm : 0.0);
-    obj = gsum(lane < kMaxDim ? objl : 0.0);
-    mu = gsum(lane < kMaxDim ? musum : 0.0) * nc_inv;
-    double* stat_row = a.stat && lane == 0
-                           ? a.stat + ((size_t)qp * (a.iter_max + 2) + iter) * kStatCols
-                           : nullptr;
-    if (stat_row) {
-      stat_row[5] = mu;
-      stat_row[6] = res_stat;
-      stat_row[7] = res_eq;
-      stat_row[8] = res_ineq;
-      stat_row[9] = res_comp;
-      stat_row[10] = obj;
-    }
-    // ---- exit test (HPIPM order: converged / iter_max / min step / NaN) ----
-    {
-      const bool isnan_ = !(res_stat == res_stat) || !(res_eq == res_eq) ||
-                          !(res_ineq == res_ineq) || !(res_comp == res_comp) || !(mu == mu) ||
-                          res_stat == __builtin_inf() || res_eq == __builtin_inf();
-      if (isnan_) {
-        status = 3;
-      } else if (res_stat <= a.tol_stat && res_eq <= a.tol_eq && res_ineq <= a.tol_ineq &&
-                 res_comp <= a.tol_comp) {
-        status = 0;
-      } else if (iter >= a.iter_max) {
-        status = 1;
-      } else if (iter > 0 && last_amin < a.alpha_min) {
-        status = 2;
+      SRBD_PHASE_FENCE();
+      // ---- predictor Gamma / gamma, factorization of stage k ----
+      double Gu = 0.0, gu = 0.0, Gx = 0.0, gx = 0.0;
+      if (lane < kMaxDim) {
+        gamma_of(su, bu, uk, 0.0, 0.0, 0.0, Gu, gu);
+        gamma_of(sx, bx, xk, 0.0, 0.0, 0.0, Gx, gx);
       }
-      if (status >= 0) break;
-    }
-
-    // =================== B1: factorization + predictor vectors ===================
-    {
-      double P[12];
-      // terminal stage: P_N = Q_N + diag(Gamma_x), p_N = q~_N
-      {
-        double* stN = c.st(N);
-        const Side sx = c.side_x(N, lane);
-        const double xv = xel ? c.x[(size_t)N * nx + lane] : 0.0;
-        double G = 0.0, g = 0.0;
-        if (lane < kMaxDim) gamma_of(sx, load_bar(stN, 1, lane), xv, 0.0, 0.0, 0.0, G, g);
-        double qt = lane < kMaxDim ? stN[kStRes + 12 + lane] + g : 0.0;
-        if constexpr (GEN) {
-          double ra, qa;
-          g_grad(N, false, 0.0, ra, qa);
-          if (lane < kMaxDim) qt += qa;
+      double rt = lane < kMaxDim ? rgu + gu : 0.0;
+      double qt = lane < kMaxDim ? rgx + gx : 0.0;
+      if constexpr (GEN) {
+        double ra, qa;
+        g_grad(k, false, 0.0, ra, qa);
+        if (lane < kMaxDim) {
+          rt += ra;
+          qt += qa;
         }
+      }
+      if (k == N) {
+        // terminal stage: P_N = Q_N + diag(Gamma_x) (+ C'Gamma C), p_N = q~_N
         double qv[12];
         gather12(qt, qv);
         c.col(c.Q + (size_t)N * c.nxx(), nx, col, xel, P);
         if constexpr (GEN) g_hess(N, 2, P, P);
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
-          if (lane == I) P[I] += G;
+          if (lane == I) P[I] += Gx;
           if (c.isv) P[I] = qv[I];
         });
-        if (lane < kMaxDim) store12(stN + kRecP + lane * 12, P);
-        if (c.isv) store12(stN + kRecPv, P);
-      }
-      for (int k = N - 1; k >= 0; --k) {
-        double* stk = c.st(k);
-        const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
-        const double uv = uel ? c.u[(size_t)k * nu + lane] : 0.0;
-        const double xv = xel ? c.x[(size_t)k * nx + lane] : 0.0;
-        double Gu = 0.0, gu = 0.0, Gx = 0.0, gx = 0.0;
-        if (lane < kMaxDim) {
-          gamma_of(su, load_bar(stk, 0, lane), uv, 0.0, 0.0, 0.0, Gu, gu);
-          gamma_of(sx, load_bar(stk, 1, lane), xv, 0.0, 0.0, 0.0, Gx, gx);
-        }
-        double rt = lane < kMaxDim ? stk[kStRes + lane] + gu : 0.0;
-        double qt = lane < kMaxDim ? stk[kStRes + 12 + lane] + gx : 0.0;
-        if constexpr (GEN) {
-          double ra, qa;
-          g_grad(k, false, 0.0, ra, qa);
-          if (lane < kMaxDim) {
-            rt += ra;
-            qt += qa;
-          }
-        }
-        const double bt = lane < kMaxDim ? stk[kStRes + 24 + lane] : 0.0;
+        if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
+        if (c.isv) store12(rec + kRecPv, P);
+      } else {
         double bv[12];
-        gather12(bt, bv);
+        gather12(rb, bv);
         double A_[12], B_[12];
         c.col(c.A + (size_t)k * c.nxx(), nx, col, xel, A_);
         c.col(c.B + (size_t)k * c.nxu(), nx, col, uel, B_);
@@ -846,58 +826,75 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         StageFactor<double> f;
         riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
         if (lane < kMaxDim) {
-          store12(stk + kRecL + lane * 12, f.Lc);
-          store12(stk + kRecK + lane * 12, f.Kc);
-          store12(stk + kRecAcl + lane * 12, A_);
-          store12(stk + kRecP + lane * 12, f.F);
-          stk[kRecRs + lane] = f.rs;
+          store_packed_col(rec + kRecL, lane, f.Lc);
+          store12(rec + kRecK + lane * 12, f.Kc);
+          store12(rec + kRecAcl + lane * 12, A_);
+          store_packed_col(rec + kRecP, lane, f.F);
+          rec[kRecRs + lane] = f.rs;
         }
         if (c.isv) {
-          store12(stk + kRecKv, f.Kc);
-          store12(stk + kRecBcl, A_);
-          store12(stk + kRecPv, f.F);
+          store12(rec + kRecKv, f.Kc);
+          store12(rec + kRecBcl, A_);
+          store12(rec + kRecPv, f.F);
         }
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
           P[I] = f.F[I];
         });
       }
+      xn = xk;
+      pin = pik;
+    }
+    res_stat = gmax(lane < kMaxDim ? mg : 0.0);
+    res_eq = gmax(lane < kMaxDim ? mb : 0.0);
+    res_ineq = gmax(lane < kMaxDim ? md : 0.0);
+    res_comp = gmax(lane < kMaxDim ? mm : 0.0);
+    obj = gsum(lane < kMaxDim ? objl : 0.0);
+    const double musum_all = gsum(lane < kMaxDim ? musum : 0.0);
+    mu = musum_all * nc_inv;
+    double* stat_row = a.stat && lane == 0
+                           ? a.stat + ((size_t)qp * (a.iter_max + 2) + iter) * kStatCols
+                           : nullptr;
+    if (stat_row) {
+      stat_row[5] = mu;
+      stat_row[6] = res_stat;
+      stat_row[7] = res_eq;
+      stat_row[8] = res_ineq;
+      stat_row[9] = res_comp;
+      stat_row[10] = obj;
+    }
+    // ---- exit test (HPIPM order: converged / iter_max / min step / NaN) ----
+    {
+      const bool isnan_ = !(res_stat == res_stat) || !(res_eq == res_eq) ||
+                          !(res_ineq == res_ineq) || !(res_comp == res_comp) || !(mu == mu) ||
+                          res_stat == __builtin_inf() || res_eq == __builtin_inf();
+      if (isnan_) {
+        status = 3;
+      } else if (res_stat <= a.tol_stat && res_eq <= a.tol_eq && res_ineq <= a.tol_ineq &&
+                 res_comp <= a.tol_comp) {
+        status = 0;
+      } else if (iter >= a.iter_max) {
+        status = 1;
+      } else if (iter > 0 && last_amin < a.alpha_min) {
+        status = 2;
+      }
+      if (status >= 0) break;
     }
 
     // =================== F1 / M / B2 / F2 ===================
     double sigma_mu = 0.0, alpha_aff = 0.0, mu_aff = 0.0, sigma = 0.0;
     const int npass = a.pred_corr ? 2 : 1;
     double ap = 1e300, ad = 1e300;
+    double s1 = 0.0, s2 = 0.0;  // predictor sums lam dt + t dlam, dlam dt (element-owned)
     for (int pass = 0; pass < npass; ++pass) {
       const bool corr = pass == 1;
       if (corr) {
-        // ---- M: alpha_aff, mu_aff, sigma ----
+        // ---- alpha_aff, mu_aff, sigma: mu_aff from the predictor sums of F1,
+        // sum (lam + a dlam)(t + a dt) = S0 + a S1 + a^2 S2 (no extra sweep) ----
         const double aa = fmin(1.0, fmin(gmin(ap), gmin(ad)));
         alpha_aff = aa;
-        double mus = 0.0;
-        for (int k = 0; k <= N; ++k) {
-          const double* stk = c.st(k);
-          if (lane < kMaxDim) {
-            const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
-            const Bar bu = load_bar(stk, 0, lane), bx = load_bar(stk, 1, lane);
-            const BarStep du = load_bstep(stk, 0, lane), dx = load_bstep(stk, 1, lane);
-            if (su.ml != 0.0) mus += (bu.ll + aa * du.dll) * (bu.tl + aa * du.dtl);
-            if (su.mu != 0.0) mus += (bu.lu + aa * du.dlu) * (bu.tu + aa * du.dtu);
-            if (sx.ml != 0.0) mus += (bx.ll + aa * dx.dll) * (bx.tl + aa * dx.dtl);
-            if (sx.mu != 0.0) mus += (bx.lu + aa * dx.dlu) * (bx.tu + aa * dx.dtu);
-            if constexpr (GEN) {
-              for (int ch = 0; ch < c.nch; ++ch) {
-                const double* g = c.gs(k, ch);
-                const Side sg = c.side_g(k, ch, lane);
-                const Bar bg = load_gbar(g, lane);
-                const BarStep d = load_gstep(g, lane);
-                if (sg.ml != 0.0) mus += (bg.ll + aa * d.dll) * (bg.tl + aa * d.dtl);
-                if (sg.mu != 0.0) mus += (bg.lu + aa * d.dlu) * (bg.tu + aa * d.dtu);
-              }
-            }
-          }
-        }
-        mu_aff = gsum(lane < kMaxDim ? mus : 0.0) * nc_inv;
+        const double S1 = gsum(lane < kMaxDim ? s1 : 0.0), S2 = gsum(lane < kMaxDim ? s2 : 0.0);
+        mu_aff = (musum_all + aa * (S1 + aa * S2)) * nc_inv;
         double sg = mu > 0.0 ? mu_aff / mu : 0.0;
         sg = sg * sg * sg;
         if (sg > 1.0) sg = 1.0;
@@ -920,11 +917,12 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
             g_grad(N, true, sigma_mu, ra, qa);
             if (lane < kMaxDim && xel) pnext += qa;
           }
-          if (lane < kMaxDim) stN[kRecPv + lane] = pnext;
+          if (lane < kMaxDim) stN[par * kRecSize + kRecPv + lane] = pnext;
         }
         for (int k = N - 1; k >= 0; --k) {
           double* stk = c.st(k);
-          const double* stn = c.st(k + 1);
+          double* rec = stk + par * kRecSize;
+          const double* recn = c.st(k + 1) + par * kRecSize;
           const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
           const double uv = uel ? c.u[(size_t)k * nu + lane] : 0.0;
           const double xv = xel ? c.x[(size_t)k * nx + lane] : 0.0;
@@ -945,7 +943,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           const double bt = lane < kMaxDim ? stk[kStRes + 24 + lane] : 0.0;
           // w = P_{k+1} b~ + p_{k+1}
           double Pc[12], bb[12];
-          load12(stn + kRecP + col * 12, Pc);
+          load_packed_sym(recn + kRecP, col, Pc);
           gather12(bt, bb);
           double w = pnext;
           sfor<0, 12>([&](auto j) {
@@ -966,7 +964,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           if (lane >= kMaxDim) g = 0.0;
           // p = f + K'g  (K column-owned: lane j holds K[:, j])
           double Kc[12], bg[12];
-          load12(stk + kRecK + col * 12, Kc);
+          load12(rec + kRecK + col * 12, Kc);
           gather12(g, bg);
           double pv = f;
           sfor<0, 12>([&](auto j) {
@@ -975,12 +973,9 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           });
           // y = L^-1 g (row-owned L), then z = L^-T y (column-owned L), k = -z
           double Lr[12], Lc[12];
-          sfor<0, 12>([&](auto j) {
-            constexpr int J = decltype(j)::value;
-            Lr[J] = stk[kRecL + J * 12 + li];
-          });
-          load12(stk + kRecL + col * 12, Lc);
-          const double rs = stk[kRecRs + li];
+          load_packed_lrow(rec + kRecL, li, Lr);
+          load_packed_lcol(rec + kRecL, col, Lc);
+          const double rs = rec[kRecRs + li];
           double y = g;
           sfor<0, 12>([&](auto kk) {
             constexpr int K = decltype(kk)::value;
@@ -1005,9 +1000,9 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
             bcl = fmadd(Br[J], bk[J], bcl);
           });
           if (lane < kMaxDim) {
-            stk[kRecKv + lane] = kv;
-            stk[kRecBcl + lane] = xel ? bcl : 0.0;
-            stk[kRecPv + lane] = xel ? pv : 0.0;
+            rec[kRecKv + lane] = kv;
+            rec[kRecBcl + lane] = xel ? bcl : 0.0;
+            rec[kRecPv + lane] = xel ? pv : 0.0;
           }
           pnext = xel ? pv : 0.0;
         }
@@ -1018,11 +1013,12 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
       double dxk = 0.0;  // dx_0 = 0 (x0 fixed)
       for (int k = 0; k <= N; ++k) {
         double* stk = c.st(k);
+        const double* rec = stk + par * kRecSize;
         double bdx[12];
         gather12(dxk, bdx);
         double Pc[12];
-        load12(stk + kRecP + col * 12, Pc);
-        double dpi = stk[kRecPv + li];
+        load_packed_sym(rec + kRecP, col, Pc);
+        double dpi = rec[kRecPv + li];
         sfor<0, 12>([&](auto j) {
           constexpr int J = decltype(j)::value;
           dpi = fmadd(Pc[J], bdx[J], dpi);
@@ -1032,11 +1028,11 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           double Kr[12], Ar[12];
           sfor<0, 12>([&](auto j) {
             constexpr int J = decltype(j)::value;
-            Kr[J] = stk[kRecK + J * 12 + li];
-            Ar[J] = stk[kRecAcl + J * 12 + li];
+            Kr[J] = rec[kRecK + J * 12 + li];
+            Ar[J] = rec[kRecAcl + J * 12 + li];
           });
-          du = stk[kRecKv + li];
-          dxn = stk[kRecBcl + li];
+          du = rec[kRecKv + li];
+          dxn = rec[kRecBcl + li];
           sfor<0, 12>([&](auto j) {
             constexpr int J = decltype(j)::value;
             du = fmadd(Kr[J], bdx[J], du);
@@ -1069,6 +1065,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
               }
               const BarStep d = bar_step(sg, bg, g[kGenVal + lane], dv, el, eu, sm);
               ratio(sg, bg, d, ap, ad);
+              if (!corr) aff_sums(sg, bg, d, s1, s2);
               store_gstep(g, lane, d);
             }
           }
@@ -1091,6 +1088,10 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           const BarStep nx_ = bar_step(sx, bx, xv, dxk, exl, exu, smu);
           ratio(su, bu, nu_, ap, ad);
           ratio(sx, bx, nx_, ap, ad);
+          if (!corr) {
+            aff_sums(su, bu, nu_, s1, s2);
+            aff_sums(sx, bx, nx_, s1, s2);
+          }
           store_bstep(stk, 0, lane, nu_);
           store_bstep(stk, 1, lane, nx_);
           stk[kStStep + lane] = du;
@@ -1110,6 +1111,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
     alpha_p = fmin(1.0, kStepTau * ap);
     alpha_d = fmin(1.0, kStepTau * ad);
     last_amin = fmin(alpha_p, alpha_d);
+    par ^= 1;
     if (stat_row) {
       double* next = stat_row + kStatCols;  // HPIPM stores step kk in row kk+1
       next[0] = alpha_aff;
@@ -1122,16 +1124,19 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
   }
 
   // =================== outputs ===================
+  // Riccati factors of the last completed iteration (HPIPM's getters); the
+  // exiting sweep's own factorization is used only when no step was taken.
+  const int out_par = iter > 0 ? (par ^ 1) : par;
   // pi_0 := Q0 x0 + S0'u0 + q0 + A0'(pi_1 + P_1 res_b0): the value of the
   // stage-0 rebuild (ocp_qp_ipm_solver.cpp:347-373) with p_1 = pi_1 - P_1 x_1.
   {
     const double* st0 = c.st(0);
-    const double* st1 = c.st(1);
+    const double* st1 = c.st(1) + out_par * kRecSize;
     double bx0[12], bu0[12];
     gather12(xel ? c.x[li] : 0.0, bx0);
     gather12(uel ? c.u[li] : 0.0, bu0);
     double P1c[12], brb[12];
-    load12(st1 + kRecP + col * 12, P1c);
+    load_packed_sym(st1 + kRecP, col, P1c);
     gather12(lane < kMaxDim ? st0[kStRes + 24 + lane] : 0.0, brb);
     double t = xel ? c.pi[(size_t)nx + lane] : 0.0;
     sfor<0, 12>([&](auto j) {
@@ -1159,11 +1164,11 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
     // vectors by consistency: p_k = pi_k - P_k x_k, k_k = u_k - K_k x_k.
     const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu;
     for (int k = 0; k <= N; ++k) {
-      const double* stk = c.st(k);
+      const double* stk = c.st(k) + out_par * kRecSize;
       double bxk[12];
       gather12(xel ? c.x[(size_t)k * nx + li] : 0.0, bxk);
       double Pc[12];
-      load12(stk + kRecP + col * 12, Pc);
+      load_packed_sym(stk + kRecP, col, Pc);
       if (a.P && xel)
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;

@@ -11,7 +11,7 @@ namespace srbd {
 // Forward-pass record of one stage, written by the backward sweep and read
 // back (row-owned) by the forward sweep.  K and Acl are row-major so that lane
 // i of the forward pass loads row i as 96 contiguous bytes; the symmetric P is
-// packed (lower triangle by columns, 78 values: see packed_off).
+// packed (lower triangle by columns, 78 values: qp_group.h packed_col).
 constexpr int kWsK = 0;      // K   [12][12] row-major (u-row i)
 constexpr int kWsAcl = 144;  // Acl [12][12] row-major
 constexpr int kWsP = 288;    // P   packed lower triangle, 78
@@ -19,13 +19,6 @@ constexpr int kWsk = 366;    // k   [12]
 constexpr int kWsbcl = 378;  // bcl [12]
 constexpr int kWsp = 390;    // p   [12]
 constexpr int kWsStage = 402;  // doubles per stage record (16-byte multiple)
-
-// offset of P[i][j] (i >= j) in the packed lower triangle: column j starts at
-// j*12 - j*(j-1)/2
-__host__ __device__ constexpr int packed_col(int j) { return j * 12 - j * (j - 1) / 2; }
-__host__ __device__ constexpr int packed_off(int i, int j) {
-  return i >= j ? packed_col(j) + (i - j) : packed_col(i) + (j - i);
-}
 
 struct ProblemArgs {
   int batch, N, nx, nu, ng;
@@ -50,14 +43,25 @@ struct ProblemArgs {
 
 constexpr int kStatCols = 18;  // HPIPM ws->stat row width
 
-// IPM per-stage workspace layout (doubles), see ipm_box.hip.
-constexpr int kRecL = 0, kRecK = 144, kRecAcl = 288, kRecP = 432, kRecRs = 576, kRecKv = 588,
-              kRecBcl = 600, kRecPv = 612, kRecSize = 624;
-constexpr int kStLam = 624;   // 8 x 12: lam_l,u / lam_u,u / t_l,u / t_u,u / same for x
-constexpr int kStRes = 720;   // 3 x 12: res_g,u / res_g,x / res_b
-constexpr int kStStep = 756;  // 3 x 12: du / dx / dpi
-constexpr int kStDlt = 792;   // 8 x 12: dt_l,u dt_u,u dlam_l,u dlam_u,u (u), same (x)
-constexpr int kIpmStage = 888;
+// IPM per-stage workspace layout (doubles), see ipm_box.hip.  Two factor
+// records per stage (ping-pong by iteration parity: the iteration that exits
+// still reports the previous iteration's Riccati factors, like HPIPM's
+// getters), then the iterate's barrier state.
+constexpr int kRecL = 0;      // L packed lower triangle (78)
+constexpr int kRecK = 78;     // K [12][12], column j contiguous
+constexpr int kRecAcl = 222;  // Acl [12][12], column j contiguous
+constexpr int kRecP = 366;    // P packed lower triangle (78)
+constexpr int kRecRs = 444;   // 1 / diag(L)
+constexpr int kRecKv = 456;   // k
+constexpr int kRecBcl = 468;  // bcl
+constexpr int kRecPv = 480;   // p
+constexpr int kRecSize = 492;
+constexpr int kStLam = 2 * kRecSize;  // 8 x 12: lam_l,u / lam_u,u / t_l,u / t_u,u / same for x
+constexpr int kStRes = kStLam + 96;   // 3 x 12: res_g,u / res_g,x / res_b
+constexpr int kStStep = kStRes + 36;  // 3 x 12: du / dx / dpi
+constexpr int kStDlt = kStStep + 36;  // 8 x 12: dt_l,u dt_u,u dlam_l,u dlam_u,u (u), same (x)
+constexpr int kIpmStage = kStDlt + 96;
+static_assert(kIpmStage % 2 == 0, "16-byte aligned stages");
 // general constraints (ng > 0): per stage and 12-row chunk, appended after
 // kIpmStage: bars lam_l / lam_u / t_l / t_u [4][12], steps [4][12], row values
 // C x + D u [12], 4 pad

@@ -175,4 +175,43 @@ __device__ __forceinline__ void load_col_pad(const T* __restrict__ p, int rows, 
   });
 }
 
+// ---------------------------------------------------------------------------
+// Packed lower triangle of a 12x12 block, by columns (78 values): column j
+// holds rows j..11 from packed_col(j).  Used for the symmetric P and the
+// Cholesky factor L in the stage records.
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int packed_col(int j) { return j * 12 - j * (j - 1) / 2; }
+
+// lane j < 12 stores its column v[i] = M[i][j], rows i >= j only
+__device__ __forceinline__ void store_packed_col(double* pk, int lane, const double (&v)[12]) {
+  const int cj = packed_col(lane) - lane;
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    if (I >= lane) pk[cj + I] = v[I];
+  });
+}
+// row r (= column r) of a symmetric matrix stored as its packed lower triangle
+__device__ __forceinline__ void load_packed_sym(const double* pk, int r, double (&v)[12]) {
+  const int cr = packed_col(r) - r;
+  sfor<0, 12>([&](auto j) {
+    constexpr int J = decltype(j)::value;
+    v[J] = J <= r ? pk[packed_col(J) + r - J] : pk[cr + J];
+  });
+}
+// strictly-lower row r of a packed lower-triangular L: v[j] = L[r][j] (j < r), else 0
+__device__ __forceinline__ void load_packed_lrow(const double* pk, int r, double (&v)[12]) {
+  sfor<0, 12>([&](auto j) {
+    constexpr int J = decltype(j)::value;
+    v[J] = J < r ? pk[packed_col(J) + r - J] : 0.0;
+  });
+}
+// strictly-lower column c of a packed lower-triangular L: v[i] = L[i][c] (i > c), else 0
+__device__ __forceinline__ void load_packed_lcol(const double* pk, int c, double (&v)[12]) {
+  const int cc = packed_col(c) - c;
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    v[I] = I > c ? pk[cc + I] : 0.0;
+  });
+}
+
 }  // namespace srbd

@@ -36,24 +36,6 @@ __device__ __forceinline__ void store_n(double* out, int n, const double (&v)[12
   });
 }
 
-// lane j < 12 stores column j of the symmetric P (v[i] = P[i][j]) into the
-// packed lower triangle: entries i >= j only
-__device__ __forceinline__ void store_packed_col(double* pk, int lane, const double (&v)[12]) {
-  const int cj = packed_col(lane) - lane;
-  sfor<0, 12>([&](auto i) {
-    constexpr int I = decltype(i)::value;
-    if (I >= lane) pk[cj + I] = v[I];
-  });
-}
-// row r of the symmetric P from the packed lower triangle
-__device__ __forceinline__ void load_packed_row(const double* pk, int r, double (&v)[12]) {
-  const int cr = packed_col(r) - r;
-  sfor<0, 12>([&](auto j) {
-    constexpr int J = decltype(j)::value;
-    v[J] = J <= r ? pk[packed_col(J) + r - J] : pk[cr + J];
-  });
-}
-
 template <bool FULL>
 struct StageLoader {
   int nx, nu;
@@ -202,7 +184,7 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgs a) {
   auto load_rows = [&](int k, double (&P_)[12], double (&K_)[12], double (&A__)[12], double& p_,
                        double& k_, double& b_) {
     const double* rec = rec_at(k);
-    load_packed_row(rec + kWsP, row, P_);
+    load_packed_sym(rec + kWsP, row, P_);
     p_ = rec[kWsp + row];
     if (k < N) {
       load12(rec + kWsK + row * 12, K_);
