@@ -34,6 +34,13 @@ namespace srbd {
 namespace {
 
 constexpr double kThr0 = 0.1;     // minimum initial slack (HPIPM init_var)
+
+// phase kernels (one launch each, per IPM iteration; see launch_ipm_box)
+constexpr int kPhInit = 0, kPhRB = 1, kPhF1 = 2, kPhB2 = 3, kPhF2 = 4, kPhOut = 5;
+// per-QP scalar state, kQsSize doubles at the head of the QP's workspace
+constexpr int kQsAlphaP = 0, kQsAlphaD = 1, kQsLastAmin = 2, kQsMu = 3, kQsMuSum = 4,
+              kQsSigmaMu = 5, kQsStatus = 6, kQsIter = 7, kQsNc = 8, kQsResStat = 9,
+              kQsResEq = 10, kQsResIneq = 11, kQsResComp = 12, kQsObj = 13, kQsSize = 16;
 constexpr double kStepTau = 0.995;  // fraction to the boundary
 
 __device__ __forceinline__ double gsum(double v) {
@@ -68,21 +75,59 @@ struct Side {
 
 template <bool FULL, bool GEN>
 struct Ctx {
-  int N, nx, nu, lane;
+  int N, nx, nu, lane, qp;
   bool isv;
-  const double *A, *B, *b, *Q, *S, *R, *q, *r, *x0;
-  const double *lbu, *ubu, *lbum, *ubum, *lbx, *ubx, *lbxm, *ubxm;
-  const double *C, *D, *lg, *ug, *lgm, *ugm;  // general constraints (GEN)
-  int ng, nch;                                // rows, 12-row chunks
-  size_t stride;                              // workspace doubles per stage
-  double *x, *u, *pi;
-  double* ws;
+  int ng, nch;    // general rows, 12-row chunks
+  size_t stride;  // workspace doubles per stage
+  size_t ws_qp;   // workspace doubles per QP
+  // Batch base pointers (wave-uniform, SGPRs).  The per-QP pointers below are
+  // recomputed at every use from an opaque copy of qp, so the compiler cannot
+  // hoist ~27 64-bit per-lane pointers into VGPRs for the whole kernel.
+  const double *bA, *bB, *bb, *bQ, *bS, *bR, *bq, *br, *bx0;
+  const double *blbu, *bubu, *blbum, *bubum, *blbx, *bubx, *blbxm, *bubxm;
+  const double *bC, *bD, *blg, *bug, *blgm, *bugm;
+  double *bxo, *buo, *bpi, *bws;
+
+  __device__ size_t oq() const {
+    int v = qp;
+    asm volatile("" : "+v"(v));
+    return (size_t)v;
+  }
+  __device__ size_t sN() const { return oq() * N; }
+  __device__ size_t sN1() const { return oq() * (N + 1); }
+  __device__ const double* A() const { return bA + sN() * nxx(); }
+  __device__ const double* B() const { return bB + sN() * nxu(); }
+  __device__ const double* b() const { return bb + sN() * nx; }
+  __device__ const double* Q() const { return bQ + sN1() * nxx(); }
+  __device__ const double* S() const { return bS + sN() * nxu(); }
+  __device__ const double* R() const { return bR + sN() * nuu(); }
+  __device__ const double* q() const { return bq + sN1() * nx; }
+  __device__ const double* r() const { return br + sN() * nu; }
+  __device__ const double* x0() const { return bx0 + oq() * nx; }
+  __device__ const double* lbu() const { return blbu ? blbu + sN() * nu : nullptr; }
+  __device__ const double* ubu() const { return bubu ? bubu + sN() * nu : nullptr; }
+  __device__ const double* lbum() const { return blbum ? blbum + sN() * nu : nullptr; }
+  __device__ const double* ubum() const { return bubum ? bubum + sN() * nu : nullptr; }
+  __device__ const double* lbx() const { return blbx ? blbx + sN1() * nx : nullptr; }
+  __device__ const double* ubx() const { return bubx ? bubx + sN1() * nx : nullptr; }
+  __device__ const double* lbxm() const { return blbxm ? blbxm + sN1() * nx : nullptr; }
+  __device__ const double* ubxm() const { return bubxm ? bubxm + sN1() * nx : nullptr; }
+  __device__ const double* C() const { return bC ? bC + sN1() * ng * nx : nullptr; }
+  __device__ const double* D() const { return bD ? bD + sN() * ng * nu : nullptr; }
+  __device__ const double* lg() const { return blg + sN1() * ng; }
+  __device__ const double* ug() const { return bug + sN1() * ng; }
+  __device__ const double* lgm() const { return blgm ? blgm + sN1() * ng : nullptr; }
+  __device__ const double* ugm() const { return bugm ? bugm + sN1() * ng : nullptr; }
+  __device__ double* x() const { return bxo + sN1() * nx; }
+  __device__ double* u() const { return buo + sN() * nu; }
+  __device__ double* pi() const { return bpi + sN1() * nx; }
+  __device__ double* ws() const { return bws + oq() * ws_qp; }
 
   __device__ size_t nxx() const { return FULL ? 144 : (size_t)nx * nx; }
   __device__ size_t nxu() const { return FULL ? 144 : (size_t)nx * nu; }
   __device__ size_t nuu() const { return FULL ? 144 : (size_t)nu * nu; }
   __device__ double* st(int k) const {
-    return ws + (size_t)k * (GEN ? stride : (size_t)kIpmStage);
+    return ws() + kQsSize + (size_t)k * (GEN ? stride : (size_t)kIpmStage);
   }
   // state of constraint chunk ch at stage k: bars [48], steps [48], row values [12]
   __device__ double* gs(int k, int ch) const { return st(k) + kIpmStage + ch * kGenChunk; }
@@ -92,10 +137,10 @@ struct Ctx {
     const int r = ch * kMaxDim + i;
     if (i < kMaxDim && r < ng) {
       const size_t o = (size_t)k * ng + r;
-      s.lb = lg[o];
-      s.ub = ug[o];
-      s.ml = lgm ? (lgm[o] != 0.0 ? 1.0 : 0.0) : 1.0;
-      s.mu = ugm ? (ugm[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+      s.lb = lg()[o];
+      s.ub = ug()[o];
+      s.ml = lgm() ? (lgm()[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+      s.mu = ugm() ? (ugm()[o] != 0.0 ? 1.0 : 0.0) : 1.0;
     }
     return s;
   }
@@ -104,9 +149,9 @@ struct Ctx {
   __device__ void g_row(int k, int ch, int i, double (&Cr)[12], double (&Dr)[12]) const {
     const int r = ch * kMaxDim + i;
     const bool ok = i < kMaxDim && r < ng;
-    const bool cok = ok && C && k > 0, dok = ok && D && k < N;
-    const double* cb = C ? C + (size_t)k * ng * nx + r : nullptr;
-    const double* db = D ? D + (size_t)k * ng * nu + r : nullptr;
+    const bool cok = ok && bC && k > 0, dok = ok && bD && k < N;
+    const double* cb = C() ? C() + (size_t)k * ng * nx + r : nullptr;
+    const double* db = D() ? D() + (size_t)k * ng * nu + r : nullptr;
     sfor<0, 12>([&](auto j) {
       constexpr int J = decltype(j)::value;
       Cr[J] = (cok && J < nx) ? cb[(size_t)J * ng] : 0.0;
@@ -116,9 +161,9 @@ struct Ctx {
   // column-owned C / D columns restricted to chunk ch (lane j = column)
   __device__ void g_col(int k, int ch, int j, double (&Cc)[12], double (&Dc)[12]) const {
     const int r0 = ch * kMaxDim;
-    const bool cok = C && k > 0 && j < nx, dok = D && k < N && j < nu;
-    const double* cb = C ? C + (size_t)k * ng * nx + (size_t)j * ng + r0 : nullptr;
-    const double* db = D ? D + (size_t)k * ng * nu + (size_t)j * ng + r0 : nullptr;
+    const bool cok = bC && k > 0 && j < nx, dok = bD && k < N && j < nu;
+    const double* cb = C() ? C() + (size_t)k * ng * nx + (size_t)j * ng + r0 : nullptr;
+    const double* db = D() ? D() + (size_t)k * ng * nu + (size_t)j * ng + r0 : nullptr;
     sfor<0, 12>([&](auto i) {
       constexpr int I = decltype(i)::value;
       Cc[I] = (cok && r0 + I < ng) ? cb[I] : 0.0;
@@ -155,23 +200,23 @@ struct Ctx {
   }
   __device__ Side side_u(int k, int i) const {
     Side s{0.0, 0.0, 0.0, 0.0};
-    if (lbu && i < nu && k < N) {
+    if (blbu && i < nu && k < N) {
       const size_t o = (size_t)k * nu + i;
-      s.lb = lbu[o];
-      s.ub = ubu[o];
-      s.ml = lbum ? (lbum[o] != 0.0 ? 1.0 : 0.0) : 1.0;
-      s.mu = ubum ? (ubum[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+      s.lb = lbu()[o];
+      s.ub = ubu()[o];
+      s.ml = lbum() ? (lbum()[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+      s.mu = ubum() ? (ubum()[o] != 0.0 ? 1.0 : 0.0) : 1.0;
     }
     return s;
   }
   __device__ Side side_x(int k, int i) const {
     Side s{0.0, 0.0, 0.0, 0.0};
-    if (lbx && i < nx && k > 0) {  // stage-0 x bounds dropped (x0 embedding)
+    if (blbx && i < nx && k > 0) {  // stage-0 x bounds dropped (x0 embedding)
       const size_t o = (size_t)k * nx + i;
-      s.lb = lbx[o];
-      s.ub = ubx[o];
-      s.ml = lbxm ? (lbxm[o] != 0.0 ? 1.0 : 0.0) : 1.0;
-      s.mu = ubxm ? (ubxm[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+      s.lb = lbx()[o];
+      s.ub = ubx()[o];
+      s.ml = lbxm() ? (lbxm()[o] != 0.0 ? 1.0 : 0.0) : 1.0;
+      s.mu = ubxm() ? (ubxm()[o] != 0.0 ? 1.0 : 0.0) : 1.0;
     }
     return s;
   }
@@ -310,8 +355,8 @@ __device__ __forceinline__ void gather12(double v, double (&out)[12]) {
   });
 }
 
-template <bool FULL, bool GEN>
-__global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
+template <bool FULL, bool GEN, int PH>
+__global__ void __launch_bounds__(256, 2) ipm_phase_kernel(ProblemArgs a) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int qp = gid >> 4;
   const int lane = threadIdx.x & (kGroup - 1);
@@ -329,43 +374,18 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
   c.nu = nu;
   c.lane = lane;
   c.isv = lane == kVecLane;
-  {
-    const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu, nuu = (size_t)nu * nu;
-    c.A = a.A + (size_t)qp * N * nxx;
-    c.B = a.B + (size_t)qp * N * nxu;
-    c.b = a.b + (size_t)qp * N * nx;
-    c.Q = a.Q + (size_t)qp * (N + 1) * nxx;
-    c.S = a.S + (size_t)qp * N * nxu;
-    c.R = a.R + (size_t)qp * N * nuu;
-    c.q = a.q + (size_t)qp * (N + 1) * nx;
-    c.r = a.r + (size_t)qp * N * nu;
-    c.x0 = a.x0 + (size_t)qp * nx;
-    const size_t su = (size_t)qp * N * nu, sx = (size_t)qp * (N + 1) * nx;
-    c.lbu = a.lbu ? a.lbu + su : nullptr;
-    c.ubu = a.ubu ? a.ubu + su : nullptr;
-    c.lbum = a.lbu_mask ? a.lbu_mask + su : nullptr;
-    c.ubum = a.ubu_mask ? a.ubu_mask + su : nullptr;
-    c.lbx = a.lbx ? a.lbx + sx : nullptr;
-    c.ubx = a.ubx ? a.ubx + sx : nullptr;
-    c.lbxm = a.lbx_mask ? a.lbx_mask + sx : nullptr;
-    c.ubxm = a.ubx_mask ? a.ubx_mask + sx : nullptr;
-    c.x = a.x + sx;
-    c.u = a.u + su;
-    c.pi = a.pi + sx;
-    c.ws = a.ws + (size_t)qp * a.ws_qp;
-    c.ng = a.ng;
-    c.nch = (a.ng + kMaxDim - 1) / kMaxDim;
-    c.stride = (size_t)kIpmStage + (size_t)c.nch * kGenChunk;
-    if constexpr (GEN) {
-      const size_t gx = (size_t)qp * (N + 1) * a.ng;
-      c.C = a.C ? a.C + gx * nx : nullptr;
-      c.D = a.D ? a.D + (size_t)qp * N * a.ng * nu : nullptr;
-      c.lg = a.lg + gx;
-      c.ug = a.ug + gx;
-      c.lgm = a.lg_mask ? a.lg_mask + gx : nullptr;
-      c.ugm = a.ug_mask ? a.ug_mask + gx : nullptr;
-    }
-  }
+  c.qp = qp;
+  c.ng = a.ng;
+  c.nch = (a.ng + kMaxDim - 1) / kMaxDim;
+  c.stride = (size_t)kIpmStage + (size_t)c.nch * kGenChunk;
+  c.ws_qp = a.ws_qp;
+  c.bA = a.A; c.bB = a.B; c.bb = a.b; c.bQ = a.Q; c.bS = a.S; c.bR = a.R; c.bq = a.q; c.br = a.r;
+  c.bx0 = a.x0;
+  c.blbu = a.lbu; c.bubu = a.ubu; c.blbum = a.lbu_mask; c.bubum = a.ubu_mask;
+  c.blbx = a.lbx; c.bubx = a.ubx; c.blbxm = a.lbx_mask; c.bubxm = a.ubx_mask;
+  c.bC = GEN ? a.C : nullptr; c.bD = GEN ? a.D : nullptr;
+  c.blg = a.lg; c.bug = a.ug; c.blgm = a.lg_mask; c.bugm = a.ug_mask;
+  c.bxo = a.x; c.buo = a.u; c.bpi = a.pi; c.bws = a.ws;
   const double reg = a.reg;
 
   // ---- general rows (GEN): Gamma / gamma and their images under C, D ----
@@ -420,6 +440,9 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
     }
   };
 
+
+  double* const qs = c.ws();  // per-QP scalar state (kQs*)
+  if constexpr (PH == kPhInit) {
   // =================== init (var_init_scheme 0, relative form) ===================
   double ncl = 0.0;
   for (int k = 0; k <= N; ++k) {
@@ -427,7 +450,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
     double ui = 0.0, xi = 0.0;  // initial u_k, x_k (element-owned)
     // u_k
     if (k < N) {
-      double v = (a.warm_start && uel) ? c.u[(size_t)k * nu + li] : 0.0;
+      double v = (a.warm_start && uel) ? c.u()[(size_t)k * nu + li] : 0.0;
       const Side s = c.side_u(k, lane);
       Bar bb{0.0, 0.0, 1.0, 1.0};
       if (s.ml != 0.0 || s.mu != 0.0) {
@@ -463,16 +486,16 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
       }
       ncl += s.ml + s.mu;
       if (lane < kMaxDim) store_bar(stk, 0, lane, bb);
-      if (uel) c.u[(size_t)k * nu + lane] = v;
+      if (uel) c.u()[(size_t)k * nu + lane] = v;
       ui = uel ? v : 0.0;
     }
     // x_k
     {
       double v;
       if (k == 0) {
-        v = xel ? c.x0[li] : 0.0;
+        v = xel ? c.x0()[li] : 0.0;
       } else {
-        v = (a.warm_start && xel) ? c.x[(size_t)k * nx + li] : 0.0;
+        v = (a.warm_start && xel) ? c.x()[(size_t)k * nx + li] : 0.0;
       }
       const Side s = c.side_x(k, lane);
       Bar bb{0.0, 0.0, 1.0, 1.0};
@@ -510,8 +533,8 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
       ncl += s.ml + s.mu;
       if (lane < kMaxDim) store_bar(stk, 1, lane, bb);
       if (xel) {
-        c.x[(size_t)k * nx + lane] = v;
-        c.pi[(size_t)k * nx + lane] = 0.0;
+        c.x()[(size_t)k * nx + lane] = v;
+        c.pi()[(size_t)k * nx + lane] = 0.0;
       }
       xi = xel ? v : 0.0;
     }
@@ -554,15 +577,127 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
     }
   }
   const double nc = gsum(lane < kMaxDim ? ncl : 0.0);
+  if (lane == 0) {
+    qs[kQsAlphaP] = 0.0;
+    qs[kQsAlphaD] = 0.0;
+    qs[kQsLastAmin] = 1.0;
+    qs[kQsSigmaMu] = 0.0;
+    qs[kQsStatus] = -1.0;
+    qs[kQsIter] = 0.0;
+    qs[kQsNc] = nc;
+  }
+
+    return;
+  }
+  const double nc = qs[kQsNc];
   const double nc_inv = nc > 0.0 ? 1.0 / nc : 0.0;
-
-  double alpha_p = 0.0, alpha_d = 0.0;  // step applied by the next RU pass
-  double res_stat = 0.0, res_eq = 0.0, res_ineq = 0.0, res_comp = 0.0, obj = 0.0, mu = 0.0;
-  int iter = 0, status = -1;
-  double last_amin = 1.0;
-
-  int par = 0;  // parity of the record the current iteration's factorization writes
-  for (;;) {
+  int status = (int)qs[kQsStatus];
+  const int iter = (int)qs[kQsIter];
+  if constexpr (PH == kPhOut) {
+    const double res_stat = qs[kQsResStat], res_eq = qs[kQsResEq], res_ineq = qs[kQsResIneq];
+    const double res_comp = qs[kQsResComp], obj = qs[kQsObj];
+    if (status < 0) status = 1;  // not reached: the last RB sweep always decides
+    const int par = iter & 1;
+  // =================== outputs ===================
+  // Riccati factors of the last completed iteration (HPIPM's getters); the
+  // exiting sweep's own factorization is used only when no step was taken.
+  const int out_par = iter > 0 ? (par ^ 1) : par;
+  // pi_0 := Q0 x0 + S0'u0 + q0 + A0'(pi_1 + P_1 res_b0): the value of the
+  // stage-0 rebuild (ocp_qp_ipm_solver.cpp:347-373) with p_1 = pi_1 - P_1 x_1.
+  {
+    const double* st0 = c.st(0);
+    const double* st1 = c.st(1) + out_par * kRecSize;
+    double bx0[12], bu0[12];
+    gather12(xel ? c.x()[li] : 0.0, bx0);
+    gather12(uel ? c.u()[li] : 0.0, bu0);
+    double P1c[12], brb[12];
+    load_packed_sym(st1 + kRecP, col, P1c);
+    gather12(lane < kMaxDim ? st0[kStRes + 24 + lane] : 0.0, brb);
+    double t = xel ? c.pi()[(size_t)nx + lane] : 0.0;
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      t = fmadd(P1c[J], brb[J], t);
+    });
+    if (!xel) t = 0.0;
+    double bt[12];
+    gather12(t, bt);
+    double Qc[12], Sc[12], Ac[12];
+    c.col(c.Q(), nx, col, xel, Qc);
+    c.col(c.S(), nu, col, xel, Sc);
+    c.col(c.A(), nx, col, xel, Ac);
+    double p0 = c.el(c.q(), nx, li);
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      p0 = fmadd(Qc[J], bx0[J], p0);
+      p0 = fmadd(Sc[J], bu0[J], p0);
+      p0 = fmadd(Ac[J], bt[J], p0);
+    });
+    if (xel) c.pi()[lane] = p0;
+  }
+  if (a.P || a.p || a.K || a.k) {
+    // Riccati matrices of the last factorization (HPIPM's get_ric_* getters),
+    // vectors by consistency: p_k = pi_k - P_k x_k, k_k = u_k - K_k x_k.
+    const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu;
+    for (int k = 0; k <= N; ++k) {
+      const double* stk = c.st(k) + out_par * kRecSize;
+      double bxk[12];
+      gather12(xel ? c.x()[(size_t)k * nx + li] : 0.0, bxk);
+      double Pc[12];
+      load_packed_sym(stk + kRecP, col, Pc);
+      if (a.P && xel)
+        sfor<0, 12>([&](auto i) {
+          constexpr int I = decltype(i)::value;
+          if (I < nx) a.P[((size_t)qp * (N + 1) + k) * nxx + (size_t)lane * nx + I] = Pc[I];
+        });
+      if (a.p) {
+        double px = 0.0;
+        sfor<0, 12>([&](auto j) {
+          constexpr int J = decltype(j)::value;
+          px = fmadd(Pc[J], bxk[J], px);
+        });
+        if (xel) a.p[((size_t)qp * (N + 1) + k) * nx + lane] = c.pi()[(size_t)k * nx + lane] - px;
+      }
+      if (k < N) {
+        double Kc[12];
+        load12(stk + kRecK + col * 12, Kc);
+        if (a.K && xel)
+          sfor<0, 12>([&](auto i) {
+            constexpr int I = decltype(i)::value;
+            if (I < nu) a.K[((size_t)qp * N + k) * nxu + (size_t)lane * nu + I] = Kc[I];
+          });
+        if (a.k) {
+          double Kr[12];
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            Kr[J] = stk[kRecK + J * 12 + li];
+          });
+          double kx = 0.0;
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            kx = fmadd(Kr[J], bxk[J], kx);
+          });
+          if (uel) a.k[((size_t)qp * N + k) * nu + lane] = c.u()[(size_t)k * nu + lane] - kx;
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    if (a.status) a.status[qp] = status;
+    if (a.iter) a.iter[qp] = nc > 0.0 ? iter : 0;
+    if (a.res) {
+      a.res[(size_t)qp * 4 + 0] = res_stat;
+      a.res[(size_t)qp * 4 + 1] = res_eq;
+      a.res[(size_t)qp * 4 + 2] = res_ineq;
+      a.res[(size_t)qp * 4 + 3] = res_comp;
+    }
+    if (a.obj) a.obj[qp] = obj;
+  }
+    return;
+  }
+  if (status >= 0) return;  // this QP has exited
+  const int par = iter & 1;  // record written by this iteration's factorization
+  const double alpha_p = qs[kQsAlphaP], alpha_d = qs[kQsAlphaD], last_amin = qs[kQsLastAmin];
+  if constexpr (PH == kPhRB) {
     // =========== RB (k = N..0): update + residuals + Gamma/gamma + factorization ===========
     // One backward sweep per iteration: stage k applies the previous step to its
     // variables, forms its residuals (x_{k+1}, pi_{k+1} were updated by stage k+1),
@@ -578,17 +713,17 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
       // ---- apply the previous step to stage k ----
       double uk = 0.0, xk = 0.0, pik = 0.0;
       if (k < N && uel) {
-        uk = c.u[(size_t)k * nu + lane] + alpha_p * stk[kStStep + lane];
-        c.u[(size_t)k * nu + lane] = uk;
+        uk = c.u()[(size_t)k * nu + lane] + alpha_p * stk[kStStep + lane];
+        c.u()[(size_t)k * nu + lane] = uk;
       }
       if (xel) {
         if (k == 0) {
-          xk = c.x[li];  // x_0 = x0 (never updated); pi_0 is not an iterate
+          xk = c.x()[li];  // x_0 = x0 (never updated); pi_0 is not an iterate
         } else {
-          xk = c.x[(size_t)k * nx + lane] + alpha_p * stk[kStStep + 12 + lane];
-          pik = c.pi[(size_t)k * nx + lane] + alpha_d * stk[kStStep + 24 + lane];
-          c.x[(size_t)k * nx + lane] = xk;
-          c.pi[(size_t)k * nx + lane] = pik;
+          xk = c.x()[(size_t)k * nx + lane] + alpha_p * stk[kStStep + 12 + lane];
+          pik = c.pi()[(size_t)k * nx + lane] + alpha_d * stk[kStStep + 24 + lane];
+          c.x()[(size_t)k * nx + lane] = xk;
+          c.pi()[(size_t)k * nx + lane] = pik;
         }
       }
       Bar bu{0, 0, 1, 1}, bx{0, 0, 1, 1};
@@ -617,9 +752,9 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         gather12(pin, bpn);
         {
           double Qc[12];
-          c.col(c.Q + (size_t)k * c.nxx(), nx, col, xel, Qc);
+          c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
           const double qx = dot12(Qc, bxk, 0.0);
-          const double qk = c.el(c.q + (size_t)k * nx, nx, li);
+          const double qk = c.el(c.q() + (size_t)k * nx, nx, li);
           rgx = qx + qk - pik;
           if (k > 0) objl += xk * (0.5 * qx + qk);
         }
@@ -628,35 +763,35 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           double ru, sx_, stu, btp, atp;
           {
             double M[12];
-            c.col(c.R + (size_t)k * c.nuu(), nu, col, uel, M);
+            c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, M);
             ru = dot12(M, buk, 0.0);
           }
           SRBD_PHASE_FENCE();
           {
             double M[12];
-            c.row(c.S + (size_t)k * c.nxu(), nu, nx, li, uel, M);
+            c.row(c.S() + (size_t)k * c.nxu(), nu, nx, li, uel, M);
             sx_ = dot12(M, bxk, 0.0);
           }
           SRBD_PHASE_FENCE();
           {
             double M[12];
-            c.col(c.S + (size_t)k * c.nxu(), nu, col, xel, M);
+            c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, M);
             stu = dot12(M, buk, 0.0);
           }
           SRBD_PHASE_FENCE();
           {
             double M[12];
-            c.col(c.B + (size_t)k * c.nxu(), nx, col, uel, M);
+            c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, M);
             btp = dot12(M, bpn, 0.0);
           }
           SRBD_PHASE_FENCE();
           {
             double M[12];
-            c.col(c.A + (size_t)k * c.nxx(), nx, col, xel, M);
+            c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, M);
             atp = dot12(M, bpn, 0.0);
           }
           SRBD_PHASE_FENCE();
-          const double rk = c.el(c.r + (size_t)k * nu, nu, li);
+          const double rk = c.el(c.r() + (size_t)k * nu, nu, li);
           rgu = ru + sx_ + rk + btp;
           rgx += stu + atp;
           objl += uk * (0.5 * ru + rk + sx_);
@@ -664,17 +799,17 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           double ax;
           {
             double M[12];
-            c.row(c.A + (size_t)k * c.nxx(), nx, nx, li, xel, M);
+            c.row(c.A() + (size_t)k * c.nxx(), nx, nx, li, xel, M);
             ax = dot12(M, bxk, 0.0);
           }
           SRBD_PHASE_FENCE();
           {
             double M[12];
-            c.row(c.B + (size_t)k * c.nxu(), nx, nu, li, xel, M);
+            c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, M);
             ax = dot12(M, buk, ax);
           }
           SRBD_PHASE_FENCE();
-          rb = ax + c.el(c.b + (size_t)k * nx, nx, li) - xn;
+          rb = ax + c.el(c.b() + (size_t)k * nx, nx, li) - xn;
         }
         if constexpr (GEN) {
           // general rows: apply the step, residuals, res_g += C'(lam_u - lam_l), D'(..)
@@ -778,7 +913,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         // terminal stage: P_N = Q_N + diag(Gamma_x) (+ C'Gamma C), p_N = q~_N
         double qv[12];
         gather12(qt, qv);
-        c.col(c.Q + (size_t)N * c.nxx(), nx, col, xel, P);
+        c.col(c.Q() + (size_t)N * c.nxx(), nx, col, xel, P);
         if constexpr (GEN) g_hess(N, 2, P, P);
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
@@ -791,8 +926,8 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         double bv[12];
         gather12(rb, bv);
         double A_[12], B_[12];
-        c.col(c.A + (size_t)k * c.nxx(), nx, col, xel, A_);
-        c.col(c.B + (size_t)k * c.nxu(), nx, col, uel, B_);
+        c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, A_);
+        c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, B_);
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
           if (c.isv) {
@@ -801,7 +936,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           }
         });
         auto loadR = [&](double (&Rc)[12]) {
-          c.col(c.R + (size_t)k * c.nuu(), nu, col, uel, Rc);
+          c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, Rc);
           if constexpr (GEN) g_hess(k, 0, Rc, Rc);
           sfor<0, 12>([&](auto i) {
             constexpr int I = decltype(i)::value;
@@ -810,8 +945,8 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           });
         };
         auto loadSQ = [&](double (&Sc)[12], double (&Qc)[12]) {
-          c.col(c.S + (size_t)k * c.nxu(), nu, col, xel, Sc);
-          c.col(c.Q + (size_t)k * c.nxx(), nx, col, xel, Qc);
+          c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, Sc);
+          c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
           if constexpr (GEN) g_hess(k, 1, Sc, Qc);
           sfor<0, 12>([&](auto i) {
             constexpr int I = decltype(i)::value;
@@ -845,14 +980,14 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
       xn = xk;
       pin = pik;
     }
-    res_stat = gmax(lane < kMaxDim ? mg : 0.0);
-    res_eq = gmax(lane < kMaxDim ? mb : 0.0);
-    res_ineq = gmax(lane < kMaxDim ? md : 0.0);
-    res_comp = gmax(lane < kMaxDim ? mm : 0.0);
-    obj = gsum(lane < kMaxDim ? objl : 0.0);
+    const double res_stat = gmax(lane < kMaxDim ? mg : 0.0);
+    const double res_eq = gmax(lane < kMaxDim ? mb : 0.0);
+    const double res_ineq = gmax(lane < kMaxDim ? md : 0.0);
+    const double res_comp = gmax(lane < kMaxDim ? mm : 0.0);
+    const double obj = gsum(lane < kMaxDim ? objl : 0.0);
     const double musum_all = gsum(lane < kMaxDim ? musum : 0.0);
-    mu = musum_all * nc_inv;
-    double* stat_row = a.stat && lane == 0
+    const double mu = musum_all * nc_inv;
+    double* const stat_row = a.stat && lane == 0
                            ? a.stat + ((size_t)qp * (a.iter_max + 2) + iter) * kStatCols
                            : nullptr;
     if (stat_row) {
@@ -878,34 +1013,29 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
       } else if (iter > 0 && last_amin < a.alpha_min) {
         status = 2;
       }
-      if (status >= 0) break;
+    }
+    if (lane == 0) {
+      qs[kQsMu] = mu;
+      qs[kQsMuSum] = musum_all;
+      qs[kQsResStat] = res_stat;
+      qs[kQsResEq] = res_eq;
+      qs[kQsResIneq] = res_ineq;
+      qs[kQsResComp] = res_comp;
+      qs[kQsObj] = obj;
+      qs[kQsStatus] = (double)status;
     }
 
-    // =================== F1 / M / B2 / F2 ===================
-    double sigma_mu = 0.0, alpha_aff = 0.0, mu_aff = 0.0, sigma = 0.0;
-    const int npass = a.pred_corr ? 2 : 1;
-    double ap = 1e300, ad = 1e300;
-    double s1 = 0.0, s2 = 0.0;  // predictor sums lam dt + t dlam, dlam dt (element-owned)
-    for (int pass = 0; pass < npass; ++pass) {
-      const bool corr = pass == 1;
-      if (corr) {
-        // ---- alpha_aff, mu_aff, sigma: mu_aff from the predictor sums of F1,
-        // sum (lam + a dlam)(t + a dt) = S0 + a S1 + a^2 S2 (no extra sweep) ----
-        const double aa = fmin(1.0, fmin(gmin(ap), gmin(ad)));
-        alpha_aff = aa;
-        const double S1 = gsum(lane < kMaxDim ? s1 : 0.0), S2 = gsum(lane < kMaxDim ? s2 : 0.0);
-        mu_aff = (musum_all + aa * (S1 + aa * S2)) * nc_inv;
-        double sg = mu > 0.0 ? mu_aff / mu : 0.0;
-        sg = sg * sg * sg;
-        if (sg > 1.0) sg = 1.0;
-        sigma = sg;
-        sigma_mu = sg * mu;
+    return;
+  }
+  const double mu = qs[kQsMu], musum_all = qs[kQsMuSum];
+  double sigma_mu = qs[kQsSigmaMu];
+  if constexpr (PH == kPhB2) {
         // ---- B2: corrector vectors (element-owned recursion) ----
         double pnext = 0.0;  // p_{k+1}, element-owned
         {
           double* stN = c.st(N);
           const Side sx = c.side_x(N, lane);
-          const double xv = xel ? c.x[(size_t)N * nx + lane] : 0.0;
+          const double xv = xel ? c.x()[(size_t)N * nx + lane] : 0.0;
           double G = 0.0, g = 0.0;
           if (lane < kMaxDim) {
             const BarStep dx = load_bstep(stN, 1, lane);
@@ -924,8 +1054,8 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           double* rec = stk + par * kRecSize;
           const double* recn = c.st(k + 1) + par * kRecSize;
           const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
-          const double uv = uel ? c.u[(size_t)k * nu + lane] : 0.0;
-          const double xv = xel ? c.x[(size_t)k * nx + lane] : 0.0;
+          const double uv = uel ? c.u()[(size_t)k * nu + lane] : 0.0;
+          const double xv = xel ? c.x()[(size_t)k * nx + lane] : 0.0;
           double Gu = 0.0, gu = 0.0, Gx = 0.0, gx = 0.0;
           if (lane < kMaxDim) {
             const BarStep du = load_bstep(stk, 0, lane), dx = load_bstep(stk, 1, lane);
@@ -952,8 +1082,8 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           });
           // g = r~ + B'w ; f = q~ + A'w
           double Bc[12], Ac[12], bw[12];
-          c.col(c.B + (size_t)k * c.nxu(), nx, col, uel, Bc);
-          c.col(c.A + (size_t)k * c.nxx(), nx, col, xel, Ac);
+          c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, Bc);
+          c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, Ac);
           gather12(w, bw);
           double g = rt, f = qt;
           sfor<0, 12>([&](auto j) {
@@ -992,7 +1122,7 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           const double kv = lane < kMaxDim && uel ? -y : 0.0;
           // bcl = b~ + B k (row-owned B)
           double Br[12], bk[12];
-          c.row(c.B + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
+          c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
           gather12(kv, bk);
           double bcl = bt;
           sfor<0, 12>([&](auto j) {
@@ -1006,7 +1136,12 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
           }
           pnext = xel ? pv : 0.0;
         }
-      }
+    return;
+  }
+  if constexpr (PH == kPhF1 || PH == kPhF2) {
+    constexpr bool corr = PH == kPhF2;
+    double ap = 1e300, ad = 1e300;
+    double s1 = 0.0, s2 = 0.0;  // predictor sums lam dt + t dlam, dlam dt (element-owned)
       // ---- forward step (F1 predictor / F2 corrector), row-owned ----
       ap = 1e300;
       ad = 1e300;
@@ -1073,8 +1208,8 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         if (lane < kMaxDim) {
           const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
           const Bar bu = load_bar(stk, 0, lane), bx = load_bar(stk, 1, lane);
-          const double uv = (uel && k < N) ? c.u[(size_t)k * nu + lane] : 0.0;
-          const double xv = xel ? c.x[(size_t)k * nx + lane] : 0.0;
+          const double uv = (uel && k < N) ? c.u()[(size_t)k * nu + lane] : 0.0;
+          const double xv = xel ? c.x()[(size_t)k * nx + lane] : 0.0;
           double eul = 0.0, euu = 0.0, exl = 0.0, exu = 0.0, smu = 0.0;
           if (corr) {
             const BarStep pu = load_bstep(stk, 0, lane), px = load_bstep(stk, 1, lane);
@@ -1100,122 +1235,45 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
         }
         dxk = dxn;
       }
-    }
-    // ---- step length ----
-    ap = gmin(lane < kMaxDim ? ap : 1e300);
-    ad = gmin(lane < kMaxDim ? ad : 1e300);
-    if (!a.split_step) {
-      ap = fmin(ap, ad);
-      ad = ap;
-    }
-    alpha_p = fmin(1.0, kStepTau * ap);
-    alpha_d = fmin(1.0, kStepTau * ad);
-    last_amin = fmin(alpha_p, alpha_d);
-    par ^= 1;
-    if (stat_row) {
-      double* next = stat_row + kStatCols;  // HPIPM stores step kk in row kk+1
-      next[0] = alpha_aff;
-      next[1] = mu_aff;
-      next[2] = sigma;
-      next[3] = alpha_p;
-      next[4] = alpha_d;
-    }
-    ++iter;
-  }
-
-  // =================== outputs ===================
-  // Riccati factors of the last completed iteration (HPIPM's getters); the
-  // exiting sweep's own factorization is used only when no step was taken.
-  const int out_par = iter > 0 ? (par ^ 1) : par;
-  // pi_0 := Q0 x0 + S0'u0 + q0 + A0'(pi_1 + P_1 res_b0): the value of the
-  // stage-0 rebuild (ocp_qp_ipm_solver.cpp:347-373) with p_1 = pi_1 - P_1 x_1.
-  {
-    const double* st0 = c.st(0);
-    const double* st1 = c.st(1) + out_par * kRecSize;
-    double bx0[12], bu0[12];
-    gather12(xel ? c.x[li] : 0.0, bx0);
-    gather12(uel ? c.u[li] : 0.0, bu0);
-    double P1c[12], brb[12];
-    load_packed_sym(st1 + kRecP, col, P1c);
-    gather12(lane < kMaxDim ? st0[kStRes + 24 + lane] : 0.0, brb);
-    double t = xel ? c.pi[(size_t)nx + lane] : 0.0;
-    sfor<0, 12>([&](auto j) {
-      constexpr int J = decltype(j)::value;
-      t = fmadd(P1c[J], brb[J], t);
-    });
-    if (!xel) t = 0.0;
-    double bt[12];
-    gather12(t, bt);
-    double Qc[12], Sc[12], Ac[12];
-    c.col(c.Q, nx, col, xel, Qc);
-    c.col(c.S, nu, col, xel, Sc);
-    c.col(c.A, nx, col, xel, Ac);
-    double p0 = c.el(c.q, nx, li);
-    sfor<0, 12>([&](auto j) {
-      constexpr int J = decltype(j)::value;
-      p0 = fmadd(Qc[J], bx0[J], p0);
-      p0 = fmadd(Sc[J], bu0[J], p0);
-      p0 = fmadd(Ac[J], bt[J], p0);
-    });
-    if (xel) c.pi[lane] = p0;
-  }
-  if (a.P || a.p || a.K || a.k) {
-    // Riccati matrices of the last factorization (HPIPM's get_ric_* getters),
-    // vectors by consistency: p_k = pi_k - P_k x_k, k_k = u_k - K_k x_k.
-    const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu;
-    for (int k = 0; k <= N; ++k) {
-      const double* stk = c.st(k) + out_par * kRecSize;
-      double bxk[12];
-      gather12(xel ? c.x[(size_t)k * nx + li] : 0.0, bxk);
-      double Pc[12];
-      load_packed_sym(stk + kRecP, col, Pc);
-      if (a.P && xel)
-        sfor<0, 12>([&](auto i) {
-          constexpr int I = decltype(i)::value;
-          if (I < nx) a.P[((size_t)qp * (N + 1) + k) * nxx + (size_t)lane * nx + I] = Pc[I];
-        });
-      if (a.p) {
-        double px = 0.0;
-        sfor<0, 12>([&](auto j) {
-          constexpr int J = decltype(j)::value;
-          px = fmadd(Pc[J], bxk[J], px);
-        });
-        if (xel) a.p[((size_t)qp * (N + 1) + k) * nx + lane] = c.pi[(size_t)k * nx + lane] - px;
-      }
-      if (k < N) {
-        double Kc[12];
-        load12(stk + kRecK + col * 12, Kc);
-        if (a.K && xel)
-          sfor<0, 12>([&](auto i) {
-            constexpr int I = decltype(i)::value;
-            if (I < nu) a.K[((size_t)qp * N + k) * nxu + (size_t)lane * nu + I] = Kc[I];
-          });
-        if (a.k) {
-          double Kr[12];
-          sfor<0, 12>([&](auto j) {
-            constexpr int J = decltype(j)::value;
-            Kr[J] = stk[kRecK + J * 12 + li];
-          });
-          double kx = 0.0;
-          sfor<0, 12>([&](auto j) {
-            constexpr int J = decltype(j)::value;
-            kx = fmadd(Kr[J], bxk[J], kx);
-          });
-          if (uel) a.k[((size_t)qp * N + k) * nu + lane] = c.u[(size_t)k * nu + lane] - kx;
-        }
+    double* const next = a.stat && lane == 0
+                             ? a.stat + ((size_t)qp * (a.iter_max + 2) + iter + 1) * kStatCols
+                             : nullptr;  // HPIPM stores step kk in row kk+1
+    if (!corr) {
+      // alpha_aff, mu_aff, sigma: sum (lam + a dlam)(t + a dt) = S0 + a S1 + a^2 S2
+      const double aa = fmin(1.0, fmin(gmin(ap), gmin(ad)));
+      const double S1 = gsum(lane < kMaxDim ? s1 : 0.0), S2 = gsum(lane < kMaxDim ? s2 : 0.0);
+      const double mu_aff = (musum_all + aa * (S1 + aa * S2)) * nc_inv;
+      double sg = mu > 0.0 ? mu_aff / mu : 0.0;
+      sg = sg * sg * sg;
+      if (sg > 1.0) sg = 1.0;
+      if (lane == 0) qs[kQsSigmaMu] = sg * mu;
+      if (next && a.pred_corr) {
+        next[0] = aa;
+        next[1] = mu_aff;
+        next[2] = sg;
       }
     }
-  }
-  if (lane == 0) {
-    if (a.status) a.status[qp] = status;
-    if (a.iter) a.iter[qp] = nc > 0.0 ? iter : 0;
-    if (a.res) {
-      a.res[(size_t)qp * 4 + 0] = res_stat;
-      a.res[(size_t)qp * 4 + 1] = res_eq;
-      a.res[(size_t)qp * 4 + 2] = res_ineq;
-      a.res[(size_t)qp * 4 + 3] = res_comp;
+    if (corr || !a.pred_corr) {
+      // ---- step length of the iteration ----
+      ap = gmin(lane < kMaxDim ? ap : 1e300);
+      ad = gmin(lane < kMaxDim ? ad : 1e300);
+      if (!a.split_step) {
+        ap = fmin(ap, ad);
+        ad = ap;
+      }
+      const double alpha_p_new = fmin(1.0, kStepTau * ap);
+      const double alpha_d_new = fmin(1.0, kStepTau * ad);
+      if (lane == 0) {
+        qs[kQsAlphaP] = alpha_p_new;
+        qs[kQsAlphaD] = alpha_d_new;
+        qs[kQsLastAmin] = fmin(alpha_p_new, alpha_d_new);
+        qs[kQsIter] = (double)(iter + 1);
+      }
+      if (next) {
+        next[3] = alpha_p_new;
+        next[4] = alpha_d_new;
+      }
     }
-    if (a.obj) a.obj[qp] = obj;
   }
 }
 
@@ -1223,27 +1281,37 @@ __global__ void __launch_bounds__(256) ipm_box_kernel(ProblemArgs a) {
 
 size_t ws_doubles_ipm(int N, int ng) {
   const int nch = (ng + kMaxDim - 1) / kMaxDim;
-  return (size_t)(N + 1) * ((size_t)kIpmStage + (size_t)nch * kGenChunk);
+  return kQsSize + (size_t)(N + 1) * ((size_t)kIpmStage + (size_t)nch * kGenChunk);
+}
+
+template <bool FULL, bool GEN>
+static hipError_t launch_phases(const ProblemArgs& a, hipStream_t stream) {
+  const int threads = 256;
+  const long long lanes = (long long)a.batch * kGroup;
+  const dim3 grid((unsigned)((lanes + threads - 1) / threads)), block(threads);
+  // Host-driven iteration: each sweep is its own launch, so every kernel gets
+  // the registers (and occupancy) of its own phase; QPs that have exited return
+  // at the top of every later launch.  iter_max + 1 factorization sweeps at
+  // most: the last one always decides (converged or MaxIterReached).
+  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhInit>), grid, block, 0, stream, a);
+  for (int it = 0;; ++it) {
+    hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB>), grid, block, 0, stream, a);
+    if (it >= a.iter_max) break;
+    hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF1>), grid, block, 0, stream, a);
+    if (a.pred_corr) {
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhB2>), grid, block, 0, stream, a);
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF2>), grid, block, 0, stream, a);
+    }
+  }
+  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut>), grid, block, 0, stream, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_ipm_box(const ProblemArgs& a, hipStream_t stream) {
   if (a.batch <= 0) return hipSuccess;
-  const int threads = 256;
-  const long long lanes = (long long)a.batch * kGroup;
-  const int blocks = (int)((lanes + threads - 1) / threads);
   const bool full = a.nx == 12 && a.nu == 12;
-  if (a.ng > 0) {
-    if (full)
-      hipLaunchKernelGGL((ipm_box_kernel<true, true>), dim3(blocks), dim3(threads), 0, stream, a);
-    else
-      hipLaunchKernelGGL((ipm_box_kernel<false, true>), dim3(blocks), dim3(threads), 0, stream, a);
-  } else {
-    if (full)
-      hipLaunchKernelGGL((ipm_box_kernel<true, false>), dim3(blocks), dim3(threads), 0, stream, a);
-    else
-      hipLaunchKernelGGL((ipm_box_kernel<false, false>), dim3(blocks), dim3(threads), 0, stream, a);
-  }
-  return hipGetLastError();
+  if (a.ng > 0) return full ? launch_phases<true, true>(a, stream) : launch_phases<false, true>(a, stream);
+  return full ? launch_phases<true, false>(a, stream) : launch_phases<false, false>(a, stream);
 }
 
 }  // namespace srbd
