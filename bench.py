@@ -30,15 +30,26 @@ PKG_DIR = REPO / "srbd-nmpc-solver_amd"
 METRIC = "SRBD OCP-QP solves/sec (N=20, nx=12, nu=12, fp64) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFS = 78.6     # FP64 vector/matrix
+FP32_PEAK_TFS = 157.3    # FP32 vector (MI355X spec sheet; 2x FP64)
+
+# solver settings of the reference caller (NMPC_solver.cpp:70-82)
+NMPC_SETTINGS = {"mode": "Speed", "iter_max": 30, "alpha_min": 1e-8, "mu0": 1e2,
+                 "tol_stat": 1e-4, "tol_eq": 1e-4, "tol_ineq": 1e-4, "tol_comp": 1e-4,
+                 "reg_prim": 1e-12, "warm_start": 0, "pred_corr": 1, "ric_alg": 0, "split_step": 1}
+# fp32: the stationarity floor of an fp32 iterate on SRBD data is ~1e-2
+F32_SETTINGS = dict(NMPC_SETTINGS, tol_stat=3e-2, tol_eq=1e-3, tol_ineq=1e-3, tol_comp=1e-3)
 
 WORKLOADS = {
-    # name: (N, constraints, default batch, description)
+    # name: (N, constraints, default batch, description[, dtype])
     "unconstr_n20": (20, "none", 65536,
                      "SRBD NMPC QP as the reference builds it (friction cone as barrier in the cost, "
                      "no inequalities), batch 65536, N=20"),
     "unconstr_n10_b4096": (10, "none", 4096, "BASELINE config 2: batch 4096, N=10"),
     "box_u_n20": (20, "box_u", 65536,
                   "BASELINE config 3: batch 65536, N=20, box constraints on u (IPM)"),
+    "cone_n40_f32": (40, "cone", 65536,
+                     "BASELINE config 5: batch 65536, N=40, friction-cone rows (ng=24), fp32 IPM",
+                     "f32"),
 }
 DEFAULT_WORKLOAD = "unconstr_n20"
 
@@ -59,14 +70,16 @@ def import_pkg():
     return mod
 
 
-def alg_bytes_per_qp(N, nx=12, nu=12, constraints="none"):
-    """dense interface read once + x, u, pi written once (fp64)."""
+def alg_bytes_per_qp(N, nx=12, nu=12, constraints="none", elem=8, ng=24):
+    """dense interface read once + x, u, pi written once."""
     stage = nx * nx + nx * nu + nx + nx * nx + nu * nx + nu * nu + nx + nu  # A B b Q S R q r
     vals = N * stage + nx * nx + nx + nx  # + terminal Q, q + x0
     if constraints == "box_u":
         vals += N * 2 * nu
+    if constraints == "cone":
+        vals += N * (ng * nx + ng * nu + 2 * ng)  # C, D, lg, ug per stage
     out = (N + 1) * nx + N * nu + (N + 1) * nx
-    return 8 * (vals + out)
+    return elem * (vals + out)
 
 
 def alg_flops_per_qp(N, nx=12, nu=12):
@@ -87,10 +100,11 @@ def make_shard(pkg, N, constraints, batch, rank, seed, pool):
     return qp, x0
 
 
-def to_device(pkg, qp, x0, batch, device):
+def to_device(pkg, qp, x0, batch, device, np_dtype=np.float64):
     import torch
-    p = qp.packed()
-    p["x0"] = np.ascontiguousarray(x0)
+    p = {k: (None if v is None else np.ascontiguousarray(v, dtype=np_dtype))
+         for k, v in qp.packed().items()}
+    p["x0"] = np.ascontiguousarray(x0, dtype=np_dtype)
     pool = qp.batch
     reps = (batch + pool - 1) // pool
     dt = {}
@@ -133,27 +147,28 @@ def main():
     pkg = import_pkg()
     capi = pkg.capi
 
-    N, constraints, default_batch, desc = WORKLOADS[args.workload]
+    wl = WORKLOADS[args.workload]
+    N, constraints, default_batch, desc = wl[:4]
+    dtype = wl[4] if len(wl) > 4 else "f64"
+    np_dtype = np.float32 if dtype == "f32" else np.float64
     batch = args.batch or default_batch
     log(f"[rank {rank}] workload={args.workload} batch/rank={batch} N={N} world={world}")
     t0 = time.perf_counter()
     qp, x0 = make_shard(pkg, N, constraints, batch, rank, args.seed, args.pool)
-    dt = to_device(pkg, qp, x0, batch, device)
+    dt = to_device(pkg, qp, x0, batch, device, np_dtype)
     log(f"[rank {rank}] generated + uploaded in {time.perf_counter() - t0:.1f}s")
 
     h = capi.Handle(N, 12, 12, qp.ng, qp.has_box_u, qp.has_box_x, capacity=batch, device=local_rank)
-    f64 = dict(dtype=torch.float64, device=device)
+    f64 = dict(dtype=torch.float32 if dtype == "f32" else torch.float64, device=device)
     sol_t = {"x": torch.zeros(batch, N + 1, 12, **f64), "u": torch.zeros(batch, N, 12, **f64),
              "pi": torch.zeros(batch, N + 1, 12, **f64),
              "status": torch.zeros(batch, dtype=torch.int32, device=device),
              "iter": torch.zeros(batch, dtype=torch.int32, device=device)}
-    data = capi.Data(**{k: (None if dt.get(k) is None else dt[k].data_ptr()) for k in capi.DATA_FIELDS})
-    sol = capi.Solution(**{k: (sol_t[k].data_ptr() if k in sol_t else None) for k in capi.SOL_FIELDS})
+    DataT, SolT = (capi.Data32, capi.Solution32) if dtype == "f32" else (capi.Data, capi.Solution)
+    data = DataT(**{k: (None if dt.get(k) is None else dt[k].data_ptr()) for k in capi.DATA_FIELDS})
+    sol = SolT(**{k: (sol_t[k].data_ptr() if k in sol_t else None) for k in capi.SOL_FIELDS})
     # solver settings of the reference caller (NMPC_solver.cpp:70-82)
-    settings = capi.settings_struct({"mode": "Speed", "iter_max": 30, "alpha_min": 1e-8, "mu0": 1e2,
-                                     "tol_stat": 1e-4, "tol_eq": 1e-4, "tol_ineq": 1e-4,
-                                     "tol_comp": 1e-4, "reg_prim": 1e-12, "warm_start": 0,
-                                     "pred_corr": 1, "ric_alg": 0, "split_step": 1})
+    settings = capi.settings_struct(F32_SETTINGS if dtype == "f32" else NMPC_SETTINGS)
     stream_ptr = h.stream()
     ext = torch.cuda.ExternalStream(stream_ptr, device=device)
 
@@ -205,13 +220,15 @@ def main():
     total_qps = batch * world
     value = total_qps * args.steps / t_max
     ms_per_step = t_max / args.steps * 1e3
-    bytes_qp = alg_bytes_per_qp(N, constraints=constraints)
+    bytes_qp = alg_bytes_per_qp(N, constraints=constraints, elem=4 if dtype == "f32" else 8)
     achieved_gbs = bytes_qp * batch / (kernel_ms * 1e-3) / 1e9
     flops_qp = alg_flops_per_qp(N)
 
     cpu = None
     if not args.no_cpu_baseline:
         cpu = cpu_baseline(pkg, qp, x0, settings_dict(settings), args.cpu_seconds)
+        if dtype == "f32":
+            cpu["sample"] += " (the oracle computes in fp64)"
 
     traffic = pmc_traffic(args.workload, batch)
     line = {
@@ -225,16 +242,19 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": dtype,
         "data": f"synthetic SRBD linearisations (seed {args.seed}; pool of {min(args.pool, batch)} "
                 f"distinct QPs per rank tiled to the batch), generated per rank",
         "config": {"workload": args.workload, "description": desc, "batch_per_gpu": batch,
                    "global_batch": total_qps, "N": N, "nx": 12, "nu": 12, "constraints": constraints,
                    "parallelism": f"dp{world} (independent QP shards)",
-                   "settings": "NMPC_solver.cpp:70-82 (Speed, iter_max 30, tol 1e-4, split_step)"},
+                   "settings": ("NMPC_solver.cpp:70-82 (Speed, iter_max 30, split_step) with fp32 "
+                                "tolerances stat 3e-2 / 1e-3" if dtype == "f32" else
+                                "NMPC_solver.cpp:70-82 (Speed, iter_max 30, tol 1e-4, split_step)")},
         "roofline": roofline(constraints, achieved_gbs, traffic, kernel_ms, bytes_qp, flops_qp, batch,
-                             iters),
-        "fp64_frac": flops_qp * batch / (kernel_ms * 1e-3) / (FP64_PEAK_TFS * 1e12),
+                             iters, dtype),
+        "fp_vector_frac_one_sweep": flops_qp * batch / (kernel_ms * 1e-3) /
+                                    ((FP32_PEAK_TFS if dtype == "f32" else FP64_PEAK_TFS) * 1e12),
         "success_rate": n_ok / batch,
         "iters_mean": float(iters.mean()), "iters_max": int(iters.max()),
         "cpu_baseline": cpu,
@@ -248,7 +268,8 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(constraints, achieved_gbs, traffic, kernel_ms, bytes_qp, flops_qp, batch, iters):
+def roofline(constraints, achieved_gbs, traffic, kernel_ms, bytes_qp, flops_qp, batch, iters,
+             dtype="f64"):
     """Unconstrained: one streaming sweep, HBM-bound.  IPM: every
     iteration re-sweeps the QP, so the binding roof is FP64 compute on the
     algorithmic flops x iterations actually taken (IPM rows)."""
@@ -261,10 +282,12 @@ def roofline(constraints, achieved_gbs, traffic, kernel_ms, bytes_qp, flops_qp, 
     it = float(np.mean(iters))
     flops = flops_qp * 1.4 * max(it, 1.0) * batch
     tf = flops / (kernel_ms * 1e-3) / 1e12
-    return {"bound": "mfma", "achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": tf / FP64_PEAK_TFS, "traffic": traffic, "kernel": "ipm_box_kernel<true>",
+    peak = FP32_PEAK_TFS if dtype == "f32" else FP64_PEAK_TFS
+    return {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s",
+            "frac": tf / peak, "traffic": traffic,
+            "kernel": "ipm_phase_kernel<*> (init, RB, F1, B2, F2, out per iteration)",
             "kernel_avg_ms": kernel_ms, "alg_flops_per_qp_iter": flops_qp * 1.4,
-            "mean_iters": it, "note": "FP64 is vector-rate on gfx950 (MFMA f64 = VALU peak)",
+            "mean_iters": it, "note": "no MFMA: 12x12 blocks run on the FP vector pipe (MFMA f64 = VALU rate)",
             "hbm_frac_of_alg_bytes": achieved_gbs / HBM_PEAK_GBS}
 
 

@@ -17,6 +17,8 @@
  *                        on a batch of device-resident QPs, asynchronous.
  *   srbd_qp_solve_host_f64  the same from host buffers, synchronous (what the
  *                        hpipm-cpp shim calls for one QP or a small batch).
+ *   srbd_qp_solve_f32 / _host_f32  the fp32 twins (HPIPM's s_ocp_qp_ipm_solve,
+ *                        hpipm_s_ocp_qp_ipm.h:238).
  *   srbd_qp_destroy      ~OcpQpIpmSolver (d_ocp_qp_*_wrapper frees).
  *   srbd_qp_status_string  hpipm::to_string(HpipmStatus) (:19-33).
  *
@@ -67,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SRBD_QP_ABI_VERSION 2
+#define SRBD_QP_ABI_VERSION 3
 #define SRBD_QP_MAX_NX 12
 #define SRBD_QP_MAX_NU 12
 #define SRBD_QP_MAX_NG 64
@@ -144,6 +146,26 @@ typedef struct srbd_qp_solution_f64 {
                             * (no LQ factorization / iterative refinement).    */
 } srbd_qp_solution_f64;
 
+/* fp32 twins (BASELINE config 5; HPIPM's s_ocp_qp_ipm, hpipm_s_ocp_qp_ipm.h:238):
+ * same fields, same layout, float elements.  Tolerances below ~1e-6 are not
+ * reachable in fp32; use the NMPC settings (1e-4). */
+typedef struct srbd_qp_data_f32 {
+  const float *A, *B, *b, *Q, *S, *R, *q, *r;
+  const float *lbu, *ubu, *lbu_mask, *ubu_mask;
+  const float *lbx, *ubx, *lbx_mask, *ubx_mask;
+  const float *C, *D, *lg, *ug, *lg_mask, *ug_mask;
+  const float *x0;
+} srbd_qp_data_f32;
+
+typedef struct srbd_qp_solution_f32 {
+  float *x, *u, *pi;
+  float *P, *p, *K, *k;
+  int *status, *iter;
+  float *res;
+  float *obj;
+  float *stat;
+} srbd_qp_solution_f32;
+
 typedef struct srbd_qp_handle_s* srbd_qp_handle;
 
 /* Fill *s with hpipm-cpp's defaults (Speed, iter_max 15, tol 1e-8, mu0 100,
@@ -170,6 +192,13 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* setti
 /* Host-buffer batch solve: copies to device, solves, copies back, waits.   */
 int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
                            const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol);
+
+/* fp32 twins of the two solve entry points (the handle serves both).      */
+int srbd_qp_solve_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
+                      const srbd_qp_data_f32* data, const srbd_qp_solution_f32* sol,
+                      void* stream);
+int srbd_qp_solve_host_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
+                           const srbd_qp_data_f32* data, const srbd_qp_solution_f32* sol);
 
 /* Blocks until all work queued on the handle's stream is done.            */
 int srbd_qp_synchronize(srbd_qp_handle h);

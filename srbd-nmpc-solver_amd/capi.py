@@ -53,6 +53,15 @@ class Solution(C.Structure):
     _fields_ = [(n, _dp) for n in SOL_FIELDS]
 
 
+# fp32 twins (srbd_qp_data_f32 / srbd_qp_solution_f32): same field order
+class Data32(C.Structure):
+    _fields_ = [(n, _dp) for n in DATA_FIELDS]
+
+
+class Solution32(C.Structure):
+    _fields_ = [(n, _dp) for n in SOL_FIELDS]
+
+
 MODES = {"SpeedAbs": 0, "Speed": 1, "Balance": 2, "Robust": 3}
 
 _lib = None
@@ -80,6 +89,12 @@ def lib():
         L.srbd_qp_solve_host_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
                                              C.POINTER(Data), C.POINTER(Solution)]
         L.srbd_qp_solve_host_f64.restype = C.c_int
+        L.srbd_qp_solve_f32.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
+                                        C.POINTER(Data32), C.POINTER(Solution32), C.c_void_p]
+        L.srbd_qp_solve_f32.restype = C.c_int
+        L.srbd_qp_solve_host_f32.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
+                                             C.POINTER(Data32), C.POINTER(Solution32)]
+        L.srbd_qp_solve_host_f32.restype = C.c_int
         L.srbd_qp_destroy.argtypes = [C.c_void_p]
         L.srbd_qp_destroy.restype = None
         L.srbd_qp_synchronize.argtypes = [C.c_void_p]
@@ -160,15 +175,14 @@ class Handle:
     def synchronize(self) -> None:
         check(lib().srbd_qp_synchronize(self._h), "srbd_qp_synchronize")
 
-    def solve_device(self, batch: int, settings: Settings, data: Data, sol: Solution,
-                     stream: int = 0) -> None:
-        check(lib().srbd_qp_solve_f64(self._h, int(batch), C.byref(settings), C.byref(data),
-                                      C.byref(sol), C.c_void_p(stream or None)),
-              "srbd_qp_solve_f64")
+    def solve_device(self, batch: int, settings: Settings, data, sol, stream: int = 0) -> None:
+        f = lib().srbd_qp_solve_f32 if isinstance(data, Data32) else lib().srbd_qp_solve_f64
+        check(f(self._h, int(batch), C.byref(settings), C.byref(data), C.byref(sol),
+                C.c_void_p(stream or None)), f.__name__)
 
-    def solve_host(self, batch: int, settings: Settings, data: Data, sol: Solution) -> None:
-        check(lib().srbd_qp_solve_host_f64(self._h, int(batch), C.byref(settings), C.byref(data),
-                                           C.byref(sol)), "srbd_qp_solve_host_f64")
+    def solve_host(self, batch: int, settings: Settings, data, sol) -> None:
+        f = lib().srbd_qp_solve_host_f32 if isinstance(data, Data32) else lib().srbd_qp_solve_host_f64
+        check(f(self._h, int(batch), C.byref(settings), C.byref(data), C.byref(sol)), f.__name__)
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -187,22 +201,24 @@ def _tensor_ptr(t) -> int:
 
 
 def device_buffers(qp, x0: np.ndarray, device="cuda:0", want_riccati: bool = False,
-                   x_init=None, u_init=None, stat_rows: int = 0):
+                   x_init=None, u_init=None, stat_rows: int = 0, dtype=np.float64):
     """Upload an OcpQpBatch (+x0) to device tensors in the C-ABI layout.
 
-    Returns (data_tensors, sol_tensors, Data, Solution)."""
+    dtype float64 -> srbd_qp_solve_f64 structs, float32 -> the fp32 twins.
+    Returns (data_tensors, sol_tensors, Data | Data32, Solution | Solution32)."""
     import torch
+    np_t = np.dtype(dtype)
     p = qp.packed()
     p["x0"] = np.ascontiguousarray(x0, dtype=np.float64).reshape(qp.batch, qp.nx)
-    dt = {k: (None if v is None else torch.from_numpy(np.ascontiguousarray(v)).to(device))
+    dt = {k: (None if v is None else torch.from_numpy(np.ascontiguousarray(v, dtype=np_t)).to(device))
           for k, v in p.items()}
     nb, N, nx, nu = qp.batch, qp.N, qp.nx, qp.nu
-    f64 = dict(dtype=torch.float64, device=device)
+    f64 = dict(dtype=torch.float32 if np_t == np.float32 else torch.float64, device=device)
     st = {
         "x": torch.zeros(nb, N + 1, nx, **f64) if x_init is None
-        else torch.from_numpy(np.ascontiguousarray(x_init, dtype=np.float64)).to(device),
+        else torch.from_numpy(np.ascontiguousarray(x_init, dtype=np_t)).to(device),
         "u": torch.zeros(nb, N, nu, **f64) if u_init is None
-        else torch.from_numpy(np.ascontiguousarray(u_init, dtype=np.float64)).to(device),
+        else torch.from_numpy(np.ascontiguousarray(u_init, dtype=np_t)).to(device),
         "pi": torch.zeros(nb, N + 1, nx, **f64),
         "status": torch.full((nb,), -1, dtype=torch.int32, device=device),
         "iter": torch.full((nb,), -1, dtype=torch.int32, device=device),
@@ -216,14 +232,15 @@ def device_buffers(qp, x0: np.ndarray, device="cuda:0", want_riccati: bool = Fal
         st["p"] = torch.zeros(nb, N + 1, nx, **f64)
         st["K"] = torch.zeros(nb, N, nx, nu, **f64)      # col-major nu x nx blocks
         st["k"] = torch.zeros(nb, N, nu, **f64)
-    data = Data(**{k: _tensor_ptr(dt.get(k)) or None for k in DATA_FIELDS})
-    sol = Solution(**{k: _tensor_ptr(st.get(k)) or None for k in SOL_FIELDS})
+    DataT, SolT = (Data32, Solution32) if np_t == np.float32 else (Data, Solution)
+    data = DataT(**{k: _tensor_ptr(dt.get(k)) or None for k in DATA_FIELDS})
+    sol = SolT(**{k: _tensor_ptr(st.get(k)) or None for k in SOL_FIELDS})
     return dt, st, data, sol
 
 
 def solve(qp, x0, settings: Optional[Dict] = None, device: str = "cuda:0", riccati: bool = False,
           x_init=None, u_init=None, handle: Optional[Handle] = None,
-          stats: bool = False) -> Dict[str, np.ndarray]:
+          stats: bool = False, dtype=np.float64) -> Dict[str, np.ndarray]:
     """Solve an OcpQpBatch on the GPU through the C-ABI; returns numpy results.
 
     stats=True also returns "stat" [batch][iter_max+2][18], the per-iteration
@@ -237,7 +254,7 @@ def solve(qp, x0, settings: Optional[Dict] = None, device: str = "cuda:0", ricca
                          capacity=qp.batch, device=dev_index)
     s = settings_struct(settings)
     dt, st, data, sol = device_buffers(qp, x0, device, riccati, x_init, u_init,
-                                       stat_rows=(s.iter_max + 2) if stats else 0)
+                                       stat_rows=(s.iter_max + 2) if stats else 0, dtype=dtype)
     h.solve_device(qp.batch, s, data, sol)
     h.synchronize()
     out = {k: v.cpu().numpy() for k, v in st.items()}

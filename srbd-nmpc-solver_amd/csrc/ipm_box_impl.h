@@ -1,0 +1,1288 @@
+// ipm_box_impl.h -- body of the batched IPM, instantiated once per precision by
+// ipm_box.hip (SRBD_REAL = double / float, namespace SRBD_NS), the way HPIPM
+// generates its d_ and s_ solvers from one source.  No include guard: included twice.
+// The kernel code is documented in ipm_box.hip.
+
+namespace srbd {
+namespace SRBD_NS {
+
+using real = SRBD_REAL;
+
+
+constexpr real kThr0 = real(0.1);     // minimum initial slack (HPIPM init_var)
+
+// phase kernels (one launch each, per IPM iteration; see launch_ipm_box)
+constexpr int kPhInit = 0, kPhRB = 1, kPhF1 = 2, kPhB2 = 3, kPhF2 = 4, kPhOut = 5;
+// per-QP scalar state, kQsSize reals at the head of the QP's workspace
+constexpr int kQsAlphaP = 0, kQsAlphaD = 1, kQsLastAmin = 2, kQsMu = 3, kQsMuSum = 4,
+              kQsSigmaMu = 5, kQsStatus = 6, kQsIter = 7, kQsNc = 8, kQsResStat = 9,
+              kQsResEq = 10, kQsResIneq = 11, kQsResComp = 12, kQsObj = 13, kQsSize = 16;
+constexpr real kStepTau = real(0.995);  // fraction to the boundary
+
+__device__ __forceinline__ real gsum(real v) {
+  v += __shfl_xor(v, 8, kGroup);
+  v += __shfl_xor(v, 4, kGroup);
+  v += __shfl_xor(v, 2, kGroup);
+  v += __shfl_xor(v, 1, kGroup);
+  return v;
+}
+__device__ __forceinline__ real gmax(real v) {
+  v = fmax(v, __shfl_xor(v, 8, kGroup));
+  v = fmax(v, __shfl_xor(v, 4, kGroup));
+  v = fmax(v, __shfl_xor(v, 2, kGroup));
+  v = fmax(v, __shfl_xor(v, 1, kGroup));
+  return v;
+}
+__device__ __forceinline__ real gmin(real v) {
+  v = fmin(v, __shfl_xor(v, 8, kGroup));
+  v = fmin(v, __shfl_xor(v, 4, kGroup));
+  v = fmin(v, __shfl_xor(v, 2, kGroup));
+  v = fmin(v, __shfl_xor(v, 1, kGroup));
+  return v;
+}
+// |v| propagating NaN (max with NaN would drop it)
+__device__ __forceinline__ real nabs(real v) { return v == v ? fabs(v) : real(__builtin_inf()); }
+
+// One inequality side on one variable (box bound, dense per variable).
+struct Side {
+  real lb, ub;   // bounds
+  real ml, mu;   // 1 if the lower / upper bound is active, else 0
+};
+
+template <bool FULL, bool GEN>
+struct Ctx {
+  int N, nx, nu, lane, qp;
+  bool isv;
+  int ng, nch;    // general rows, 12-row chunks
+  size_t stride;  // workspace doubles per stage
+  size_t ws_qp;   // workspace doubles per QP
+  // Batch base pointers (wave-uniform, SGPRs).  The per-QP pointers below are
+  // recomputed at every use from an opaque copy of qp, so the compiler cannot
+  // hoist ~27 64-bit per-lane pointers into VGPRs for the whole kernel.
+  const real *bA, *bB, *bb, *bQ, *bS, *bR, *bq, *br, *bx0;
+  const real *blbu, *bubu, *blbum, *bubum, *blbx, *bubx, *blbxm, *bubxm;
+  const real *bC, *bD, *blg, *bug, *blgm, *bugm;
+  real *bxo, *buo, *bpi, *bws;
+
+  __device__ size_t oq() const {
+    int v = qp;
+    asm volatile("" : "+v"(v));
+    return (size_t)v;
+  }
+  __device__ size_t sN() const { return oq() * N; }
+  __device__ size_t sN1() const { return oq() * (N + 1); }
+  __device__ const real* A() const { return bA + sN() * nxx(); }
+  __device__ const real* B() const { return bB + sN() * nxu(); }
+  __device__ const real* b() const { return bb + sN() * nx; }
+  __device__ const real* Q() const { return bQ + sN1() * nxx(); }
+  __device__ const real* S() const { return bS + sN() * nxu(); }
+  __device__ const real* R() const { return bR + sN() * nuu(); }
+  __device__ const real* q() const { return bq + sN1() * nx; }
+  __device__ const real* r() const { return br + sN() * nu; }
+  __device__ const real* x0() const { return bx0 + oq() * nx; }
+  __device__ const real* lbu() const { return blbu ? blbu + sN() * nu : nullptr; }
+  __device__ const real* ubu() const { return bubu ? bubu + sN() * nu : nullptr; }
+  __device__ const real* lbum() const { return blbum ? blbum + sN() * nu : nullptr; }
+  __device__ const real* ubum() const { return bubum ? bubum + sN() * nu : nullptr; }
+  __device__ const real* lbx() const { return blbx ? blbx + sN1() * nx : nullptr; }
+  __device__ const real* ubx() const { return bubx ? bubx + sN1() * nx : nullptr; }
+  __device__ const real* lbxm() const { return blbxm ? blbxm + sN1() * nx : nullptr; }
+  __device__ const real* ubxm() const { return bubxm ? bubxm + sN1() * nx : nullptr; }
+  __device__ const real* C() const { return bC ? bC + sN1() * ng * nx : nullptr; }
+  __device__ const real* D() const { return bD ? bD + sN() * ng * nu : nullptr; }
+  __device__ const real* lg() const { return blg + sN1() * ng; }
+  __device__ const real* ug() const { return bug + sN1() * ng; }
+  __device__ const real* lgm() const { return blgm ? blgm + sN1() * ng : nullptr; }
+  __device__ const real* ugm() const { return bugm ? bugm + sN1() * ng : nullptr; }
+  __device__ real* x() const { return bxo + sN1() * nx; }
+  __device__ real* u() const { return buo + sN() * nu; }
+  __device__ real* pi() const { return bpi + sN1() * nx; }
+  __device__ real* ws() const { return bws + oq() * ws_qp; }
+
+  __device__ size_t nxx() const { return FULL ? 144 : (size_t)nx * nx; }
+  __device__ size_t nxu() const { return FULL ? 144 : (size_t)nx * nu; }
+  __device__ size_t nuu() const { return FULL ? 144 : (size_t)nu * nu; }
+  __device__ real* st(int k) const {
+    return ws() + kQsSize + (size_t)k * (GEN ? stride : (size_t)kIpmStage);
+  }
+  // state of constraint chunk ch at stage k: bars [48], steps [48], row values [12]
+  __device__ real* gs(int k, int ch) const { return st(k) + kIpmStage + ch * kGenChunk; }
+  // row i of chunk ch (element-owned): lg <= v <= ug
+  __device__ Side side_g(int k, int ch, int i) const {
+    Side s{real(0.0), real(0.0), real(0.0), real(0.0)};
+    const int r = ch * kMaxDim + i;
+    if (i < kMaxDim && r < ng) {
+      const size_t o = (size_t)k * ng + r;
+      s.lb = lg()[o];
+      s.ub = ug()[o];
+      s.ml = lgm() ? (lgm()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
+      s.mu = ugm() ? (ugm()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
+    }
+    return s;
+  }
+  // row-owned C / D rows of chunk ch (lane i = row); C_0 dropped like the
+  // reference's x0 embedding (nx[0] = 0), D_N absent
+  __device__ void g_row(int k, int ch, int i, real (&Cr)[12], real (&Dr)[12]) const {
+    const int r = ch * kMaxDim + i;
+    const bool ok = i < kMaxDim && r < ng;
+    const bool cok = ok && bC && k > 0, dok = ok && bD && k < N;
+    const real* cb = C() ? C() + (size_t)k * ng * nx + r : nullptr;
+    const real* db = D() ? D() + (size_t)k * ng * nu + r : nullptr;
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      Cr[J] = (cok && J < nx) ? cb[(size_t)J * ng] : real(0.0);
+      Dr[J] = (dok && J < nu) ? db[(size_t)J * ng] : real(0.0);
+    });
+  }
+  // column-owned C / D columns restricted to chunk ch (lane j = column)
+  __device__ void g_col(int k, int ch, int j, real (&Cc)[12], real (&Dc)[12]) const {
+    const int r0 = ch * kMaxDim;
+    const bool cok = bC && k > 0 && j < nx, dok = bD && k < N && j < nu;
+    const real* cb = C() ? C() + (size_t)k * ng * nx + (size_t)j * ng + r0 : nullptr;
+    const real* db = D() ? D() + (size_t)k * ng * nu + (size_t)j * ng + r0 : nullptr;
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      Cc[I] = (cok && r0 + I < ng) ? cb[I] : real(0.0);
+      Dc[I] = (dok && r0 + I < ng) ? db[I] : real(0.0);
+    });
+  }
+
+  // ---- column-owned loads (lane = column), zero padded ----
+  __device__ void col(const real* blk, int rows, int c, bool ok, real (&v)[12]) const {
+    if constexpr (FULL) {
+      load12(blk + c * 12, v);
+    } else {
+      load_col_pad(blk + (size_t)c * rows, rows, ok, v);
+    }
+  }
+  // ---- row-owned loads (lane = row) of a column-major (rows x cols) block ----
+  __device__ void row(const real* blk, int rows, int cols, int rw, bool ok, real (&v)[12]) const {
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      if constexpr (FULL) {
+        v[J] = blk[rw + J * 12];
+      } else {
+        v[J] = (ok && J < cols) ? blk[(size_t)rw + (size_t)J * rows] : real(0.0);
+      }
+    });
+  }
+  // element i of a length-n vector (0 beyond n)
+  __device__ real el(const real* v, int n, int i) const {
+    if constexpr (FULL) {
+      return i < 12 ? v[i] : real(0.0);
+    } else {
+      return i < n ? v[i] : real(0.0);
+    }
+  }
+  __device__ Side side_u(int k, int i) const {
+    Side s{real(0.0), real(0.0), real(0.0), real(0.0)};
+    if (blbu && i < nu && k < N) {
+      const size_t o = (size_t)k * nu + i;
+      s.lb = lbu()[o];
+      s.ub = ubu()[o];
+      s.ml = lbum() ? (lbum()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
+      s.mu = ubum() ? (ubum()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
+    }
+    return s;
+  }
+  __device__ Side side_x(int k, int i) const {
+    Side s{real(0.0), real(0.0), real(0.0), real(0.0)};
+    if (blbx && i < nx && k > 0) {  // stage-0 x bounds dropped (x0 embedding)
+      const size_t o = (size_t)k * nx + i;
+      s.lb = lbx()[o];
+      s.ub = ubx()[o];
+      s.ml = lbxm() ? (lbxm()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
+      s.mu = ubxm() ? (ubxm()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
+    }
+    return s;
+  }
+};
+
+// barrier state of one variable: lam_l, lam_u, t_l, t_u
+struct Bar {
+  real ll, lu, tl, tu;
+};
+__device__ __forceinline__ Bar load_bar(const real* stk, int which, int i) {
+  const real* p = stk + kStLam + which * 48;
+  return Bar{p[i], p[12 + i], p[24 + i], p[36 + i]};
+}
+__device__ __forceinline__ void store_bar(real* stk, int which, int i, const Bar& b) {
+  real* p = stk + kStLam + which * 48;
+  p[i] = b.ll;
+  p[12 + i] = b.lu;
+  p[24 + i] = b.tl;
+  p[36 + i] = b.tu;
+}
+// step of one variable's barrier pair: dt_l, dt_u, dlam_l, dlam_u
+struct BarStep {
+  real dtl, dtu, dll, dlu;
+};
+__device__ __forceinline__ BarStep load_bstep(const real* stk, int which, int i) {
+  const real* p = stk + kStDlt + which * 48;
+  return BarStep{p[i], p[12 + i], p[24 + i], p[36 + i]};
+}
+__device__ __forceinline__ void store_bstep(real* stk, int which, int i, const BarStep& d) {
+  real* p = stk + kStDlt + which * 48;
+  p[i] = d.dtl;
+  p[12 + i] = d.dtu;
+  p[24 + i] = d.dll;
+  p[36 + i] = d.dlu;
+}
+
+// general-constraint chunk state (see kGenChunk)
+__device__ __forceinline__ Bar load_gbar(const real* g, int i) {
+  return Bar{g[i], g[12 + i], g[24 + i], g[36 + i]};
+}
+__device__ __forceinline__ void store_gbar(real* g, int i, const Bar& b) {
+  g[i] = b.ll;
+  g[12 + i] = b.lu;
+  g[24 + i] = b.tl;
+  g[36 + i] = b.tu;
+}
+__device__ __forceinline__ BarStep load_gstep(const real* g, int i) {
+  return BarStep{g[48 + i], g[60 + i], g[72 + i], g[84 + i]};
+}
+__device__ __forceinline__ void store_gstep(real* g, int i, const BarStep& d) {
+  g[48 + i] = d.dtl;
+  g[60 + i] = d.dtu;
+  g[72 + i] = d.dll;
+  g[84 + i] = d.dlu;
+}
+constexpr int kGenVal = 96;
+
+template <typename T>
+__device__ __forceinline__ T dot12(const T (&a)[12], const T (&b)[12], T acc) {
+  sfor<0, 12>([&](auto j) {
+    constexpr int J = decltype(j)::value;
+    acc = fmadd(a[J], b[J], acc);
+  });
+  return acc;
+}
+
+// Gamma (Hessian add) and gamma (gradient add) of one variable:
+// Gamma = lam_l/t_l + lam_u/t_u,
+// gamma = (rm_l + lam_l rd_l)/t_l - (rm_u + lam_u rd_u)/t_u, with
+// rm = lam t + extra - sigma_mu (extra = dlam_aff dt_aff in the corrector).
+__device__ __forceinline__ void gamma_of(const Side& s, const Bar& b, real v, real ext_l,
+                                         real ext_u, real smu, real& G, real& g) {
+  G = real(0.0);
+  g = real(0.0);
+  if (s.ml != real(0.0)) {
+    const real rd = v - s.lb - b.tl;
+    const real rm = b.ll * b.tl + ext_l - smu;
+    G += b.ll / b.tl;
+    g += (rm + b.ll * rd) / b.tl;
+  }
+  if (s.mu != real(0.0)) {
+    const real rd = s.ub - v - b.tu;
+    const real rm = b.lu * b.tu + ext_u - smu;
+    G += b.lu / b.tu;
+    g -= (rm + b.lu * rd) / b.tu;
+  }
+}
+
+// dt / dlam of one variable given its primal step dv.
+__device__ __forceinline__ BarStep bar_step(const Side& s, const Bar& b, real v, real dv,
+                                            real ext_l, real ext_u, real smu) {
+  BarStep d{real(0.0), real(0.0), real(0.0), real(0.0)};
+  if (s.ml != real(0.0)) {
+    const real rd = v - s.lb - b.tl;
+    d.dtl = rd + dv;
+    d.dll = -(b.ll * b.tl + ext_l - smu + b.ll * d.dtl) / b.tl;
+  }
+  if (s.mu != real(0.0)) {
+    const real rd = s.ub - v - b.tu;
+    d.dtu = rd - dv;
+    d.dlu = -(b.lu * b.tu + ext_u - smu + b.lu * d.dtu) / b.tu;
+  }
+  return d;
+}
+
+__device__ __forceinline__ void ratio(const Side& s, const Bar& b, const BarStep& d, real& ap,
+                                      real& ad) {
+  if (s.ml != real(0.0)) {
+    if (d.dtl < real(0.0)) ap = fmin(ap, -b.tl / d.dtl);
+    if (d.dll < real(0.0)) ad = fmin(ad, -b.ll / d.dll);
+  }
+  if (s.mu != real(0.0)) {
+    if (d.dtu < real(0.0)) ap = fmin(ap, -b.tu / d.dtu);
+    if (d.dlu < real(0.0)) ad = fmin(ad, -b.lu / d.dlu);
+  }
+}
+
+// predictor sums for mu_aff: s1 += lam dt + t dlam, s2 += dlam dt (active sides)
+__device__ __forceinline__ void aff_sums(const Side& s, const Bar& b, const BarStep& d, real& s1,
+                                         real& s2) {
+  if (s.ml != real(0.0)) {
+    s1 += b.ll * d.dtl + b.tl * d.dll;
+    s2 += d.dll * d.dtl;
+  }
+  if (s.mu != real(0.0)) {
+    s1 += b.lu * d.dtu + b.tu * d.dlu;
+    s2 += d.dlu * d.dtu;
+  }
+}
+
+// gather an element-owned value (lane i < 12 holds v_i) into VL's registers
+__device__ __forceinline__ void gather12(real v, real (&out)[12]) {
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    out[I] = bc<I>(v);
+  });
+}
+
+template <bool FULL, bool GEN, int PH>
+__global__ void __launch_bounds__(256, 2) ipm_phase_kernel(ProblemArgsT<real> a) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int qp = gid >> 4;
+  const int lane = threadIdx.x & (kGroup - 1);
+  if (qp >= a.batch) return;
+  const int N = a.N;
+  const int nx = FULL ? 12 : a.nx;
+  const int nu = FULL ? 12 : a.nu;
+  const int col = lane < kMaxDim ? lane : kMaxDim - 1;
+  const int li = lane < kMaxDim ? lane : 0;  // element index used for addressing
+  const bool xel = lane < nx, uel = lane < nu;
+
+  Ctx<FULL, GEN> c;
+  c.N = N;
+  c.nx = nx;
+  c.nu = nu;
+  c.lane = lane;
+  c.isv = lane == kVecLane;
+  c.qp = qp;
+  c.ng = a.ng;
+  c.nch = (a.ng + kMaxDim - 1) / kMaxDim;
+  c.stride = (size_t)kIpmStage + (size_t)c.nch * kGenChunk;
+  c.ws_qp = a.ws_qp;
+  c.bA = a.A; c.bB = a.B; c.bb = a.b; c.bQ = a.Q; c.bS = a.S; c.bR = a.R; c.bq = a.q; c.br = a.r;
+  c.bx0 = a.x0;
+  c.blbu = a.lbu; c.bubu = a.ubu; c.blbum = a.lbu_mask; c.bubum = a.ubu_mask;
+  c.blbx = a.lbx; c.bubx = a.ubx; c.blbxm = a.lbx_mask; c.bubxm = a.ubx_mask;
+  c.bC = GEN ? a.C : nullptr; c.bD = GEN ? a.D : nullptr;
+  c.blg = a.lg; c.bug = a.ug; c.blgm = a.lg_mask; c.bugm = a.ug_mask;
+  c.bxo = a.x; c.buo = a.u; c.bpi = a.pi; c.bws = a.ws;
+  const real reg = a.reg;
+
+  // ---- general rows (GEN): Gamma / gamma and their images under C, D ----
+  // Gamma / gamma of row `lane` of chunk ch (corrector: + dlam_aff dt_aff - sigma mu)
+  auto g_gamma = [&](int k, int ch, bool corr, real smu, real& G, real& gg) {
+    G = real(0.0);
+    gg = real(0.0);
+    if (lane < kMaxDim) {
+      const real* g = c.gs(k, ch);
+      real el = real(0.0), eu = real(0.0);
+      if (corr) {
+        const BarStep d = load_gstep(g, lane);
+        el = d.dll * d.dtl;
+        eu = d.dlu * d.dtu;
+      }
+      gamma_of(c.side_g(k, ch, lane), load_gbar(g, lane), g[kGenVal + lane], el, eu, smu, G, gg);
+    }
+  };
+  // gradient adds of lane j: radd = (D'gamma)_j, qadd = (C'gamma)_j
+  auto g_grad = [&](int k, bool corr, real smu, real& radd, real& qadd) {
+    radd = real(0.0);
+    qadd = real(0.0);
+    for (int ch = 0; ch < c.nch; ++ch) {
+      real G, gg, bg[12], Cc[12], Dc[12];
+      g_gamma(k, ch, corr, smu, G, gg);
+      gather12(gg, bg);
+      c.g_col(k, ch, col, Cc, Dc);
+      qadd = dot12(Cc, bg, qadd);
+      radd = dot12(Dc, bg, radd);
+    }
+  };
+  // Hessian adds (column-owned): which 0: M1 = R += D'Gamma D;
+  // 1: M1 = S += D'Gamma C, M2 = Q += C'Gamma C;  2: M1 = Q += C'Gamma C
+  auto g_hess = [&](int k, int which, real (&M1)[12], real (&M2)[12]) {
+    for (int ch = 0; ch < c.nch; ++ch) {
+      real G, gg, Gb[12], Cc[12], Dc[12], Y[12];
+      g_gamma(k, ch, false, real(0.0), G, gg);
+      gather12(G, Gb);
+      c.g_col(k, ch, col, Cc, Dc);
+      sfor<0, 12>([&](auto i) {
+        constexpr int I = decltype(i)::value;
+        Y[I] = Gb[I] * (which == 0 ? Dc[I] : Cc[I]);
+      });
+      if (which == 0) {
+        tmul_acc(Dc, Y, M1);
+      } else if (which == 1) {
+        tmul_acc(Dc, Y, M1);
+        tmul_acc(Cc, Y, M2);
+      } else {
+        tmul_acc(Cc, Y, M1);
+      }
+    }
+  };
+
+
+  real* const qs = c.ws();  // per-QP scalar state (kQs*)
+  if constexpr (PH == kPhInit) {
+  // =================== init (var_init_scheme 0, relative form) ===================
+  real ncl = real(0.0);
+  for (int k = 0; k <= N; ++k) {
+    real* stk = c.st(k);
+    real ui = real(0.0), xi = real(0.0);  // initial u_k, x_k (element-owned)
+    // u_k
+    if (k < N) {
+      real v = (a.warm_start && uel) ? c.u()[(size_t)k * nu + li] : real(0.0);
+      const Side s = c.side_u(k, lane);
+      Bar bb{real(0.0), real(0.0), real(1.0), real(1.0)};
+      if (s.ml != real(0.0) || s.mu != real(0.0)) {
+        real tl = v - s.lb, tu = s.ub - v;
+        if (s.ml != real(0.0) && s.mu != real(0.0)) {
+          if (tl < kThr0) {
+            if (tu < kThr0) {
+              v = real(0.5) * (s.lb + s.ub);
+              tl = tu = kThr0;
+            } else {
+              tl = kThr0;
+              v = s.lb + kThr0;
+              tu = s.ub - v;
+            }
+          } else if (tu < kThr0) {
+            tu = kThr0;
+            v = s.ub - kThr0;
+            tl = v - s.lb;
+          }
+        } else if (s.ml != real(0.0)) {
+          if (tl < kThr0) {
+            tl = kThr0;
+            v = s.lb + kThr0;
+          }
+        } else if (tu < kThr0) {
+          tu = kThr0;
+          v = s.ub - kThr0;
+        }
+        bb.tl = s.ml != real(0.0) ? tl : real(1.0);
+        bb.tu = s.mu != real(0.0) ? tu : real(1.0);
+        bb.ll = s.ml != real(0.0) ? a.mu0 / tl : real(0.0);
+        bb.lu = s.mu != real(0.0) ? a.mu0 / tu : real(0.0);
+      }
+      ncl += s.ml + s.mu;
+      if (lane < kMaxDim) store_bar(stk, 0, lane, bb);
+      if (uel) c.u()[(size_t)k * nu + lane] = v;
+      ui = uel ? v : real(0.0);
+    }
+    // x_k
+    {
+      real v;
+      if (k == 0) {
+        v = xel ? c.x0()[li] : real(0.0);
+      } else {
+        v = (a.warm_start && xel) ? c.x()[(size_t)k * nx + li] : real(0.0);
+      }
+      const Side s = c.side_x(k, lane);
+      Bar bb{real(0.0), real(0.0), real(1.0), real(1.0)};
+      if (s.ml != real(0.0) || s.mu != real(0.0)) {
+        real tl = v - s.lb, tu = s.ub - v;
+        if (s.ml != real(0.0) && s.mu != real(0.0)) {
+          if (tl < kThr0) {
+            if (tu < kThr0) {
+              v = real(0.5) * (s.lb + s.ub);
+              tl = tu = kThr0;
+            } else {
+              tl = kThr0;
+              v = s.lb + kThr0;
+              tu = s.ub - v;
+            }
+          } else if (tu < kThr0) {
+            tu = kThr0;
+            v = s.ub - kThr0;
+            tl = v - s.lb;
+          }
+        } else if (s.ml != real(0.0)) {
+          if (tl < kThr0) {
+            tl = kThr0;
+            v = s.lb + kThr0;
+          }
+        } else if (tu < kThr0) {
+          tu = kThr0;
+          v = s.ub - kThr0;
+        }
+        bb.tl = s.ml != real(0.0) ? tl : real(1.0);
+        bb.tu = s.mu != real(0.0) ? tu : real(1.0);
+        bb.ll = s.ml != real(0.0) ? a.mu0 / tl : real(0.0);
+        bb.lu = s.mu != real(0.0) ? a.mu0 / tu : real(0.0);
+      }
+      ncl += s.ml + s.mu;
+      if (lane < kMaxDim) store_bar(stk, 1, lane, bb);
+      if (xel) {
+        c.x()[(size_t)k * nx + lane] = v;
+        c.pi()[(size_t)k * nx + lane] = real(0.0);
+      }
+      xi = xel ? v : real(0.0);
+    }
+    // general rows: t = max(v - lg, thr0), max(ug - v, thr0) at the initial
+    // x_k / u_k (no projection possible), lam = mu0 / t
+    if constexpr (GEN) {
+      real bxi[12], bui[12];
+      gather12(xi, bxi);
+      gather12(ui, bui);
+      for (int ch = 0; ch < c.nch; ++ch) {
+        real Cr[12], Dr[12];
+        c.g_row(k, ch, lane, Cr, Dr);
+        const real v = dot12(Dr, bui, dot12(Cr, bxi, real(0.0)));
+        const Side s = c.side_g(k, ch, lane);
+        Bar bb{real(0.0), real(0.0), real(1.0), real(1.0)};
+        if (s.ml != real(0.0)) {
+          bb.tl = fmax(v - s.lb, kThr0);
+          bb.ll = a.mu0 / bb.tl;
+        }
+        if (s.mu != real(0.0)) {
+          bb.tu = fmax(s.ub - v, kThr0);
+          bb.lu = a.mu0 / bb.tu;
+        }
+        ncl += s.ml + s.mu;
+        if (lane < kMaxDim) {
+          real* g = c.gs(k, ch);
+          store_gbar(g, lane, bb);
+          store_gstep(g, lane, BarStep{0, 0, 0, 0});
+          g[kGenVal + lane] = v;
+        }
+      }
+    }
+    if (lane < kMaxDim) {
+      // zero step: the first RU pass applies nothing
+      stk[kStStep + lane] = real(0.0);
+      stk[kStStep + 12 + lane] = real(0.0);
+      stk[kStStep + 24 + lane] = real(0.0);
+      store_bstep(stk, 0, lane, BarStep{0, 0, 0, 0});
+      store_bstep(stk, 1, lane, BarStep{0, 0, 0, 0});
+    }
+  }
+  const real nc = gsum(lane < kMaxDim ? ncl : real(0.0));
+  if (lane == 0) {
+    qs[kQsAlphaP] = real(0.0);
+    qs[kQsAlphaD] = real(0.0);
+    qs[kQsLastAmin] = real(1.0);
+    qs[kQsSigmaMu] = real(0.0);
+    qs[kQsStatus] = -real(1.0);
+    qs[kQsIter] = real(0.0);
+    qs[kQsNc] = nc;
+  }
+
+    return;
+  }
+  const real nc = qs[kQsNc];
+  const real nc_inv = nc > real(0.0) ? real(1.0) / nc : real(0.0);
+  int status = (int)qs[kQsStatus];
+  const int iter = (int)qs[kQsIter];
+  if constexpr (PH == kPhOut) {
+    const real res_stat = qs[kQsResStat], res_eq = qs[kQsResEq], res_ineq = qs[kQsResIneq];
+    const real res_comp = qs[kQsResComp], obj = qs[kQsObj];
+    if (status < 0) status = 1;  // not reached: the last RB sweep always decides
+    const int par = iter & 1;
+  // =================== outputs ===================
+  // Riccati factors of the last completed iteration (HPIPM's getters); the
+  // exiting sweep's own factorization is used only when no step was taken.
+  const int out_par = iter > 0 ? (par ^ 1) : par;
+  // pi_0 := Q0 x0 + S0'u0 + q0 + A0'(pi_1 + P_1 res_b0): the value of the
+  // stage-0 rebuild (ocp_qp_ipm_solver.cpp:347-373) with p_1 = pi_1 - P_1 x_1.
+  {
+    const real* st0 = c.st(0);
+    const real* st1 = c.st(1) + out_par * kRecSize;
+    real bx0[12], bu0[12];
+    gather12(xel ? c.x()[li] : real(0.0), bx0);
+    gather12(uel ? c.u()[li] : real(0.0), bu0);
+    real P1c[12], brb[12];
+    load_packed_sym(st1 + kRecP, col, P1c);
+    gather12(lane < kMaxDim ? st0[kStRes + 24 + lane] : real(0.0), brb);
+    real t = xel ? c.pi()[(size_t)nx + lane] : real(0.0);
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      t = fmadd(P1c[J], brb[J], t);
+    });
+    if (!xel) t = real(0.0);
+    real bt[12];
+    gather12(t, bt);
+    real Qc[12], Sc[12], Ac[12];
+    c.col(c.Q(), nx, col, xel, Qc);
+    c.col(c.S(), nu, col, xel, Sc);
+    c.col(c.A(), nx, col, xel, Ac);
+    real p0 = c.el(c.q(), nx, li);
+    sfor<0, 12>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      p0 = fmadd(Qc[J], bx0[J], p0);
+      p0 = fmadd(Sc[J], bu0[J], p0);
+      p0 = fmadd(Ac[J], bt[J], p0);
+    });
+    if (xel) c.pi()[lane] = p0;
+  }
+  if (a.P || a.p || a.K || a.k) {
+    // Riccati matrices of the last factorization (HPIPM's get_ric_* getters),
+    // vectors by consistency: p_k = pi_k - P_k x_k, k_k = u_k - K_k x_k.
+    const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu;
+    for (int k = 0; k <= N; ++k) {
+      const real* stk = c.st(k) + out_par * kRecSize;
+      real bxk[12];
+      gather12(xel ? c.x()[(size_t)k * nx + li] : real(0.0), bxk);
+      real Pc[12];
+      load_packed_sym(stk + kRecP, col, Pc);
+      if (a.P && xel)
+        sfor<0, 12>([&](auto i) {
+          constexpr int I = decltype(i)::value;
+          if (I < nx) a.P[((size_t)qp * (N + 1) + k) * nxx + (size_t)lane * nx + I] = Pc[I];
+        });
+      if (a.p) {
+        real px = real(0.0);
+        sfor<0, 12>([&](auto j) {
+          constexpr int J = decltype(j)::value;
+          px = fmadd(Pc[J], bxk[J], px);
+        });
+        if (xel) a.p[((size_t)qp * (N + 1) + k) * nx + lane] = c.pi()[(size_t)k * nx + lane] - px;
+      }
+      if (k < N) {
+        real Kc[12];
+        load12(stk + kRecK + col * 12, Kc);
+        if (a.K && xel)
+          sfor<0, 12>([&](auto i) {
+            constexpr int I = decltype(i)::value;
+            if (I < nu) a.K[((size_t)qp * N + k) * nxu + (size_t)lane * nu + I] = Kc[I];
+          });
+        if (a.k) {
+          real Kr[12];
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            Kr[J] = stk[kRecK + J * 12 + li];
+          });
+          real kx = real(0.0);
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            kx = fmadd(Kr[J], bxk[J], kx);
+          });
+          if (uel) a.k[((size_t)qp * N + k) * nu + lane] = c.u()[(size_t)k * nu + lane] - kx;
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    if (a.status) a.status[qp] = status;
+    if (a.iter) a.iter[qp] = nc > real(0.0) ? iter : 0;
+    if (a.res) {
+      a.res[(size_t)qp * 4 + 0] = res_stat;
+      a.res[(size_t)qp * 4 + 1] = res_eq;
+      a.res[(size_t)qp * 4 + 2] = res_ineq;
+      a.res[(size_t)qp * 4 + 3] = res_comp;
+    }
+    if (a.obj) a.obj[qp] = obj;
+  }
+    return;
+  }
+  if (status >= 0) return;  // this QP has exited
+  const int par = iter & 1;  // record written by this iteration's factorization
+  const real alpha_p = qs[kQsAlphaP], alpha_d = qs[kQsAlphaD], last_amin = qs[kQsLastAmin];
+  if constexpr (PH == kPhRB) {
+    // =========== RB (k = N..0): update + residuals + Gamma/gamma + factorization ===========
+    // One backward sweep per iteration: stage k applies the previous step to its
+    // variables, forms its residuals (x_{k+1}, pi_{k+1} were updated by stage k+1),
+    // and factorizes its barrier-augmented block right away, so the QP data is
+    // streamed once per iteration.  If the exit test after the sweep fires, this
+    // sweep's factorization is simply not used (outputs read the other parity).
+    real mg = real(0.0), mb = real(0.0), md = real(0.0), mm = real(0.0), musum = real(0.0), objl = real(0.0);
+    real xn = real(0.0), pin = real(0.0);  // updated x_{k+1}, pi_{k+1} (element-owned), from stage k+1
+    real P[12];
+    for (int k = N; k >= 0; --k) {
+      real* stk = c.st(k);
+      real* rec = stk + par * kRecSize;
+      // ---- apply the previous step to stage k ----
+      real uk = real(0.0), xk = real(0.0), pik = real(0.0);
+      if (k < N && uel) {
+        uk = c.u()[(size_t)k * nu + lane] + alpha_p * stk[kStStep + lane];
+        c.u()[(size_t)k * nu + lane] = uk;
+      }
+      if (xel) {
+        if (k == 0) {
+          xk = c.x()[li];  // x_0 = x0 (never updated); pi_0 is not an iterate
+        } else {
+          xk = c.x()[(size_t)k * nx + lane] + alpha_p * stk[kStStep + 12 + lane];
+          pik = c.pi()[(size_t)k * nx + lane] + alpha_d * stk[kStStep + 24 + lane];
+          c.x()[(size_t)k * nx + lane] = xk;
+          c.pi()[(size_t)k * nx + lane] = pik;
+        }
+      }
+      Bar bu{0, 0, 1, 1}, bx{0, 0, 1, 1};
+      const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
+      if (lane < kMaxDim) {
+        bu = load_bar(stk, 0, lane);
+        bx = load_bar(stk, 1, lane);
+        const BarStep du = load_bstep(stk, 0, lane), dx = load_bstep(stk, 1, lane);
+        bu.tl += alpha_p * du.dtl;
+        bu.tu += alpha_p * du.dtu;
+        bu.ll += alpha_d * du.dll;
+        bu.lu += alpha_d * du.dlu;
+        bx.tl += alpha_p * dx.dtl;
+        bx.tu += alpha_p * dx.dtu;
+        bx.ll += alpha_d * dx.dll;
+        bx.lu += alpha_d * dx.dlu;
+        store_bar(stk, 0, lane, bu);
+        store_bar(stk, 1, lane, bx);
+      }
+      // ---- residuals of stage k (element-owned) ----
+      real rgx = real(0.0), rgu = real(0.0), rb = real(0.0);
+      {
+        real bxk[12], buk[12], bpn[12];
+        gather12(xk, bxk);
+        gather12(uk, buk);
+        gather12(pin, bpn);
+        {
+          real Qc[12];
+          c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
+          const real qx = dot12(Qc, bxk, real(0.0));
+          const real qk = c.el(c.q() + (size_t)k * nx, nx, li);
+          rgx = qx + qk - pik;
+          if (k > 0) objl += xk * (real(0.5) * qx + qk);
+        }
+        if (k < N) {
+          // one block at a time (fenced) so that at most two 12-arrays are in flight
+          real ru, sx_, stu, btp, atp;
+          {
+            real M[12];
+            c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, M);
+            ru = dot12(M, buk, real(0.0));
+          }
+          SRBD_PHASE_FENCE();
+          {
+            real M[12];
+            c.row(c.S() + (size_t)k * c.nxu(), nu, nx, li, uel, M);
+            sx_ = dot12(M, bxk, real(0.0));
+          }
+          SRBD_PHASE_FENCE();
+          {
+            real M[12];
+            c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, M);
+            stu = dot12(M, buk, real(0.0));
+          }
+          SRBD_PHASE_FENCE();
+          {
+            real M[12];
+            c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, M);
+            btp = dot12(M, bpn, real(0.0));
+          }
+          SRBD_PHASE_FENCE();
+          {
+            real M[12];
+            c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, M);
+            atp = dot12(M, bpn, real(0.0));
+          }
+          SRBD_PHASE_FENCE();
+          const real rk = c.el(c.r() + (size_t)k * nu, nu, li);
+          rgu = ru + sx_ + rk + btp;
+          rgx += stu + atp;
+          objl += uk * (real(0.5) * ru + rk + sx_);
+          // res_b = A x + B u + b - x_{k+1} (row-owned A, B)
+          real ax;
+          {
+            real M[12];
+            c.row(c.A() + (size_t)k * c.nxx(), nx, nx, li, xel, M);
+            ax = dot12(M, bxk, real(0.0));
+          }
+          SRBD_PHASE_FENCE();
+          {
+            real M[12];
+            c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, M);
+            ax = dot12(M, buk, ax);
+          }
+          SRBD_PHASE_FENCE();
+          rb = ax + c.el(c.b() + (size_t)k * nx, nx, li) - xn;
+        }
+        if constexpr (GEN) {
+          // general rows: apply the step, residuals, res_g += C'(lam_u - lam_l), D'(..)
+          for (int ch = 0; ch < c.nch; ++ch) {
+            real* g = c.gs(k, ch);
+            const Side sg = c.side_g(k, ch, lane);
+            Bar bg{0, 0, 1, 1};
+            if (lane < kMaxDim) {
+              bg = load_gbar(g, lane);
+              const BarStep d = load_gstep(g, lane);
+              bg.tl += alpha_p * d.dtl;
+              bg.tu += alpha_p * d.dtu;
+              bg.ll += alpha_d * d.dll;
+              bg.lu += alpha_d * d.dlu;
+              store_gbar(g, lane, bg);
+            }
+            real Cr[12], Dr[12];
+            c.g_row(k, ch, lane, Cr, Dr);
+            const real v = dot12(Dr, buk, dot12(Cr, bxk, real(0.0)));
+            if (lane < kMaxDim) g[kGenVal + lane] = v;
+            if (sg.ml != real(0.0)) {
+              const real rd = v - sg.lb - bg.tl, rm = bg.ll * bg.tl;
+              md = fmax(md, nabs(rd));
+              mm = fmax(mm, nabs(rm));
+              musum += rm;
+            }
+            if (sg.mu != real(0.0)) {
+              const real rd = sg.ub - v - bg.tu, rm = bg.lu * bg.tu;
+              md = fmax(md, nabs(rd));
+              mm = fmax(mm, nabs(rm));
+              musum += rm;
+            }
+            real bdl[12], Cc[12], Dc[12];
+            gather12(lane < kMaxDim ? bg.lu - bg.ll : real(0.0), bdl);
+            c.g_col(k, ch, col, Cc, Dc);
+            rgx = dot12(Cc, bdl, rgx);
+            rgu = dot12(Dc, bdl, rgu);
+          }
+        }
+      }
+      // box terms
+      if (su.ml != real(0.0)) {
+        rgu -= bu.ll;
+        const real rd = uk - su.lb - bu.tl, rm = bu.ll * bu.tl;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (su.mu != real(0.0)) {
+        rgu += bu.lu;
+        const real rd = su.ub - uk - bu.tu, rm = bu.lu * bu.tu;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (sx.ml != real(0.0)) {
+        rgx -= bx.ll;
+        const real rd = xk - sx.lb - bx.tl, rm = bx.ll * bx.tl;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (sx.mu != real(0.0)) {
+        rgx += bx.lu;
+        const real rd = sx.ub - xk - bx.tu, rm = bx.lu * bx.tu;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (!xel) rgx = real(0.0);
+      if (!uel) rgu = real(0.0);
+      if (k < N) {
+        mg = fmax(mg, nabs(rgu));
+        mb = fmax(mb, nabs(xel ? rb : real(0.0)));
+      }
+      if (k > 0) mg = fmax(mg, nabs(rgx));
+      if (!xel) rb = real(0.0);
+      if (lane < kMaxDim) {
+        stk[kStRes + lane] = rgu;
+        stk[kStRes + 12 + lane] = rgx;
+        stk[kStRes + 24 + lane] = rb;
+      }
+      SRBD_PHASE_FENCE();
+      // ---- predictor Gamma / gamma, factorization of stage k ----
+      real Gu = real(0.0), gu = real(0.0), Gx = real(0.0), gx = real(0.0);
+      if (lane < kMaxDim) {
+        gamma_of(su, bu, uk, real(0.0), real(0.0), real(0.0), Gu, gu);
+        gamma_of(sx, bx, xk, real(0.0), real(0.0), real(0.0), Gx, gx);
+      }
+      real rt = lane < kMaxDim ? rgu + gu : real(0.0);
+      real qt = lane < kMaxDim ? rgx + gx : real(0.0);
+      if constexpr (GEN) {
+        real ra, qa;
+        g_grad(k, false, real(0.0), ra, qa);
+        if (lane < kMaxDim) {
+          rt += ra;
+          qt += qa;
+        }
+      }
+      if (k == N) {
+        // terminal stage: P_N = Q_N + diag(Gamma_x) (+ C'Gamma C), p_N = q~_N
+        real qv[12];
+        gather12(qt, qv);
+        c.col(c.Q() + (size_t)N * c.nxx(), nx, col, xel, P);
+        if constexpr (GEN) g_hess(N, 2, P, P);
+        sfor<0, 12>([&](auto i) {
+          constexpr int I = decltype(i)::value;
+          if (lane == I) P[I] += Gx;
+          if (c.isv) P[I] = qv[I];
+        });
+        if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
+        if (c.isv) store12(rec + kRecPv, P);
+      } else {
+        real bv[12];
+        gather12(rb, bv);
+        real A_[12], B_[12];
+        c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, A_);
+        c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, B_);
+        sfor<0, 12>([&](auto i) {
+          constexpr int I = decltype(i)::value;
+          if (c.isv) {
+            A_[I] = bv[I];
+            B_[I] = real(0.0);
+          }
+        });
+        auto loadR = [&](real (&Rc)[12]) {
+          c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, Rc);
+          if constexpr (GEN) g_hess(k, 0, Rc, Rc);
+          sfor<0, 12>([&](auto i) {
+            constexpr int I = decltype(i)::value;
+            if (lane == I) Rc[I] += (I < nu) ? Gu : real(1.0);  // padded inputs: R = 1
+            if (c.isv) Rc[I] = real(0.0);
+          });
+        };
+        auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
+          c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, Sc);
+          c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
+          if constexpr (GEN) g_hess(k, 1, Sc, Qc);
+          sfor<0, 12>([&](auto i) {
+            constexpr int I = decltype(i)::value;
+            const real rI = bc<I>(rt), qI = bc<I>(qt);
+            if (lane == I) Qc[I] += Gx;
+            if (c.isv) {
+              Sc[I] = rI;
+              Qc[I] = qI;
+            }
+          });
+        };
+        StageFactor<real> f;
+        riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
+        if (lane < kMaxDim) {
+          store_packed_col(rec + kRecL, lane, f.Lc);
+          store12(rec + kRecK + lane * 12, f.Kc);
+          store12(rec + kRecAcl + lane * 12, A_);
+          store_packed_col(rec + kRecP, lane, f.F);
+          rec[kRecRs + lane] = f.rs;
+        }
+        if (c.isv) {
+          store12(rec + kRecKv, f.Kc);
+          store12(rec + kRecBcl, A_);
+          store12(rec + kRecPv, f.F);
+        }
+        sfor<0, 12>([&](auto i) {
+          constexpr int I = decltype(i)::value;
+          P[I] = f.F[I];
+        });
+      }
+      xn = xk;
+      pin = pik;
+    }
+    const real res_stat = gmax(lane < kMaxDim ? mg : real(0.0));
+    const real res_eq = gmax(lane < kMaxDim ? mb : real(0.0));
+    const real res_ineq = gmax(lane < kMaxDim ? md : real(0.0));
+    const real res_comp = gmax(lane < kMaxDim ? mm : real(0.0));
+    const real obj = gsum(lane < kMaxDim ? objl : real(0.0));
+    const real musum_all = gsum(lane < kMaxDim ? musum : real(0.0));
+    const real mu = musum_all * nc_inv;
+    real* const stat_row = a.stat && lane == 0
+                           ? a.stat + ((size_t)qp * (a.iter_max + 2) + iter) * kStatCols
+                           : nullptr;
+    if (stat_row) {
+      stat_row[5] = mu;
+      stat_row[6] = res_stat;
+      stat_row[7] = res_eq;
+      stat_row[8] = res_ineq;
+      stat_row[9] = res_comp;
+      stat_row[10] = obj;
+    }
+    // ---- exit test (HPIPM order: converged / iter_max / min step / NaN) ----
+    {
+      const bool isnan_ = !(res_stat == res_stat) || !(res_eq == res_eq) ||
+                          !(res_ineq == res_ineq) || !(res_comp == res_comp) || !(mu == mu) ||
+                          res_stat == real(__builtin_inf()) || res_eq == real(__builtin_inf());
+      if (isnan_) {
+        status = 3;
+      } else if (res_stat <= a.tol_stat && res_eq <= a.tol_eq && res_ineq <= a.tol_ineq &&
+                 res_comp <= a.tol_comp) {
+        status = 0;
+      } else if (iter >= a.iter_max) {
+        status = 1;
+      } else if (iter > 0 && last_amin < a.alpha_min) {
+        status = 2;
+      }
+    }
+    if (lane == 0) {
+      qs[kQsMu] = mu;
+      qs[kQsMuSum] = musum_all;
+      qs[kQsResStat] = res_stat;
+      qs[kQsResEq] = res_eq;
+      qs[kQsResIneq] = res_ineq;
+      qs[kQsResComp] = res_comp;
+      qs[kQsObj] = obj;
+      qs[kQsStatus] = (real)status;
+    }
+
+    return;
+  }
+  const real mu = qs[kQsMu], musum_all = qs[kQsMuSum];
+  real sigma_mu = qs[kQsSigmaMu];
+  if constexpr (PH == kPhB2) {
+        // ---- B2: corrector vectors (element-owned recursion) ----
+        real pnext = real(0.0);  // p_{k+1}, element-owned
+        {
+          real* stN = c.st(N);
+          const Side sx = c.side_x(N, lane);
+          const real xv = xel ? c.x()[(size_t)N * nx + lane] : real(0.0);
+          real G = real(0.0), g = real(0.0);
+          if (lane < kMaxDim) {
+            const BarStep dx = load_bstep(stN, 1, lane);
+            gamma_of(sx, load_bar(stN, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, G, g);
+          }
+          pnext = lane < kMaxDim && xel ? stN[kStRes + 12 + lane] + g : real(0.0);
+          if constexpr (GEN) {
+            real ra, qa;
+            g_grad(N, true, sigma_mu, ra, qa);
+            if (lane < kMaxDim && xel) pnext += qa;
+          }
+          if (lane < kMaxDim) stN[par * kRecSize + kRecPv + lane] = pnext;
+        }
+        for (int k = N - 1; k >= 0; --k) {
+          real* stk = c.st(k);
+          real* rec = stk + par * kRecSize;
+          const real* recn = c.st(k + 1) + par * kRecSize;
+          const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
+          const real uv = uel ? c.u()[(size_t)k * nu + lane] : real(0.0);
+          const real xv = xel ? c.x()[(size_t)k * nx + lane] : real(0.0);
+          real Gu = real(0.0), gu = real(0.0), Gx = real(0.0), gx = real(0.0);
+          if (lane < kMaxDim) {
+            const BarStep du = load_bstep(stk, 0, lane), dx = load_bstep(stk, 1, lane);
+            gamma_of(su, load_bar(stk, 0, lane), uv, du.dll * du.dtl, du.dlu * du.dtu, sigma_mu, Gu, gu);
+            gamma_of(sx, load_bar(stk, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, Gx, gx);
+          }
+          real rt = lane < kMaxDim && uel ? stk[kStRes + lane] + gu : real(0.0);
+          real qt = lane < kMaxDim && xel ? stk[kStRes + 12 + lane] + gx : real(0.0);
+          if constexpr (GEN) {
+            real ra, qa;
+            g_grad(k, true, sigma_mu, ra, qa);
+            if (lane < kMaxDim && uel) rt += ra;
+            if (lane < kMaxDim && xel) qt += qa;
+          }
+          const real bt = lane < kMaxDim ? stk[kStRes + 24 + lane] : real(0.0);
+          // w = P_{k+1} b~ + p_{k+1}
+          real Pc[12], bb[12];
+          load_packed_sym(recn + kRecP, col, Pc);
+          gather12(bt, bb);
+          real w = pnext;
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            w = fmadd(Pc[J], bb[J], w);
+          });
+          // g = r~ + B'w ; f = q~ + A'w
+          real Bc[12], Ac[12], bw[12];
+          c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, Bc);
+          c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, Ac);
+          gather12(w, bw);
+          real g = rt, f = qt;
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            g = fmadd(Bc[J], bw[J], g);
+            f = fmadd(Ac[J], bw[J], f);
+          });
+          if (lane >= kMaxDim) g = real(0.0);
+          // p = f + K'g  (K column-owned: lane j holds K[:, j])
+          real Kc[12], bg[12];
+          load12(rec + kRecK + col * 12, Kc);
+          gather12(g, bg);
+          real pv = f;
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            pv = fmadd(Kc[J], bg[J], pv);
+          });
+          // y = L^-1 g (row-owned L), then z = L^-T y (column-owned L), k = -z
+          real Lr[12], Lc[12];
+          load_packed_lrow(rec + kRecL, li, Lr);
+          load_packed_lcol(rec + kRecL, col, Lc);
+          const real rs = rec[kRecRs + li];
+          real y = g;
+          sfor<0, 12>([&](auto kk) {
+            constexpr int K = decltype(kk)::value;
+            const real yk = bc<K>(y * rs);
+            if (lane == K) y = yk;
+            if (lane > K) y = fmadd(-Lr[K], yk, y);
+          });
+          sfor_down<0, 12>([&](auto kk) {
+            constexpr int K = decltype(kk)::value;
+            const real zk = bc<K>(y * rs);
+            if (lane == K) y = zk;
+            if (lane < K) y = fmadd(-Lc[K], zk, y);
+          });
+          const real kv = lane < kMaxDim && uel ? -y : real(0.0);
+          // bcl = b~ + B k (row-owned B)
+          real Br[12], bk[12];
+          c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
+          gather12(kv, bk);
+          real bcl = bt;
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            bcl = fmadd(Br[J], bk[J], bcl);
+          });
+          if (lane < kMaxDim) {
+            rec[kRecKv + lane] = kv;
+            rec[kRecBcl + lane] = xel ? bcl : real(0.0);
+            rec[kRecPv + lane] = xel ? pv : real(0.0);
+          }
+          pnext = xel ? pv : real(0.0);
+        }
+    return;
+  }
+  if constexpr (PH == kPhF1 || PH == kPhF2) {
+    constexpr bool corr = PH == kPhF2;
+    real ap = real(1e30), ad = real(1e30);
+    real s1 = real(0.0), s2 = real(0.0);  // predictor sums lam dt + t dlam, dlam dt (element-owned)
+      // ---- forward step (F1 predictor / F2 corrector), row-owned ----
+      ap = real(1e30);
+      ad = real(1e30);
+      real dxk = real(0.0);  // dx_0 = 0 (x0 fixed)
+      for (int k = 0; k <= N; ++k) {
+        real* stk = c.st(k);
+        const real* rec = stk + par * kRecSize;
+        real bdx[12];
+        gather12(dxk, bdx);
+        real Pc[12];
+        load_packed_sym(rec + kRecP, col, Pc);
+        real dpi = rec[kRecPv + li];
+        sfor<0, 12>([&](auto j) {
+          constexpr int J = decltype(j)::value;
+          dpi = fmadd(Pc[J], bdx[J], dpi);
+        });
+        real du = real(0.0), dxn = real(0.0);
+        if (k < N) {
+          real Kr[12], Ar[12];
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            Kr[J] = rec[kRecK + J * 12 + li];
+            Ar[J] = rec[kRecAcl + J * 12 + li];
+          });
+          du = rec[kRecKv + li];
+          dxn = rec[kRecBcl + li];
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            du = fmadd(Kr[J], bdx[J], du);
+            dxn = fmadd(Ar[J], bdx[J], dxn);
+          });
+        }
+        if (!uel || k == N) du = real(0.0);
+        if (!xel) {
+          dxn = real(0.0);
+          dpi = real(0.0);
+        }
+        if constexpr (GEN) {
+          // general rows: dv = C dx + D du, dt / dlam, step ratios
+          real bdu[12];
+          gather12(du, bdu);
+          for (int ch = 0; ch < c.nch; ++ch) {
+            real* g = c.gs(k, ch);
+            real Cr[12], Dr[12];
+            c.g_row(k, ch, lane, Cr, Dr);
+            const real dv = dot12(Dr, bdu, dot12(Cr, bdx, real(0.0)));
+            if (lane < kMaxDim) {
+              const Side sg = c.side_g(k, ch, lane);
+              const Bar bg = load_gbar(g, lane);
+              real el = real(0.0), eu = real(0.0), sm = real(0.0);
+              if (corr) {
+                const BarStep pd = load_gstep(g, lane);
+                el = pd.dll * pd.dtl;
+                eu = pd.dlu * pd.dtu;
+                sm = sigma_mu;
+              }
+              const BarStep d = bar_step(sg, bg, g[kGenVal + lane], dv, el, eu, sm);
+              ratio(sg, bg, d, ap, ad);
+              if (!corr) aff_sums(sg, bg, d, s1, s2);
+              store_gstep(g, lane, d);
+            }
+          }
+        }
+        if (lane < kMaxDim) {
+          const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
+          const Bar bu = load_bar(stk, 0, lane), bx = load_bar(stk, 1, lane);
+          const real uv = (uel && k < N) ? c.u()[(size_t)k * nu + lane] : real(0.0);
+          const real xv = xel ? c.x()[(size_t)k * nx + lane] : real(0.0);
+          real eul = real(0.0), euu = real(0.0), exl = real(0.0), exu = real(0.0), smu = real(0.0);
+          if (corr) {
+            const BarStep pu = load_bstep(stk, 0, lane), px = load_bstep(stk, 1, lane);
+            eul = pu.dll * pu.dtl;
+            euu = pu.dlu * pu.dtu;
+            exl = px.dll * px.dtl;
+            exu = px.dlu * px.dtu;
+            smu = sigma_mu;
+          }
+          const BarStep nu_ = bar_step(su, bu, uv, du, eul, euu, smu);
+          const BarStep nx_ = bar_step(sx, bx, xv, dxk, exl, exu, smu);
+          ratio(su, bu, nu_, ap, ad);
+          ratio(sx, bx, nx_, ap, ad);
+          if (!corr) {
+            aff_sums(su, bu, nu_, s1, s2);
+            aff_sums(sx, bx, nx_, s1, s2);
+          }
+          store_bstep(stk, 0, lane, nu_);
+          store_bstep(stk, 1, lane, nx_);
+          stk[kStStep + lane] = du;
+          stk[kStStep + 12 + lane] = dxk;
+          stk[kStStep + 24 + lane] = k > 0 ? dpi : real(0.0);
+        }
+        dxk = dxn;
+      }
+    real* const next = a.stat && lane == 0
+                             ? a.stat + ((size_t)qp * (a.iter_max + 2) + iter + 1) * kStatCols
+                             : nullptr;  // HPIPM stores step kk in row kk+1
+    if (!corr) {
+      // alpha_aff, mu_aff, sigma: sum (lam + a dlam)(t + a dt) = S0 + a S1 + a^2 S2
+      const real aa = fmin(real(1.0), fmin(gmin(ap), gmin(ad)));
+      const real S1 = gsum(lane < kMaxDim ? s1 : real(0.0)), S2 = gsum(lane < kMaxDim ? s2 : real(0.0));
+      const real mu_aff = (musum_all + aa * (S1 + aa * S2)) * nc_inv;
+      real sg = mu > real(0.0) ? mu_aff / mu : real(0.0);
+      sg = sg * sg * sg;
+      if (sg > real(1.0)) sg = real(1.0);
+      if (lane == 0) qs[kQsSigmaMu] = sg * mu;
+      if (next && a.pred_corr) {
+        next[0] = aa;
+        next[1] = mu_aff;
+        next[2] = sg;
+      }
+    }
+    if (corr || !a.pred_corr) {
+      // ---- step length of the iteration ----
+      ap = gmin(lane < kMaxDim ? ap : real(1e30));
+      ad = gmin(lane < kMaxDim ? ad : real(1e30));
+      if (!a.split_step) {
+        ap = fmin(ap, ad);
+        ad = ap;
+      }
+      const real alpha_p_new = fmin(real(1.0), kStepTau * ap);
+      const real alpha_d_new = fmin(real(1.0), kStepTau * ad);
+      if (lane == 0) {
+        qs[kQsAlphaP] = alpha_p_new;
+        qs[kQsAlphaD] = alpha_d_new;
+        qs[kQsLastAmin] = fmin(alpha_p_new, alpha_d_new);
+        qs[kQsIter] = (real)(iter + 1);
+      }
+      if (next) {
+        next[3] = alpha_p_new;
+        next[4] = alpha_d_new;
+      }
+    }
+  }
+}
+
+
+template <bool FULL, bool GEN>
+static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream) {
+  const int threads = 256;
+  const long long lanes = (long long)a.batch * kGroup;
+  const dim3 grid((unsigned)((lanes + threads - 1) / threads)), block(threads);
+  // Host-driven iteration: each sweep is its own launch, so every kernel gets
+  // the registers (and occupancy) of its own phase; QPs that have exited return
+  // at the top of every later launch.  iter_max + 1 factorization sweeps at
+  // most: the last one always decides (converged or MaxIterReached).
+  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhInit>), grid, block, 0, stream, a);
+  for (int it = 0;; ++it) {
+    hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB>), grid, block, 0, stream, a);
+    if (it >= a.iter_max) break;
+    hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF1>), grid, block, 0, stream, a);
+    if (a.pred_corr) {
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhB2>), grid, block, 0, stream, a);
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF2>), grid, block, 0, stream, a);
+    }
+  }
+  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut>), grid, block, 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {
+  if (a.batch <= 0) return hipSuccess;
+  const bool full = a.nx == 12 && a.nu == 12;
+  if (a.ng > 0) return full ? launch_phases<true, true>(a, stream) : launch_phases<false, true>(a, stream);
+  return full ? launch_phases<true, false>(a, stream) : launch_phases<false, false>(a, stream);
+}
+
+}  // namespace SRBD_NS
+}  // namespace srbd

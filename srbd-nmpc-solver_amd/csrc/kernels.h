@@ -20,26 +20,30 @@ constexpr int kWsbcl = 378;  // bcl [12]
 constexpr int kWsp = 390;    // p   [12]
 constexpr int kWsStage = 402;  // doubles per stage record (16-byte multiple)
 
-struct ProblemArgs {
+// Arguments of every launch; T = double (srbd_qp_solve_f64) or float
+// (srbd_qp_solve_f32).  Workspace offsets below count elements of T.
+template <typename T>
+struct ProblemArgsT {
   int batch, N, nx, nu, ng;
   // QP data (device)
-  const double *A, *B, *b, *Q, *S, *R, *q, *r, *x0;
-  const double *lbu, *ubu, *lbu_mask, *ubu_mask;
-  const double *lbx, *ubx, *lbx_mask, *ubx_mask;
-  const double *C, *D, *lg, *ug, *lg_mask, *ug_mask;
+  const T *A, *B, *b, *Q, *S, *R, *q, *r, *x0;
+  const T *lbu, *ubu, *lbu_mask, *ubu_mask;
+  const T *lbx, *ubx, *lbx_mask, *ubx_mask;
+  const T *C, *D, *lg, *ug, *lg_mask, *ug_mask;
   // solution (device)
-  double *x, *u, *pi, *P, *p, *K, *k;
+  T *x, *u, *pi, *P, *p, *K, *k;
   int *status, *iter;
-  double *res, *obj;
-  double* stat;  // [batch][iter_max+2][kStatCols] or null
+  T *res, *obj;
+  T* stat;  // [batch][iter_max+2][kStatCols] or null
   // workspace
-  double* ws;
-  size_t ws_qp;  // doubles per QP
-  double reg;
+  T* ws;
+  size_t ws_qp;  // elements per QP
+  T reg;
   // IPM settings (hpipm-cpp OcpQpIpmSolverSettings semantics)
   int iter_max, pred_corr, split_step, warm_start;
-  double alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp;
+  T alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp;
 };
+using ProblemArgs = ProblemArgsT<double>;
 
 constexpr int kStatCols = 18;  // HPIPM ws->stat row width
 
@@ -67,12 +71,14 @@ static_assert(kIpmStage % 2 == 0, "16-byte aligned stages");
 // C x + D u [12], 4 pad
 constexpr int kGenChunk = 112;
 
-size_t ws_doubles_ipm(int N, int ng);
-hipError_t launch_ipm_box(const ProblemArgs& a, hipStream_t stream);
+size_t ws_doubles_ipm(int N, int ng);  // elements per QP (either precision)
+template <typename T>
+hipError_t launch_ipm_box(const ProblemArgsT<T>& a, hipStream_t stream);
 
 // Workspace doubles per QP needed by the unconstrained solve.
 size_t ws_doubles_unconstr(int N);
 
-hipError_t launch_riccati_unconstr(const ProblemArgs& a, hipStream_t stream);
+template <typename T>
+hipError_t launch_riccati_unconstr(const ProblemArgsT<T>& a, hipStream_t stream);
 
 }  // namespace srbd

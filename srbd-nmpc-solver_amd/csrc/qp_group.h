@@ -138,6 +138,49 @@ __device__ __forceinline__ void fma_bcast_lanes(double (&C)[12], double x, doubl
       : "v"(x), "v"(y));
 }
 
+// fp32 twins (v_fmac_f32_dpp): same shapes, same hazard rule
+template <int SRC>
+__device__ __forceinline__ void fma_bcast_src(float (&C)[12], const float (&X)[12], float y) {
+  static_assert(SRC >= 0 && SRC < kGroup, "row_newbcast source lane");
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f32_dpp %0, %12, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %13, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %2, %14, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %3, %15, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %4, %16, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %5, %17, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %6, %18, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %7, %19, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %8, %20, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %9, %21, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %10, %22, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %11, %23, %24 row_newbcast:%25 row_mask:0xf bank_mask:0xf"
+      : "+v"(C[0]), "+v"(C[1]), "+v"(C[2]), "+v"(C[3]), "+v"(C[4]), "+v"(C[5]), "+v"(C[6]),
+        "+v"(C[7]), "+v"(C[8]), "+v"(C[9]), "+v"(C[10]), "+v"(C[11])
+      : "v"(X[0]), "v"(X[1]), "v"(X[2]), "v"(X[3]), "v"(X[4]), "v"(X[5]), "v"(X[6]), "v"(X[7]),
+        "v"(X[8]), "v"(X[9]), "v"(X[10]), "v"(X[11]), "v"(y), "i"(SRC));
+}
+__device__ __forceinline__ void fma_bcast_lanes(float (&C)[12], float x, float y) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f32_dpp %0, %12, %13 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %12, %13 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %2, %12, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %3, %12, %13 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %4, %12, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %5, %12, %13 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %6, %12, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %7, %12, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %8, %12, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %9, %12, %13 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %10, %12, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %11, %12, %13 row_newbcast:11 row_mask:0xf bank_mask:0xf"
+      : "+v"(C[0]), "+v"(C[1]), "+v"(C[2]), "+v"(C[3]), "+v"(C[4]), "+v"(C[5]), "+v"(C[6]),
+        "+v"(C[7]), "+v"(C[8]), "+v"(C[9]), "+v"(C[10]), "+v"(C[11])
+      : "v"(x), "v"(y));
+}
+
 template <typename T>
 __device__ __forceinline__ T fmadd(T a, T b, T c) {
   return __builtin_fma(a, b, c);
@@ -165,6 +208,24 @@ __device__ __forceinline__ void store12(double* __restrict__ p, const double (&v
   });
 }
 
+// fp32: 12 contiguous floats as 8-byte pairs (record offsets are even)
+__device__ __forceinline__ void load12(const float* __restrict__ p, float (&v)[12]) {
+  const float2* p2 = reinterpret_cast<const float2*>(p);
+  sfor<0, 6>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    float2 t = p2[I];
+    v[2 * I] = t.x;
+    v[2 * I + 1] = t.y;
+  });
+}
+__device__ __forceinline__ void store12(float* __restrict__ p, const float (&v)[12]) {
+  float2* p2 = reinterpret_cast<float2*>(p);
+  sfor<0, 6>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    p2[I] = make_float2(v[2 * I], v[2 * I + 1]);
+  });
+}
+
 // Generic predicated column load: v[i] = (col_ok && i < rows) ? p[i] : 0.
 template <typename T>
 __device__ __forceinline__ void load_col_pad(const T* __restrict__ p, int rows, bool col_ok,
@@ -183,7 +244,8 @@ __device__ __forceinline__ void load_col_pad(const T* __restrict__ p, int rows, 
 __host__ __device__ constexpr int packed_col(int j) { return j * 12 - j * (j - 1) / 2; }
 
 // lane j < 12 stores its column v[i] = M[i][j], rows i >= j only
-__device__ __forceinline__ void store_packed_col(double* pk, int lane, const double (&v)[12]) {
+template <typename T>
+__device__ __forceinline__ void store_packed_col(T* pk, int lane, const T (&v)[12]) {
   const int cj = packed_col(lane) - lane;
   sfor<0, 12>([&](auto i) {
     constexpr int I = decltype(i)::value;
@@ -191,7 +253,8 @@ __device__ __forceinline__ void store_packed_col(double* pk, int lane, const dou
   });
 }
 // row r (= column r) of a symmetric matrix stored as its packed lower triangle
-__device__ __forceinline__ void load_packed_sym(const double* pk, int r, double (&v)[12]) {
+template <typename T>
+__device__ __forceinline__ void load_packed_sym(const T* pk, int r, T (&v)[12]) {
   const int cr = packed_col(r) - r;
   sfor<0, 12>([&](auto j) {
     constexpr int J = decltype(j)::value;
@@ -199,18 +262,20 @@ __device__ __forceinline__ void load_packed_sym(const double* pk, int r, double 
   });
 }
 // strictly-lower row r of a packed lower-triangular L: v[j] = L[r][j] (j < r), else 0
-__device__ __forceinline__ void load_packed_lrow(const double* pk, int r, double (&v)[12]) {
+template <typename T>
+__device__ __forceinline__ void load_packed_lrow(const T* pk, int r, T (&v)[12]) {
   sfor<0, 12>([&](auto j) {
     constexpr int J = decltype(j)::value;
-    v[J] = J < r ? pk[packed_col(J) + r - J] : 0.0;
+    v[J] = J < r ? pk[packed_col(J) + r - J] : T(0);
   });
 }
 // strictly-lower column c of a packed lower-triangular L: v[i] = L[i][c] (i > c), else 0
-__device__ __forceinline__ void load_packed_lcol(const double* pk, int c, double (&v)[12]) {
+template <typename T>
+__device__ __forceinline__ void load_packed_lcol(const T* pk, int c, T (&v)[12]) {
   const int cc = packed_col(c) - c;
   sfor<0, 12>([&](auto i) {
     constexpr int I = decltype(i)::value;
-    v[I] = I > c ? pk[cc + I] : 0.0;
+    v[I] = I > c ? pk[cc + I] : T(0);
   });
 }
 

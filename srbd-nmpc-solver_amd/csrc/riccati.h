@@ -42,7 +42,7 @@ namespace srbd {
 // C[:,l] = P M[:,l] (+ init): P symmetric & column-owned, M column-owned.
 template <typename T>
 __device__ __forceinline__ void sym_mul_col(const T (&P)[12], const T (&M)[12], T (&C)[12]) {
-  if constexpr (std::is_same_v<T, double> && SRBD_FUSED_DPP) {
+  if constexpr ((std::is_same_v<T, double> || std::is_same_v<T, float>) && SRBD_FUSED_DPP) {
     sfor<0, 12>([&](auto kk) {
       constexpr int K = decltype(kk)::value;
       fma_bcast_src<K>(C, P, M[K]);
@@ -61,7 +61,7 @@ __device__ __forceinline__ void sym_mul_col(const T (&P)[12], const T (&M)[12], 
 // C[i][l] += X[:,i]' Y[:,l] for i < 12 (X, Y column-owned)
 template <typename T>
 __device__ __forceinline__ void tmul_acc(const T (&X)[12], const T (&Y)[12], T (&C)[12]) {
-  if constexpr (std::is_same_v<T, double> && SRBD_FUSED_DPP) {
+  if constexpr ((std::is_same_v<T, double> || std::is_same_v<T, float>) && SRBD_FUSED_DPP) {
     sfor<0, 12>([&](auto kk) {
       constexpr int K = decltype(kk)::value;
       fma_bcast_lanes(C, X[K], Y[K]);

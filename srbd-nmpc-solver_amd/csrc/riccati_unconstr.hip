@@ -24,243 +24,28 @@
 #define SRBD_WS_STAGE_MAJOR 1
 #endif
 
+#define SRBD_REAL double
+#define SRBD_NS ric_f64
+#include "riccati_unconstr_impl.h"
+#undef SRBD_REAL
+#undef SRBD_NS
+#define SRBD_REAL float
+#define SRBD_NS ric_f32
+#include "riccati_unconstr_impl.h"
+#undef SRBD_REAL
+#undef SRBD_NS
+
 namespace srbd {
-
-namespace {
-
-// out[i] = v[i] for i < n (static register indices, predicated stores)
-__device__ __forceinline__ void store_n(double* out, int n, const double (&v)[12]) {
-  sfor<0, 12>([&](auto i) {
-    constexpr int I = decltype(i)::value;
-    if (I < n) out[I] = v[I];
-  });
-}
-
-template <bool FULL>
-struct StageLoader {
-  int nx, nu;
-  // column `col` of an (rows x ncols) column-major block, zero-padded
-  __device__ __forceinline__ void col(const double* blk, int rows, int ld, int c, bool ok,
-                                      double (&v)[12]) const {
-    if constexpr (FULL) {
-      load12(blk + c * 12, v);
-    } else {
-      load_col_pad(blk + (size_t)c * ld, rows, ok, v);
-    }
-  }
-};
-
-template <bool FULL>
-__global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgs a) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int qp = gid >> 4;
-  const int lane = threadIdx.x & (kGroup - 1);
-  if (qp >= a.batch) return;
-  const int N = a.N;
-  const int nx = FULL ? 12 : a.nx;
-  const int nu = FULL ? 12 : a.nu;
-  const bool isv = lane == kVecLane;
-  const int col = lane < kMaxDim ? lane : kMaxDim - 1;
-  const double reg = a.reg;
-
-  const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu, nuu = (size_t)nu * nu;
-#ifdef SRBD_DIAG_SHARED_INPUT  // diagnostic build only: every QP reads QP (qp & 63)'s data
-  const int qin = qp & 63;
-#else
-  const int qin = qp;
-#endif
-  const double* Aq = a.A + (size_t)qin * N * nxx;
-  const double* Bq = a.B + (size_t)qin * N * nxu;
-  const double* bq = a.b + (size_t)qin * N * nx;
-  const double* Qq = a.Q + (size_t)qin * (N + 1) * nxx;
-  const double* Sq = a.S + (size_t)qin * N * nxu;
-  const double* Rq = a.R + (size_t)qin * N * nuu;
-  const double* qq = a.q + (size_t)qin * (N + 1) * nx;
-  const double* rq = a.r + (size_t)qin * N * nu;
-  // forward records, stage-major: stage k of QP q at ws[(k * batch + q) * kWsStage], so the
-  // four QPs of a wavefront write / read one contiguous 15 KB block per stage
-  auto rec_at = [&](int k) -> double* {
-#if SRBD_WS_STAGE_MAJOR
-    return a.ws + ((size_t)k * a.batch + qp) * kWsStage;
-#else
-    return a.ws + (size_t)qp * a.ws_qp + (size_t)k * kWsStage;
-#endif
-  };
-
-  StageLoader<FULL> ld{nx, nu};
-  const bool xcol = lane < nx;  // lane owns a real state column
-  const bool ucol = lane < nu;  // lane owns a real input column
-
-  // ---------------- terminal stage: P_N = Q_N, p_N = q_N ----------------
-  double P[12];
-  if (isv) {
-    ld.col(qq + (size_t)N * nx, nx, nx, 0, true, P);
-  } else {
-    ld.col(Qq + (size_t)N * nxx, nx, nx, col, xcol, P);
-  }
-  {
-    double* rec = rec_at(N);
-    if (lane < kMaxDim) store_packed_col(rec + kWsP, lane, P);
-    if (isv) store12(rec + kWsp, P);
-    if (a.P && xcol) store_n(a.P + ((size_t)qp * (N + 1) + N) * nxx + (size_t)lane * nx, nx, P);
-    if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + N) * nx, nx, P);
-  }
-
-  // ---------------- backward sweep ----------------
-#pragma unroll 1
-  for (int k = N - 1; k >= 0; --k) {
-    double A_[12], B_[12];
-    if (isv) {
-      ld.col(bq + (size_t)k * nx, nx, nx, 0, true, A_);
-      sfor<0, 12>([&](auto i) { B_[decltype(i)::value] = 0.0; });
-    } else {
-      ld.col(Aq + (size_t)k * nxx, nx, nx, col, xcol, A_);
-      ld.col(Bq + (size_t)k * nxu, nx, nx, col, ucol, B_);
-    }
-    auto loadR = [&](double (&Rc)[12]) {
-      if (isv) {
-        sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = 0.0; });
-      } else {
-        ld.col(Rq + (size_t)k * nuu, nu, nu, col, ucol, Rc);
-        if constexpr (!FULL) {
-          // padded inputs: R = 1 on the diagonal keeps G positive definite
-          sfor<0, 12>([&](auto i) {
-            constexpr int I = decltype(i)::value;
-            if (lane == I && lane >= nu) Rc[I] = 1.0;
-          });
-        }
-      }
-    };
-    auto loadSQ = [&](double (&Sc)[12], double (&Qc)[12]) {
-      if (isv) {
-        ld.col(rq + (size_t)k * nu, nu, nu, 0, true, Sc);
-        ld.col(qq + (size_t)k * nx, nx, nx, 0, true, Qc);
-      } else {
-        ld.col(Sq + (size_t)k * nxu, nu, nu, col, xcol, Sc);
-        ld.col(Qq + (size_t)k * nxx, nx, nx, col, xcol, Qc);
-      }
-    };
-    StageFactor<double> f;
-    riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
-
-    double* rec = rec_at(k);
-#ifdef SRBD_DIAG_NO_RECORD  // diagnostic build only: no record traffic
-    if (k == -7) {
-#else
-    if (lane < kMaxDim) {
-#endif
-      sfor<0, 12>([&](auto m) {
-        constexpr int M = decltype(m)::value;
-        rec[kWsK + M * 12 + lane] = f.Kc[M];
-        rec[kWsAcl + M * 12 + lane] = A_[M];
-      });
-      store_packed_col(rec + kWsP, lane, f.F);
-    }
-    if (isv) {
-      store12(rec + kWsk, f.Kc);
-      store12(rec + kWsbcl, A_);
-      store12(rec + kWsp, f.F);
-    }
-    if (a.P && xcol) store_n(a.P + ((size_t)qp * (N + 1) + k) * nxx + (size_t)lane * nx, nx, f.F);
-    if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + k) * nx, nx, f.F);
-    if (a.K && xcol) store_n(a.K + ((size_t)qp * N + k) * nxu + (size_t)lane * nu, nu, f.Kc);
-    if (a.k && isv) store_n(a.k + ((size_t)qp * N + k) * nu, nu, f.Kc);
-    sfor<0, 12>([&](auto i) {
-      constexpr int I = decltype(i)::value;
-      P[I] = f.F[I];
-    });
-  }
-
-  // ---------------- forward sweep (row-owned) ----------------
-  // The record rows of stage k+1 are loaded while stage k computes (the loads
-  // do not depend on x), so each stage pays one memory latency less.
-  const int row = lane < kMaxDim ? lane : kMaxDim - 1;
-  double xv = (lane < nx) ? a.x0[(size_t)qp * nx + lane] : 0.0;
-  bool bad = false;
-  double* xo = a.x + (size_t)qp * (N + 1) * nx;
-  double* uo = a.u + (size_t)qp * N * nu;
-  double* po = a.pi + (size_t)qp * (N + 1) * nx;
-  double Pr[12], Kr[12], Ar[12], pv, kv, bv;
-  auto load_rows = [&](int k, double (&P_)[12], double (&K_)[12], double (&A__)[12], double& p_,
-                       double& k_, double& b_) {
-    const double* rec = rec_at(k);
-    load_packed_sym(rec + kWsP, row, P_);
-    p_ = rec[kWsp + row];
-    if (k < N) {
-      load12(rec + kWsK + row * 12, K_);
-      load12(rec + kWsAcl + row * 12, A__);
-      k_ = rec[kWsk + row];
-      b_ = rec[kWsbcl + row];
-    }
-  };
-  load_rows(0, Pr, Kr, Ar, pv, kv, bv);
-#ifdef SRBD_DIAG_NO_FWD  // diagnostic build only
-  if (N > 0) return;
-#endif
-#pragma unroll 1
-  for (int k = 0; k <= N; ++k) {
-    double Pn[12], Kn[12], An[12], pvn = 0.0, kvn = 0.0, bvn = 0.0;
-    if (k < N) load_rows(k + 1, Pn, Kn, An, pvn, kvn, bvn);
-    double bx[12];
-    sfor<0, 12>([&](auto j) {
-      constexpr int J = decltype(j)::value;
-      bx[J] = bc<J>(xv);
-    });
-    double pp = pv;
-    sfor<0, 12>([&](auto j) {
-      constexpr int J = decltype(j)::value;
-      pp = fmadd(Pr[J], bx[J], pp);
-    });
-    if (lane < nx) {
-      xo[(size_t)k * nx + lane] = xv;
-      po[(size_t)k * nx + lane] = pp;
-    }
-    if (k == N) break;
-    double uu = kv, xn = bv;
-    sfor<0, 12>([&](auto j) {
-      constexpr int J = decltype(j)::value;
-      uu = fmadd(Kr[J], bx[J], uu);
-      xn = fmadd(Ar[J], bx[J], xn);
-    });
-    if (lane < nu) uo[(size_t)k * nu + lane] = uu;
-    bad |= (lane < nu && !(uu == uu)) || (lane < nx && !(xn == xn));
-    xv = xn;
-    sfor<0, 12>([&](auto j) {
-      constexpr int J = decltype(j)::value;
-      Pr[J] = Pn[J];
-      Kr[J] = Kn[J];
-      Ar[J] = An[J];
-    });
-    pv = pvn;
-    kv = kvn;
-    bv = bvn;
-  }
-  if (a.status || a.iter) {
-    const unsigned long long m = __ballot(bad);
-    const int shift = (threadIdx.x & 63) & ~(kGroup - 1);
-    const bool any_bad = ((m >> shift) & 0xffffull) != 0;
-    if (lane == 0) {
-      if (a.status) a.status[qp] = any_bad ? 3 : 0;
-      if (a.iter) a.iter[qp] = 0;
-    }
-  }
-}
-
-}  // namespace
 
 size_t ws_doubles_unconstr(int N) { return (size_t)(N + 1) * kWsStage; }
 
-hipError_t launch_riccati_unconstr(const ProblemArgs& a, hipStream_t stream) {
-  if (a.batch <= 0) return hipSuccess;
-  const int threads = 256;
-  const long long lanes = (long long)a.batch * kGroup;
-  const int blocks = (int)((lanes + threads - 1) / threads);
-  if (a.nx == 12 && a.nu == 12) {
-    hipLaunchKernelGGL(riccati_unconstr_kernel<true>, dim3(blocks), dim3(threads), 0, stream, a);
-  } else {
-    hipLaunchKernelGGL(riccati_unconstr_kernel<false>, dim3(blocks), dim3(threads), 0, stream, a);
-  }
-  return hipGetLastError();
+template <>
+hipError_t launch_riccati_unconstr<double>(const ProblemArgsT<double>& a, hipStream_t stream) {
+  return ric_f64::launch(a, stream);
+}
+template <>
+hipError_t launch_riccati_unconstr<float>(const ProblemArgsT<float>& a, hipStream_t stream) {
+  return ric_f32::launch(a, stream);
 }
 
 }  // namespace srbd

@@ -181,8 +181,11 @@ int srbd_qp_synchronize(srbd_qp_handle h) {
   return SRBD_QP_OK;
 }
 
-static int validate_call(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
-                         const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s) {
+}  // extern "C"
+
+template <typename DataT, typename SolT>
+static int validate_call(srbd_qp_handle h, int batch, const srbd_qp_settings* st, const DataT* d,
+                         const SolT* s) {
   if (!h) return fail(SRBD_QP_EINVAL, "handle is NULL");
   if (!d || !s) return fail(SRBD_QP_EINVAL, "data/solution is NULL");
   if (batch < 0) return fail(SRBD_QP_EINVAL, "batch must be >= 0");
@@ -202,8 +205,9 @@ static int validate_call(srbd_qp_handle h, int batch, const srbd_qp_settings* st
   return SRBD_QP_OK;
 }
 
-int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
-                      const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s, void* stream) {
+template <typename T, typename DataT, typename SolT>
+static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, const DataT* d,
+                      const SolT* s, void* stream) {
   int rc = validate_call(h, batch, st, d, s);
   if (rc) return rc;
   if (batch == 0) return SRBD_QP_OK;
@@ -211,7 +215,7 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   int prev = 0;
   hipGetDevice(&prev);
   hipSetDevice(h->device);
-  srbd::ProblemArgs a{};
+  srbd::ProblemArgsT<T> a{};
   a.batch = batch;
   a.N = h->dims.N;
   a.nx = h->dims.nx;
@@ -226,7 +230,7 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   a.P = s->P; a.p = s->p; a.K = s->K; a.k = s->k;
   a.status = s->status; a.iter = s->iter; a.res = s->res; a.obj = s->obj;
   a.stat = s->stat;
-  a.ws = h->ws;
+  a.ws = reinterpret_cast<T*>(h->ws);
   a.ws_qp = h->ws_qp;
   a.reg = st->reg_prim;
   a.iter_max = st->iter_max;
@@ -242,7 +246,7 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   hipError_t e = hipSuccess;
   if (s->stat)
     e = hipMemsetAsync(s->stat, 0,
-                       sizeof(double) * srbd::kStatCols * (size_t)(st->iter_max + 2) * (size_t)batch, strm);
+                       sizeof(T) * srbd::kStatCols * (size_t)(st->iter_max + 2) * (size_t)batch, strm);
   if (e != hipSuccess) {
   } else if (constrained(h->dims)) {
     e = srbd::launch_ipm_box(a, strm);
@@ -251,8 +255,8 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
     if (e == hipSuccess && (s->res || s->obj)) {
       // an unconstrained solve reports zero residual norms / objective unless
       // computed (compute_residuals is not implemented for nc == 0 yet)
-      if (s->res) e = hipMemsetAsync(s->res, 0, sizeof(double) * 4 * (size_t)batch, strm);
-      if (e == hipSuccess && s->obj) e = hipMemsetAsync(s->obj, 0, sizeof(double) * (size_t)batch, strm);
+      if (s->res) e = hipMemsetAsync(s->res, 0, sizeof(T) * 4 * (size_t)batch, strm);
+      if (e == hipSuccess && s->obj) e = hipMemsetAsync(s->obj, 0, sizeof(T) * (size_t)batch, strm);
     }
   }
   hipSetDevice(prev);
@@ -271,19 +275,20 @@ struct Field {
 };
 }  // namespace
 
-int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
-                           const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s) {
+template <typename T, typename DataT, typename SolT>
+static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                           const DataT* d, const SolT* s) {
   int rc = validate_call(h, batch, st, d, s);
   if (rc) return rc;
   if (batch == 0) return SRBD_QP_OK;
   const srbd_qp_dims& m = h->dims;
   const size_t B = (size_t)batch, N = (size_t)m.N, nx = (size_t)m.nx, nu = (size_t)m.nu,
                ng = (size_t)m.ng;
-  const size_t D = sizeof(double);
+  const size_t D = sizeof(T);
   // input fields
   std::vector<Field> in;
   size_t off = 0;
-  auto add = [&](const double* p, size_t n) -> size_t {
+  auto add = [&](const T* p, size_t n) -> size_t {
     if (!p) return (size_t)-1;
     size_t o = off;
     in.push_back({p, n * D, o});
@@ -347,23 +352,23 @@ int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* 
     hipSetDevice(prev);
     return fail(SRBD_QP_EDEVICE, std::string("host->device copy: ") + hipGetErrorString(e));
   }
-  auto dp = [&](size_t o) -> double* {
-    return o == (size_t)-1 ? nullptr : reinterpret_cast<double*>(base + o);
+  auto dp = [&](size_t o) -> T* {
+    return o == (size_t)-1 ? nullptr : reinterpret_cast<T*>(base + o);
   };
   auto ip = [&](size_t o) -> int* { return o == (size_t)-1 ? nullptr : reinterpret_cast<int*>(base + o); };
-  srbd_qp_data_f64 dd{};
+  DataT dd{};
   dd.A = dp(oA); dd.B = dp(oB); dd.b = dp(ob); dd.Q = dp(oQ); dd.S = dp(oS); dd.R = dp(oR);
   dd.q = dp(oq); dd.r = dp(orr); dd.x0 = dp(ox0);
   dd.lbu = dp(olbu); dd.ubu = dp(oubu); dd.lbu_mask = dp(olbum); dd.ubu_mask = dp(oubum);
   dd.lbx = dp(olbx); dd.ubx = dp(oubx); dd.lbx_mask = dp(olbxm); dd.ubx_mask = dp(oubxm);
   dd.C = dp(oC); dd.D = dp(oD); dd.lg = dp(olg); dd.ug = dp(oug); dd.lg_mask = dp(olgm);
   dd.ug_mask = dp(ougm);
-  srbd_qp_solution_f64 ss{};
+  SolT ss{};
   ss.x = dp(ox); ss.u = dp(ou); ss.pi = dp(opi); ss.P = dp(oP); ss.p = dp(op); ss.K = dp(oK);
   ss.k = dp(ok); ss.status = ip(ost); ss.iter = ip(oit); ss.res = dp(ores); ss.obj = dp(oobj);
   ss.stat = dp(ostat);
   hipSetDevice(prev);
-  rc = srbd_qp_solve_f64(h, batch, st, &dd, &ss, nullptr);
+  rc = solve_impl<T>(h, batch, st, &dd, &ss, nullptr);
   if (rc) return rc;
   hipSetDevice(h->device);
   for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)
@@ -372,6 +377,25 @@ int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* 
   hipSetDevice(prev);
   if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("device->host copy: ") + hipGetErrorString(e));
   return SRBD_QP_OK;
+}
+
+extern "C" {
+
+int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                      const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s, void* stream) {
+  return solve_impl<double>(h, batch, st, d, s, stream);
+}
+int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                           const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s) {
+  return solve_host_impl<double>(h, batch, st, d, s);
+}
+int srbd_qp_solve_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                      const srbd_qp_data_f32* d, const srbd_qp_solution_f32* s, void* stream) {
+  return solve_impl<float>(h, batch, st, d, s, stream);
+}
+int srbd_qp_solve_host_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                           const srbd_qp_data_f32* d, const srbd_qp_solution_f32* s) {
+  return solve_host_impl<float>(h, batch, st, d, s);
 }
 
 }  // extern "C"
