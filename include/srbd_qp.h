@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SRBD_QP_ABI_VERSION 3
+#define SRBD_QP_ABI_VERSION 4
 #define SRBD_QP_MAX_NX 12
 #define SRBD_QP_MAX_NU 12
 #define SRBD_QP_MAX_NG 64
@@ -199,6 +199,43 @@ int srbd_qp_solve_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* setti
                       void* stream);
 int srbd_qp_solve_host_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
                            const srbd_qp_data_f32* data, const srbd_qp_solution_f32* sol);
+
+/* ------------------------------------------------------------------------
+ * Device-side SRBD linearisation: the producer of the QP data, i.e.
+ * NMPCSolver::prepareQpStructures (NMPC_solver.cpp:276-314) with the model of
+ * dynamics/SRBD_model.cpp:75-295 (RK4 defect with Euler Jacobians, friction
+ * cone as a relaxed log barrier in the cost), for a batch of linearisation
+ * points, written straight into the solver's input buffers.
+ * Parameters: config/mpc_option.yaml:2-18, NMPC_solver.cpp:53-82, :332-351.
+ * ---------------------------------------------------------------------- */
+typedef struct srbd_model_params {
+  double Q[12], Qf[12];   /* diagonal state weights (mpc_option.yaml Q, Qf)    */
+  double R;               /* input weight                                      */
+  double dt;              /* discretisation step                               */
+  double Lbody[3];        /* body inertia diagonal (the model stores L^-1)     */
+  double mu_b, theta_b;   /* relaxed-barrier weight / threshold                */
+  double mass;
+  double foot_r[3], foot_l[3];  /* foot positions in the body frame          */
+  double mu, Lfx, Lfz, fmax, fmin;  /* friction cone / torque limits         */
+  double x_ref[12];       /* reference state                                   */
+  double qf_scale;        /* terminal weight factor (<= 0: N, NMPC_solver.cpp:58) */
+  double u_lo[12], u_hi[12];  /* box on u + du for SRBD_QP_SRBD_BOX_U         */
+} srbd_model_params;
+
+enum { SRBD_QP_SRBD_NONE = 0, SRBD_QP_SRBD_BOX_U = 1, SRBD_QP_SRBD_CONE = 2 };
+
+/* mpc_option.yaml / setupDynamics defaults (box: (+-50, +-50, 0..300 N,
+ * +-5 Nm) per foot). */
+void srbd_qp_srbd_default_params(srbd_model_params* p);
+
+/* Linearise `batch` SRBD trajectories on the handle's device and stream (or
+ * `stream`): xs [batch][N+1][12], us [batch][N][12] (device).  Fills A, B, b,
+ * Q, S, R, q, r of `out` and, per `constraints`, lbu/ubu (BOX_U) or C, D, lg,
+ * ug, lg_mask, ug_mask (CONE: ng = 24, lg = -f(u), ug masked).  The handle's
+ * dims must be N, nx = nu = 12 (and ng = 24 for CONE).  Asynchronous.       */
+int srbd_qp_srbd_linearize_f64(srbd_qp_handle h, int batch, const srbd_model_params* params,
+                               int constraints, const double* xs, const double* us,
+                               const srbd_qp_data_f64* out, void* stream);
 
 /* Blocks until all work queued on the handle's stream is done.            */
 int srbd_qp_synchronize(srbd_qp_handle h);

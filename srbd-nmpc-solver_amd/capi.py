@@ -64,6 +64,20 @@ class Solution32(C.Structure):
 
 MODES = {"SpeedAbs": 0, "Speed": 1, "Balance": 2, "Robust": 3}
 
+
+class ModelParams(C.Structure):
+    """srbd_model_params (include/srbd_qp.h): mpc_option.yaml / setupDynamics."""
+    _fields_ = [("Q", C.c_double * 12), ("Qf", C.c_double * 12), ("R", C.c_double),
+                ("dt", C.c_double), ("Lbody", C.c_double * 3), ("mu_b", C.c_double),
+                ("theta_b", C.c_double), ("mass", C.c_double), ("foot_r", C.c_double * 3),
+                ("foot_l", C.c_double * 3), ("mu", C.c_double), ("Lfx", C.c_double),
+                ("Lfz", C.c_double), ("fmax", C.c_double), ("fmin", C.c_double),
+                ("x_ref", C.c_double * 12), ("qf_scale", C.c_double),
+                ("u_lo", C.c_double * 12), ("u_hi", C.c_double * 12)]
+
+
+SRBD_CONSTRAINTS = {"none": 0, "box_u": 1, "cone": 2}
+
 _lib = None
 
 
@@ -113,6 +127,11 @@ def lib():
         L.srbd_qp_error_string.restype = C.c_char_p
         L.srbd_qp_last_error.argtypes = []
         L.srbd_qp_last_error.restype = C.c_char_p
+        L.srbd_qp_srbd_default_params.argtypes = [C.POINTER(ModelParams)]
+        L.srbd_qp_srbd_default_params.restype = None
+        L.srbd_qp_srbd_linearize_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(ModelParams), C.c_int,
+                                                 C.c_void_p, C.c_void_p, C.POINTER(Data), C.c_void_p]
+        L.srbd_qp_srbd_linearize_f64.restype = C.c_int
         L.srbd_qp_abi_version.argtypes = []
         L.srbd_qp_abi_version.restype = C.c_int
         _lib = L
@@ -264,3 +283,42 @@ def solve(qp, x0, settings: Optional[Dict] = None, device: str = "cuda:0", ricca
     if handle is None:
         h.close()
     return out
+
+
+def default_model_params() -> ModelParams:
+    p = ModelParams()
+    lib().srbd_qp_srbd_default_params(C.byref(p))
+    return p
+
+
+def srbd_linearize(handle: Handle, xs, us, constraints: str = "none",
+                   params: Optional[ModelParams] = None, stream: int = 0):
+    """Device-side prepareQpStructures: linearise SRBD trajectories xs [B][N+1][12],
+    us [B][N][12] (torch fp64 device tensors) into the solver's input buffers.
+    Asynchronous on the handle's stream: keep xs / us alive (and do not reuse
+    their memory from another stream) until that stream has finished.
+    Returns (dict of device tensors in the C-ABI layout, Data)."""
+    import torch
+    B, N1, _ = xs.shape
+    N = N1 - 1
+    dev = xs.device
+    f = dict(dtype=torch.float64, device=dev)
+    t = {"A": torch.empty(B, N, 144, **f), "B": torch.empty(B, N, 144, **f),
+         "b": torch.empty(B, N, 12, **f), "Q": torch.empty(B, N + 1, 144, **f),
+         "S": torch.empty(B, N, 144, **f), "R": torch.empty(B, N, 144, **f),
+         "q": torch.empty(B, N + 1, 12, **f), "r": torch.empty(B, N, 12, **f)}
+    if constraints == "box_u":
+        t["lbu"] = torch.empty(B, N, 12, **f)
+        t["ubu"] = torch.empty(B, N, 12, **f)
+    elif constraints == "cone":
+        t["C"] = torch.empty(B, N + 1, 24 * 12, **f)
+        t["D"] = torch.empty(B, N, 24 * 12, **f)
+        for k in ("lg", "ug", "lg_mask", "ug_mask"):
+            t[k] = torch.empty(B, N + 1, 24, **f)
+    data = Data(**{k: _tensor_ptr(t.get(k)) or None for k in DATA_FIELDS})
+    p = params or default_model_params()
+    check(lib().srbd_qp_srbd_linearize_f64(handle.ptr, int(B), C.byref(p), SRBD_CONSTRAINTS[constraints],
+                                           C.c_void_p(xs.data_ptr()), C.c_void_p(us.data_ptr()),
+                                           C.byref(data), C.c_void_p(stream or None)),
+          "srbd_qp_srbd_linearize_f64")
+    return t, data

@@ -82,3 +82,10 @@ template <typename T>
 hipError_t launch_riccati_unconstr(const ProblemArgsT<T>& a, hipStream_t stream);
 
 }  // namespace srbd
+#include "../../include/srbd_qp.h"
+namespace srbd {
+hipError_t launch_srbd_linearize(const srbd_model_params& p, int batch, int N, int mode,
+                                 const double* xs, const double* us,
+                                 const srbd_qp_data_f64& out, hipStream_t stream);
+
+}  // namespace srbd

@@ -389,6 +389,66 @@ int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* 
                            const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s) {
   return solve_host_impl<double>(h, batch, st, d, s);
 }
+void srbd_qp_srbd_default_params(srbd_model_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  const double Q[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 10};
+  const double Qf[12] = {0.5, 0.5, 0.5, 0.01, 0.01, 0.01, 100, 100, 100, 0.0, 0.0, 100.0};
+  const double xr[12] = {0, 0, 0.2, 0, 0, 0, 0.5, 0, 1.0, 0, 0, 0};
+  const double lo[6] = {-50.0, -50.0, 0.0, -5.0, -5.0, -5.0}, hi[6] = {50.0, 50.0, 300.0, 5.0, 5.0, 5.0};
+  for (int i = 0; i < 12; ++i) {
+    p->Q[i] = Q[i];
+    p->Qf[i] = Qf[i];
+    p->x_ref[i] = xr[i];
+    p->u_lo[i] = lo[i % 6];
+    p->u_hi[i] = hi[i % 6];
+  }
+  p->R = 0.0001;
+  p->dt = 0.015;
+  p->Lbody[0] = 0.541667;
+  p->Lbody[1] = 0.516667;
+  p->Lbody[2] = 1.0416667;
+  p->mu_b = 0.1;
+  p->theta_b = 5.0;
+  p->mass = 15.0;
+  p->foot_r[1] = -0.1;
+  p->foot_l[1] = 0.1;
+  p->mu = 0.5;
+  p->Lfx = 0.05;
+  p->Lfz = 0.05;
+  p->fmax = 1000.0;
+  p->fmin = 0.0;
+  p->qf_scale = 0.0;  // N
+}
+
+int srbd_qp_srbd_linearize_f64(srbd_qp_handle h, int batch, const srbd_model_params* params,
+                               int constraints, const double* xs, const double* us,
+                               const srbd_qp_data_f64* out, void* stream) {
+  if (!h || !params || !xs || !us || !out) return fail(SRBD_QP_EINVAL, "NULL argument");
+  const srbd_qp_dims& d = h->dims;
+  if (d.nx != 12 || d.nu != 12) return fail(SRBD_QP_EDIM, "SRBD linearisation needs nx = nu = 12");
+  if (batch < 0 || batch > h->capacity) return fail(SRBD_QP_ECAPACITY, "batch exceeds capacity");
+  if (constraints < SRBD_QP_SRBD_NONE || constraints > SRBD_QP_SRBD_CONE)
+    return fail(SRBD_QP_EINVAL, "unknown constraints mode");
+  if (!out->A || !out->B || !out->b || !out->Q || !out->S || !out->R || !out->q || !out->r)
+    return fail(SRBD_QP_EINVAL, "A, B, b, Q, S, R, q, r outputs are required");
+  if (constraints == SRBD_QP_SRBD_BOX_U && (!out->lbu || !out->ubu))
+    return fail(SRBD_QP_EINVAL, "BOX_U needs lbu / ubu outputs");
+  if (constraints == SRBD_QP_SRBD_CONE &&
+      (d.ng != 24 || !out->C || !out->D || !out->lg || !out->ug || !out->lg_mask || !out->ug_mask))
+    return fail(SRBD_QP_EINVAL, "CONE needs ng = 24 and C, D, lg, ug, lg_mask, ug_mask outputs");
+  srbd_model_params p = *params;
+  if (p.qf_scale <= 0.0) p.qf_scale = (double)d.N;
+  hipStream_t strm = stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(h->device);
+  const hipError_t e = srbd::launch_srbd_linearize(p, batch, d.N, constraints, xs, us, *out, strm);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
+  return SRBD_QP_OK;
+}
+
 int srbd_qp_solve_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                       const srbd_qp_data_f32* d, const srbd_qp_solution_f32* s, void* stream) {
   return solve_impl<float>(h, batch, st, d, s, stream);
