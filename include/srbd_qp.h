@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SRBD_QP_ABI_VERSION 4
+#define SRBD_QP_ABI_VERSION 5
 #define SRBD_QP_MAX_NX 12
 #define SRBD_QP_MAX_NU 12
 #define SRBD_QP_MAX_NG 64
@@ -236,6 +236,23 @@ void srbd_qp_srbd_default_params(srbd_model_params* p);
 int srbd_qp_srbd_linearize_f64(srbd_qp_handle h, int batch, const srbd_model_params* params,
                                int constraints, const double* xs, const double* us,
                                const srbd_qp_data_f64* out, void* stream);
+
+/* Batched filter line search of the SQP iteration (NMPCSolver::linearSearch,
+ * NMPC_solver.cpp:149-274): per QP, merit phi (cost + friction barrier) and
+ * theta (shooting defect) at xs/us, trial steps alpha, beta alpha, ... along
+ * the QP solution (dx [B][N+1][12], du [B][N][12]) until the filter accepts;
+ * xs/us (device, in place) move to the accepted point.  alpha [B] is read and
+ * written like the reference's persistent alpha_ (NMPC_solver.h:104); merit
+ * [B][3] (phi, theta, dphi) and converged [B] (dphi > -1e-3 && theta < 1e-6)
+ * are optional.  Constants: NMPC_solver.h:97-103.                         */
+typedef struct srbd_linesearch_params {
+  double theta_max, theta_min, eta, beta_phi, beta_theta, beta_alpha, alpha_min;
+} srbd_linesearch_params;
+void srbd_qp_srbd_default_linesearch(srbd_linesearch_params* p);
+int srbd_qp_srbd_linesearch_f64(srbd_qp_handle h, int batch, const srbd_model_params* params,
+                                const srbd_linesearch_params* ls, double* xs, double* us,
+                                const double* dx, const double* du, double* alpha, double* merit,
+                                int* converged, void* stream);
 
 /* Blocks until all work queued on the handle's stream is done.            */
 int srbd_qp_synchronize(srbd_qp_handle h);

@@ -78,6 +78,12 @@ class ModelParams(C.Structure):
 
 SRBD_CONSTRAINTS = {"none": 0, "box_u": 1, "cone": 2}
 
+
+class LsParams(C.Structure):
+    """srbd_linesearch_params (NMPC_solver.h:97-103)."""
+    _fields_ = [(n, C.c_double) for n in ("theta_max", "theta_min", "eta", "beta_phi",
+                                         "beta_theta", "beta_alpha", "alpha_min")]
+
 _lib = None
 
 
@@ -132,6 +138,11 @@ def lib():
         L.srbd_qp_srbd_linearize_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(ModelParams), C.c_int,
                                                  C.c_void_p, C.c_void_p, C.POINTER(Data), C.c_void_p]
         L.srbd_qp_srbd_linearize_f64.restype = C.c_int
+        L.srbd_qp_srbd_default_linesearch.argtypes = [C.POINTER(LsParams)]
+        L.srbd_qp_srbd_default_linesearch.restype = None
+        L.srbd_qp_srbd_linesearch_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(ModelParams),
+                                                  C.POINTER(LsParams)] + [C.c_void_p] * 8
+        L.srbd_qp_srbd_linesearch_f64.restype = C.c_int
         L.srbd_qp_abi_version.argtypes = []
         L.srbd_qp_abi_version.restype = C.c_int
         _lib = L
@@ -322,3 +333,28 @@ def srbd_linearize(handle: Handle, xs, us, constraints: str = "none",
                                            C.byref(data), C.c_void_p(stream or None)),
           "srbd_qp_srbd_linearize_f64")
     return t, data
+
+
+def default_linesearch() -> LsParams:
+    p = LsParams()
+    lib().srbd_qp_srbd_default_linesearch(C.byref(p))
+    return p
+
+
+def srbd_linesearch(handle: Handle, xs, us, dx, du, alpha, params: Optional[ModelParams] = None,
+                    ls: Optional[LsParams] = None, stream: int = 0):
+    """Device filter line search (NMPCSolver::linearSearch) on a batch: xs/us
+    (torch fp64, in place), dx/du the QP step, alpha [B] in/out.  Returns
+    (merit [B,3] = phi, theta, dphi; converged [B]) device tensors."""
+    import torch
+    B = xs.shape[0]
+    merit = torch.empty(B, 3, dtype=torch.float64, device=xs.device)
+    conv = torch.empty(B, dtype=torch.int32, device=xs.device)
+    p = params or default_model_params()
+    lp = ls or default_linesearch()
+    ptr = lambda t: C.c_void_p(t.data_ptr())
+    check(lib().srbd_qp_srbd_linesearch_f64(handle.ptr, int(B), C.byref(p), C.byref(lp), ptr(xs),
+                                            ptr(us), ptr(dx), ptr(du), ptr(alpha), ptr(merit),
+                                            ptr(conv), C.c_void_p(stream or None)),
+          "srbd_qp_srbd_linesearch_f64")
+    return merit, conv

@@ -84,6 +84,10 @@ hipError_t launch_riccati_unconstr(const ProblemArgsT<T>& a, hipStream_t stream)
 }  // namespace srbd
 #include "../../include/srbd_qp.h"
 namespace srbd {
+hipError_t launch_srbd_linesearch(const srbd_model_params& p, const srbd_linesearch_params& ls,
+                                  int batch, int N, double* xs, double* us, const double* dx,
+                                  const double* du, double* alpha, double* merit, int* converged,
+                                  hipStream_t stream);
 hipError_t launch_srbd_linearize(const srbd_model_params& p, int batch, int N, int mode,
                                  const double* xs, const double* us,
                                  const srbd_qp_data_f64& out, hipStream_t stream);

@@ -315,7 +315,164 @@ __global__ void __launch_bounds__(64) srbd_linearize_kernel(Model m, LinArgs a) 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Batched filter line search (NMPCSolver::linearSearch, NMPC_solver.cpp:149-274).
+// One 32-lane group per QP, lane l owns stages l, l + 32, ...; each trial step
+// length is one pass over the stages + a group reduction, decisions are
+// group-uniform.  Restated for the tests in oracle/nmpc_linesearch.py.
+// ---------------------------------------------------------------------------
+constexpr int kLsGroup = 32;
+
+__device__ __forceinline__ double gsum32(double v) {
+  for (int m = kLsGroup / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, kLsGroup);
+  return v;
+}
+
+struct LsArgs {
+  int batch, N;
+  double *xs, *us;
+  const double *dx, *du;
+  double* alpha;
+  double* merit;
+  int* converged;
+  srbd_linesearch_params ls;
+  double qf_scale;
+};
+
+// merit terms of stage k at (x + a dx, u + a du): phi_k, theta_k and, when
+// grad, the directional derivative dx'Jphi_x + du'Jphi_u
+__device__ void stage_merit(const Model& m, const LsArgs& a, int qp, int k, double al, bool grad,
+                            double& phi, double& theta, double& dphi) {
+  const srbd_model_params& p = m.p;
+  const int N = a.N;
+  const double* x = a.xs + ((size_t)qp * (N + 1) + k) * 12;
+  const double* dx = a.dx + ((size_t)qp * (N + 1) + k) * 12;
+  double xa[12];
+  for (int i = 0; i < 12; ++i) xa[i] = x[i] + al * dx[i];
+  const double* w = k < N ? p.Q : p.Qf;
+  const double sc = k < N ? 1.0 : a.qf_scale;
+  for (int i = 0; i < 12; ++i) {
+    const double e = xa[i] - p.x_ref[i];
+    phi += 0.5 * sc * w[i] * e * e;
+    if (grad) dphi += dx[i] * sc * w[i] * e;
+  }
+  if (k == N) return;
+  const double* u = a.us + ((size_t)qp * N + k) * 12;
+  const double* du = a.du + ((size_t)qp * N + k) * 12;
+  const double* xn = a.xs + ((size_t)qp * (N + 1) + k + 1) * 12;
+  const double* dxn = a.dx + ((size_t)qp * (N + 1) + k + 1) * 12;
+  double ua[12], k1[12], k2[12], k3[12], k4[12], xt[12];
+  for (int i = 0; i < 12; ++i) ua[i] = u[i] + al * du[i];
+  // shooting defect f = x_next - RK4(x, u) (GetShootingDynamic)
+  const double dt = p.dt;
+  m.f(xa, ua, k1, nullptr, nullptr);
+  for (int i = 0; i < 12; ++i) xt[i] = xa[i] + 0.5 * dt * k1[i];
+  m.f(xt, ua, k2, nullptr, nullptr);
+  for (int i = 0; i < 12; ++i) xt[i] = xa[i] + 0.5 * dt * k2[i];
+  m.f(xt, ua, k3, nullptr, nullptr);
+  for (int i = 0; i < 12; ++i) xt[i] = xa[i] + dt * k3[i];
+  m.f(xt, ua, k4, nullptr, nullptr);
+  for (int i = 0; i < 12; ++i) {
+    const double xg = xa[i] + (dt / 6.0) * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
+    const double f = (xn[i] + al * dxn[i]) - xg;
+    theta += 0.5 * f * f;
+  }
+  // input cost: relaxed barrier of the friction cone + 0.5 u'R u
+  double ju[12];
+  for (int i = 0; i < 12; ++i) {
+    ju[i] = p.R * ua[i];
+    phi += 0.5 * p.R * ua[i] * ua[i];
+  }
+  for (int c = 0; c < 24; ++c) {
+    double v = m.bc(c);
+    for (int j = 0; j < 12; ++j) v = fma(m.ac(c, j), ua[j], v);
+    double db;
+    if (v > p.theta_b) {
+      phi += -p.mu_b * log(v);
+      db = -p.mu_b / v;
+    } else {
+      const double z = (v - 2.0 * p.theta_b) / p.theta_b;
+      phi += 0.5 * p.mu_b * (z * z - 1.0) - p.mu_b * log(p.theta_b);
+      db = p.mu_b * (v - 2.0 * p.theta_b) / (p.theta_b * p.theta_b);
+    }
+    if (grad)
+      for (int j = 0; j < 12; ++j) ju[j] = fma(m.ac(c, j), db, ju[j]);
+  }
+  if (grad)
+    for (int i = 0; i < 12; ++i) dphi += du[i] * ju[i];
+}
+
+__global__ void __launch_bounds__(64) srbd_linesearch_kernel(Model m, LsArgs a) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int qp = gid / kLsGroup, lane = gid % kLsGroup;
+  if (qp >= a.batch) return;
+  const int N = a.N;
+  const srbd_linesearch_params& ls = a.ls;
+  // merit at the current iterate
+  double phi = 0.0, theta = 0.0, dphi = 0.0;
+  for (int k = lane; k <= N; k += kLsGroup) stage_merit(m, a, qp, k, 0.0, true, phi, theta, dphi);
+  phi = gsum32(phi);
+  theta = gsum32(theta);
+  dphi = gsum32(dphi);
+  double alpha = a.alpha[qp];
+  double accepted = -1.0;  // accepted step length, -1: none
+  while (alpha > ls.alpha_min) {
+    double pa = 0.0, ta = 0.0, unused = 0.0;
+    for (int k = lane; k <= N; k += kLsGroup) stage_merit(m, a, qp, k, alpha, false, pa, ta, unused);
+    pa = gsum32(pa);
+    ta = gsum32(ta);
+    bool ok;
+    if (ta > ls.theta_max) {
+      ok = ta < (1.0 - ls.beta_theta) * theta;
+    } else if (fmax(ta, theta) < ls.theta_min && dphi < 0.0) {
+      ok = pa < phi + ls.eta * alpha * dphi;
+    } else {
+      ok = pa < phi - ls.beta_phi * theta || ta < (1.0 - ls.beta_theta) * theta;
+    }
+    if (ok) {
+      accepted = alpha;
+      break;
+    }
+    alpha = ls.beta_alpha * alpha;
+  }
+  if (accepted > 0.0) {
+    for (int k = lane; k <= N; k += kLsGroup) {
+      double* x = a.xs + ((size_t)qp * (N + 1) + k) * 12;
+      const double* dx = a.dx + ((size_t)qp * (N + 1) + k) * 12;
+      for (int i = 0; i < 12; ++i) x[i] += accepted * dx[i];
+      if (k < N) {
+        double* u = a.us + ((size_t)qp * N + k) * 12;
+        const double* du = a.du + ((size_t)qp * N + k) * 12;
+        for (int i = 0; i < 12; ++i) u[i] += accepted * du[i];
+      }
+    }
+  }
+  if (lane == 0) {
+    a.alpha[qp] = alpha;
+    if (a.merit) {
+      a.merit[(size_t)qp * 3 + 0] = phi;
+      a.merit[(size_t)qp * 3 + 1] = theta;
+      a.merit[(size_t)qp * 3 + 2] = dphi;
+    }
+    if (a.converged) a.converged[qp] = (dphi > -1e-3 && theta < 1e-6) ? 1 : 0;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_srbd_linesearch(const srbd_model_params& p, const srbd_linesearch_params& ls,
+                                  int batch, int N, double* xs, double* us, const double* dx,
+                                  const double* du, double* alpha, double* merit, int* converged,
+                                  hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  Model m{p};
+  LsArgs a{batch, N, xs, us, dx, du, alpha, merit, converged, ls, p.qf_scale};
+  const long long n = (long long)batch * kLsGroup;
+  const int threads = 64;
+  hipLaunchKernelGGL(srbd_linesearch_kernel, dim3((unsigned)((n + threads - 1) / threads)),
+                     dim3(threads), 0, stream, m, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_srbd_linearize(const srbd_model_params& p, int batch, int N, int mode,
                                  const double* xs, const double* us,

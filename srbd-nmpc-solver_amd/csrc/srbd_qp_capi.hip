@@ -449,6 +449,41 @@ int srbd_qp_srbd_linearize_f64(srbd_qp_handle h, int batch, const srbd_model_par
   return SRBD_QP_OK;
 }
 
+void srbd_qp_srbd_default_linesearch(srbd_linesearch_params* p) {
+  if (!p) return;
+  p->theta_max = 1e-6;
+  p->theta_min = 5e-10;
+  p->eta = 1e-4;
+  p->beta_phi = 1e-6;
+  p->beta_theta = 1e-6;
+  p->beta_alpha = 0.5;
+  p->alpha_min = 1e-4;
+}
+
+int srbd_qp_srbd_linesearch_f64(srbd_qp_handle h, int batch, const srbd_model_params* params,
+                                const srbd_linesearch_params* ls, double* xs, double* us,
+                                const double* dx, const double* du, double* alpha, double* merit,
+                                int* converged, void* stream) {
+  if (!h || !params || !ls || !xs || !us || !dx || !du || !alpha)
+    return fail(SRBD_QP_EINVAL, "NULL argument");
+  const srbd_qp_dims& d = h->dims;
+  if (d.nx != 12 || d.nu != 12) return fail(SRBD_QP_EDIM, "SRBD line search needs nx = nu = 12");
+  if (batch < 0 || batch > h->capacity) return fail(SRBD_QP_ECAPACITY, "batch exceeds capacity");
+  if (!(ls->beta_alpha > 0.0 && ls->beta_alpha < 1.0) || !(ls->alpha_min > 0.0))
+    return fail(SRBD_QP_EINVAL, "line search needs 0 < beta_alpha < 1 and alpha_min > 0");
+  srbd_model_params p = *params;
+  if (p.qf_scale <= 0.0) p.qf_scale = (double)d.N;
+  hipStream_t strm = stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(h->device);
+  const hipError_t e = srbd::launch_srbd_linesearch(p, *ls, batch, d.N, xs, us, dx, du, alpha,
+                                                    merit, converged, strm);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
+  return SRBD_QP_OK;
+}
+
 int srbd_qp_solve_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                       const srbd_qp_data_f32* d, const srbd_qp_solution_f32* s, void* stream) {
   return solve_impl<float>(h, batch, st, d, s, stream);

@@ -29,7 +29,7 @@ import numpy as np
 
 from .qp import OcpQpBatch
 
-__all__ = ["SrbdParams", "generate_batch", "shooting_dynamics", "friction_cone", "barrier"]
+__all__ = ["SrbdParams", "generate_batch", "build_qp", "sample_trajectories", "shooting_dynamics", "friction_cone", "barrier"]
 
 
 @dataclass(frozen=True)
@@ -239,16 +239,11 @@ def sample_trajectories(batch, N, seed, p: SrbdParams, first: int = 0):
     return xs, us, x0
 
 
-def generate_batch(batch: int, N: int = 20, seed: int = 1001, constraints: str = "none",
-                   p: Optional[SrbdParams] = None, first: int = 0):
-    """Build `batch` SRBD OCP-QPs exactly as prepareQpStructures does.
-
-    constraints: "none" (the reference's own QP: friction cone as a barrier in
-    the cost, no inequalities), "box_u" (config 3: u + du inside per-foot force /
-    torque boxes), "cone" (config 5: lg <= Ac du with lg = -f(u), ug masked).
-    Returns (OcpQpBatch, x0)."""
+def build_qp(xs, us, p: Optional[SrbdParams] = None, constraints: str = "none", meta=None):
+    """QP data of NMPCSolver::prepareQpStructures (NMPC_solver.cpp:276-314) at the
+    linearisation points xs [B][N+1][12], us [B][N][12].  Returns (OcpQpBatch, fc)."""
     p = p or SrbdParams()
-    xs, us, x0 = sample_trajectories(batch, N, seed, p, first)
+    batch, N = us.shape[0], us.shape[1]
     A, B, b = shooting_dynamics(xs[:, :-1], xs[:, 1:], us, p)
     Ac, bc = friction_cone(p)
     fc = np.einsum("ij,bkj->bki", Ac, us) + bc
@@ -267,7 +262,7 @@ def generate_batch(batch: int, N: int = 20, seed: int = 1001, constraints: str =
     r = np.einsum("ij,bkj->bki", Rm, us) + np.einsum("ci,bkc->bki", Ac, db)
     S = np.zeros((batch, N, 12, 12))
     qp = OcpQpBatch(N=N, nx=12, nu=12, A=A, B=B, b=b, Q=Q, S=S, R=R, q=q, r=r,
-                    meta={"seed": seed, "first": first, "constraints": constraints})
+                    meta=dict(meta or {}, constraints=constraints))
     if constraints == "box_u":
         qp.lbu = U_BOX_LO - us
         qp.ubu = U_BOX_HI - us
@@ -283,4 +278,18 @@ def generate_batch(batch: int, N: int = 20, seed: int = 1001, constraints: str =
         qp.ug_mask = np.zeros((batch, N + 1, 24))
     elif constraints != "none":
         raise ValueError(f"unknown constraints {constraints!r}")
+    return qp, fc
+
+
+def generate_batch(batch: int, N: int = 20, seed: int = 1001, constraints: str = "none",
+                   p: Optional[SrbdParams] = None, first: int = 0):
+    """Build `batch` SRBD OCP-QPs exactly as prepareQpStructures does.
+
+    constraints: "none" (the reference's own QP: friction cone as a barrier in
+    the cost, no inequalities), "box_u" (config 3: u + du inside per-foot force /
+    torque boxes), "cone" (config 5: lg <= Ac du with lg = -f(u), ug masked).
+    Returns (OcpQpBatch, x0)."""
+    p = p or SrbdParams()
+    xs, us, x0 = sample_trajectories(batch, N, seed, p, first)
+    qp, _ = build_qp(xs, us, p, constraints, meta={"seed": seed, "first": first})
     return qp, x0
