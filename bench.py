@@ -131,6 +131,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="skip the on-device SQP-iteration measurement (linearise + solve + line search)")
     args = ap.parse_args()
 
     import torch
@@ -198,6 +200,11 @@ def main():
     log(f"[rank {rank}] wall {t_wall * 1e3:.2f} ms for {args.steps} steps, kernel avg {kernel_ms:.3f} ms, "
         f"success {n_ok}/{batch}")
 
+    # ---- the whole SQP iteration on the device (secondary; not `value`) ----
+    pipeline = None
+    if not args.no_pipeline and dtype == "f64":
+        pipeline = sqp_pipeline(pkg, h, N, constraints, batch, args.seed, args.pool, rank, device, settings)
+
     # ---- solution gather to rank 0 over RCCL (BASELINE config 4) ----
     gather_ms = None
     if distributed and not args.no_gather:
@@ -259,6 +266,8 @@ def main():
         "iters_mean": float(iters.mean()), "iters_max": int(iters.max()),
         "cpu_baseline": cpu,
     }
+    if pipeline is not None:
+        line["sqp_pipeline"] = pipeline
     if gather_ms is not None:
         line["gather"] = {"ms": gather_ms, "bytes_per_rank": batch * (2 * (N + 1) * 12 + N * 12) * 8,
                           "value_with_gather": total_qps / (t_max / args.steps + gather_ms * 1e-3)}
@@ -266,6 +275,61 @@ def main():
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def sqp_pipeline(pkg, h, N, constraints, batch, seed, pool, rank, device, settings, iters=3):
+    """One SQP iteration of NMPCSolver::controlLoop (NMPC_solver.cpp:362-372) for the
+    whole batch on the device: srbd_qp_srbd_linearize_f64 -> solve ->
+    srbd_qp_srbd_linesearch_f64, timed with HIP events on the handle's stream."""
+    import torch
+    capi = pkg.capi
+    p = pkg.srbd_model.SrbdParams()
+    pool = min(pool, batch)
+    first, _ = pkg.dist.shard_range(rank, batch)
+    xs, us, x0 = pkg.srbd_model.sample_trajectories(pool, N, seed, p, first)
+    reps = (batch + pool - 1) // pool
+    tile = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device).repeat(
+        (reps,) + (1,) * (a.ndim - 1))[:batch].contiguous()
+    xs_t, us_t, x0_t = tile(xs), tile(us), tile(x0)
+    alpha = torch.ones(batch, dtype=torch.float64, device=device)
+    f64 = dict(dtype=torch.float64, device=device)
+    sol = {"x": torch.zeros(batch, N + 1, 12, **f64), "u": torch.zeros(batch, N, 12, **f64),
+           "pi": torch.zeros(batch, N + 1, 12, **f64)}
+    S = capi.Solution(**{k: (sol[k].data_ptr() if k in sol else None) for k in capi.SOL_FIELDS})
+    t, data = capi.srbd_linearize(h, xs_t, us_t, constraints)
+    dx0 = torch.empty_like(x0_t)
+    merit = torch.empty(batch, 3, **f64)
+    conv = torch.empty(batch, dtype=torch.int32, device=device)
+    ext = torch.cuda.ExternalStream(h.stream(), device=device)
+    lp, mp = capi.default_linesearch(), capi.default_model_params()
+    ptr = lambda x: capi.C.c_void_p(x.data_ptr())
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    tot = [0.0, 0.0, 0.0]
+    h.synchronize()
+    for it in range(iters + 1):  # iteration 0 warms up (lazy torch / HIP init on the stream)
+        ev[0].record(ext)
+        capi.srbd_linearize(h, xs_t, us_t, constraints, out=t)
+        ev[1].record(ext)
+        with torch.cuda.stream(ext):
+            torch.sub(x0_t, xs_t[:, 0], out=dx0)  # x0 - x_nmpc(:,0) (NMPC_solver.cpp:320)
+        data.x0 = dx0.data_ptr()
+        h.solve_device(batch, settings, data, S)
+        ev[2].record(ext)
+        capi.check(capi.lib().srbd_qp_srbd_linesearch_f64(
+            h.ptr, batch, capi.C.byref(mp), capi.C.byref(lp), ptr(xs_t), ptr(us_t), ptr(sol["x"]),
+            ptr(sol["u"]), ptr(alpha), ptr(merit), ptr(conv), None), "linesearch")
+        ev[3].record(ext)
+        h.synchronize()
+        if it > 0:
+            for j in range(3):
+                tot[j] += ev[j].elapsed_time(ev[j + 1])
+    lin, solve, ls = (x / iters for x in tot)
+    return {"what": "SQP iteration of NMPC_solver.cpp:362-372 on device: linearise + QP solve + "
+                    "filter line search, whole batch, inputs/outputs resident",
+            "iterations_timed": iters, "ms_linearize": lin, "ms_qp_solve": solve,
+            "ms_line_search": ls, "ms_per_sqp_iteration": lin + solve + ls,
+            "sqp_iterations_per_s": batch / ((lin + solve + ls) * 1e-3),
+            "converged_after": float(conv.float().mean().item())}
 
 
 def roofline(constraints, achieved_gbs, traffic, kernel_ms, bytes_qp, flops_qp, batch, iters,

@@ -303,7 +303,7 @@ def default_model_params() -> ModelParams:
 
 
 def srbd_linearize(handle: Handle, xs, us, constraints: str = "none",
-                   params: Optional[ModelParams] = None, stream: int = 0):
+                   params: Optional[ModelParams] = None, stream: int = 0, out=None):
     """Device-side prepareQpStructures: linearise SRBD trajectories xs [B][N+1][12],
     us [B][N][12] (torch fp64 device tensors) into the solver's input buffers.
     Asynchronous on the handle's stream: keep xs / us alive (and do not reuse
@@ -314,6 +314,15 @@ def srbd_linearize(handle: Handle, xs, us, constraints: str = "none",
     N = N1 - 1
     dev = xs.device
     f = dict(dtype=torch.float64, device=dev)
+    if out is not None:  # caller-owned buffers from a previous call (no allocation)
+        t = out
+        data = Data(**{k: _tensor_ptr(t.get(k)) or None for k in DATA_FIELDS})
+        p = params or default_model_params()
+        check(lib().srbd_qp_srbd_linearize_f64(handle.ptr, int(B), C.byref(p),
+                                               SRBD_CONSTRAINTS[constraints], C.c_void_p(xs.data_ptr()),
+                                               C.c_void_p(us.data_ptr()), C.byref(data),
+                                               C.c_void_p(stream or None)), "srbd_qp_srbd_linearize_f64")
+        return t, data
     t = {"A": torch.empty(B, N, 144, **f), "B": torch.empty(B, N, 144, **f),
          "b": torch.empty(B, N, 12, **f), "Q": torch.empty(B, N + 1, 144, **f),
          "S": torch.empty(B, N, 144, **f), "R": torch.empty(B, N, 144, **f),
