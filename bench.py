@@ -100,7 +100,7 @@ def make_shard(pkg, N, constraints, batch, rank, seed, pool):
     return qp, x0
 
 
-def to_device(pkg, qp, x0, batch, device, np_dtype=np.float64):
+def to_device(pkg, qp, x0, batch, device, np_dtype=np.float64, stage_major=False):
     import torch
     p = {k: (None if v is None else np.ascontiguousarray(v, dtype=np_dtype))
          for k, v in qp.packed().items()}
@@ -115,7 +115,10 @@ def to_device(pkg, qp, x0, batch, device, np_dtype=np.float64):
         t = torch.from_numpy(v).to(device)
         if reps > 1:
             t = t.repeat((reps,) + (1,) * (t.dim() - 1))
-        dt[k] = t[:batch].contiguous()
+        t = t[:batch]
+        if stage_major and k != "x0":  # [batch][stage][...] -> [stage][batch][...]
+            t = t.transpose(0, 1)
+        dt[k] = t.contiguous()
     return dt
 
 
@@ -131,6 +134,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--layout", choices=("qp", "stage"), default="qp",
+                    help="input layout handed to the solver (stage: [stage][batch][block], "
+                         "unconstrained workloads only)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip the on-device SQP-iteration measurement (linearise + solve + line search)")
     args = ap.parse_args()
@@ -157,10 +163,14 @@ def main():
     log(f"[rank {rank}] workload={args.workload} batch/rank={batch} N={N} world={world}")
     t0 = time.perf_counter()
     qp, x0 = make_shard(pkg, N, constraints, batch, rank, args.seed, args.pool)
-    dt = to_device(pkg, qp, x0, batch, device, np_dtype)
+    stage_major = args.layout == "stage"
+    if stage_major and constraints != "none":
+        raise SystemExit("--layout stage: unconstrained workloads only")
+    dt = to_device(pkg, qp, x0, batch, device, np_dtype, stage_major)
     log(f"[rank {rank}] generated + uploaded in {time.perf_counter() - t0:.1f}s")
 
-    h = capi.Handle(N, 12, 12, qp.ng, qp.has_box_u, qp.has_box_x, capacity=batch, device=local_rank)
+    h = capi.Handle(N, 12, 12, qp.ng, qp.has_box_u, qp.has_box_x, capacity=batch, device=local_rank,
+                    layout=1 if stage_major else 0)
     f64 = dict(dtype=torch.float32 if dtype == "f32" else torch.float64, device=device)
     sol_t = {"x": torch.zeros(batch, N + 1, 12, **f64), "u": torch.zeros(batch, N, 12, **f64),
              "pi": torch.zeros(batch, N + 1, 12, **f64),
@@ -202,7 +212,7 @@ def main():
 
     # ---- the whole SQP iteration on the device (secondary; not `value`) ----
     pipeline = None
-    if not args.no_pipeline and dtype == "f64":
+    if not args.no_pipeline and dtype == "f64" and not stage_major:
         pipeline = sqp_pipeline(pkg, h, N, constraints, batch, args.seed, args.pool, rank, device, settings)
 
     # ---- solution gather to rank 0 over RCCL (BASELINE config 4) ----
@@ -255,6 +265,7 @@ def main():
         "config": {"workload": args.workload, "description": desc, "batch_per_gpu": batch,
                    "global_batch": total_qps, "N": N, "nx": 12, "nu": 12, "constraints": constraints,
                    "parallelism": f"dp{world} (independent QP shards)",
+                   "input_layout": "stage-major" if stage_major else "qp-major",
                    "settings": ("NMPC_solver.cpp:70-82 (Speed, iter_max 30, split_step) with fp32 "
                                 "tolerances stat 3e-2 / 1e-3" if dtype == "f32" else
                                 "NMPC_solver.cpp:70-82 (Speed, iter_max 30, tol 1e-4, split_step)")},

@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SRBD_QP_ABI_VERSION 5
+#define SRBD_QP_ABI_VERSION 6
 #define SRBD_QP_MAX_NX 12
 #define SRBD_QP_MAX_NU 12
 #define SRBD_QP_MAX_NG 64
@@ -105,7 +105,16 @@ typedef struct srbd_qp_dims {
   int ng;         /* general constraints per stage (0 = none)                */
   int has_box_u;  /* 1 if lbu/ubu will be passed                             */
   int has_box_x;  /* 1 if lbx/ubx will be passed                             */
+  int layout;     /* SRBD_QP_LAYOUT_QP_MAJOR (0, default) or _STAGE_MAJOR (1) */
 } srbd_qp_dims;
+
+/* Input layouts.  QP-major: every array [batch][stage][block] (Eigen order,
+ * what the hpipm-cpp shim packs).  Stage-major: [stage][batch][block], so the
+ * QPs of one wavefront are adjacent in HBM (longer contiguous streams); the
+ * unconstrained solve reads it (the IPM and the linearisation write / read
+ * QP-major only for now: srbd_qp_create rejects stage-major with
+ * constraints).  Outputs are always QP-major.                              */
+enum { SRBD_QP_LAYOUT_QP_MAJOR = 0, SRBD_QP_LAYOUT_STAGE_MAJOR = 1 };
 
 /* hpipm::OcpQpIpmSolverSettings (ocp_qp_ipm_solver_settings.hpp:26-86);
  * srbd_qp_default_settings() gives the same defaults.                     */

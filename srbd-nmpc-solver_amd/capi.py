@@ -27,7 +27,7 @@ class SrbdQpError(RuntimeError):
 
 class Dims(C.Structure):
     _fields_ = [("N", C.c_int), ("nx", C.c_int), ("nu", C.c_int), ("ng", C.c_int),
-                ("has_box_u", C.c_int), ("has_box_x", C.c_int)]
+                ("has_box_u", C.c_int), ("has_box_x", C.c_int), ("layout", C.c_int)]
 
 
 class Settings(C.Structure):
@@ -183,8 +183,8 @@ class Handle:
     """Owns a srbd_qp_handle (device workspace + stream) for fixed dims."""
 
     def __init__(self, N: int, nx: int, nu: int, ng: int = 0, has_box_u: bool = False,
-                 has_box_x: bool = False, capacity: int = 1, device: int = 0):
-        self.dims = Dims(N, nx, nu, ng, int(has_box_u), int(has_box_x))
+                 has_box_x: bool = False, capacity: int = 1, device: int = 0, layout: int = 0):
+        self.dims = Dims(N, nx, nu, ng, int(has_box_u), int(has_box_x), int(layout))
         self.capacity = int(capacity)
         self.device = int(device)
         h = C.c_void_p()

@@ -3,6 +3,9 @@
 // generates its d_ and s_ solvers from one source.  No include guard: included twice.
 // The kernel code is documented in ipm_box.hip.
 
+#ifndef SRBD_RES_FENCE
+#define SRBD_RES_FENCE() SRBD_PHASE_FENCE()
+#endif
 namespace srbd {
 namespace SRBD_NS {
 
@@ -742,31 +745,31 @@ __global__ void __launch_bounds__(256, 2) ipm_phase_kernel(ProblemArgsT<real> a)
             c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, M);
             ru = dot12(M, buk, real(0.0));
           }
-          SRBD_PHASE_FENCE();
+          SRBD_RES_FENCE();
           {
             real M[12];
             c.row(c.S() + (size_t)k * c.nxu(), nu, nx, li, uel, M);
             sx_ = dot12(M, bxk, real(0.0));
           }
-          SRBD_PHASE_FENCE();
+          SRBD_RES_FENCE();
           {
             real M[12];
             c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, M);
             stu = dot12(M, buk, real(0.0));
           }
-          SRBD_PHASE_FENCE();
+          SRBD_RES_FENCE();
           {
             real M[12];
             c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, M);
             btp = dot12(M, bpn, real(0.0));
           }
-          SRBD_PHASE_FENCE();
+          SRBD_RES_FENCE();
           {
             real M[12];
             c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, M);
             atp = dot12(M, bpn, real(0.0));
           }
-          SRBD_PHASE_FENCE();
+          SRBD_RES_FENCE();
           const real rk = c.el(c.r() + (size_t)k * nu, nu, li);
           rgu = ru + sx_ + rk + btp;
           rgx += stu + atp;
@@ -778,13 +781,13 @@ __global__ void __launch_bounds__(256, 2) ipm_phase_kernel(ProblemArgsT<real> a)
             c.row(c.A() + (size_t)k * c.nxx(), nx, nx, li, xel, M);
             ax = dot12(M, bxk, real(0.0));
           }
-          SRBD_PHASE_FENCE();
+          SRBD_RES_FENCE();
           {
             real M[12];
             c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, M);
             ax = dot12(M, buk, ax);
           }
-          SRBD_PHASE_FENCE();
+          SRBD_RES_FENCE();
           rb = ax + c.el(c.b() + (size_t)k * nx, nx, li) - xn;
         }
         if constexpr (GEN) {

@@ -25,6 +25,7 @@ constexpr int kWsStage = 402;  // doubles per stage record (16-byte multiple)
 template <typename T>
 struct ProblemArgsT {
   int batch, N, nx, nu, ng;
+  int layout;  // 0: QP-major inputs, 1: stage-major (srbd_qp_dims.layout)
   // QP data (device)
   const T *A, *B, *b, *Q, *S, *R, *q, *r, *x0;
   const T *lbu, *ubu, *lbu_mask, *ubu_mask;

@@ -1,6 +1,12 @@
 // riccati_unconstr_impl.h -- body of the unconstrained batched solve, instantiated
 // per precision by riccati_unconstr.hip (SRBD_REAL, SRBD_NS).  No include guard.
 
+#ifndef SRBD_EARLY_LOADS
+#define SRBD_EARLY_LOADS 0
+#endif
+#ifndef SRBD_NT_INPUTS
+#define SRBD_NT_INPUTS 0
+#endif
 namespace srbd {
 namespace SRBD_NS {
 
@@ -22,7 +28,16 @@ struct StageLoader {
   __device__ __forceinline__ void col(const real* blk, int rows, int ld, int c, bool ok,
                                       real (&v)[12]) const {
     if constexpr (FULL) {
+#if SRBD_NT_INPUTS
+      // streamed once: non-temporal, so the records keep the caches
+      const real* q = blk + c * 12;
+      sfor<0, 12>([&](auto i) {
+        constexpr int I = decltype(i)::value;
+        v[I] = __builtin_nontemporal_load(q + I);
+      });
+#else
       load12(blk + c * 12, v);
+#endif
     } else {
       load_col_pad(blk + (size_t)c * ld, rows, ok, v);
     }
@@ -48,14 +63,12 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgsT<real
 #else
   const int qin = qp;
 #endif
-  const real* Aq = a.A + (size_t)qin * N * nxx;
-  const real* Bq = a.B + (size_t)qin * N * nxu;
-  const real* bq = a.b + (size_t)qin * N * nx;
-  const real* Qq = a.Q + (size_t)qin * (N + 1) * nxx;
-  const real* Sq = a.S + (size_t)qin * N * nxu;
-  const real* Rq = a.R + (size_t)qin * N * nuu;
-  const real* qq = a.q + (size_t)qin * (N + 1) * nx;
-  const real* rq = a.r + (size_t)qin * N * nu;
+  // input block of stage k: QP-major ([batch][stage][blk], Eigen order) or
+  // stage-major ([stage][batch][blk]: a wavefront's QPs adjacent in memory)
+  const bool smaj = a.layout == 1;
+  auto at = [&](const real* base, int nstage, size_t blk, int k) -> const real* {
+    return smaj ? base + ((size_t)k * a.batch + qin) * blk : base + ((size_t)qin * nstage + k) * blk;
+  };
   // forward records, stage-major: stage k of QP q at ws[(k * batch + q) * kWsStage], so the
   // four QPs of a wavefront write / read one contiguous 15 KB block per stage
   auto rec_at = [&](int k) -> real* {
@@ -73,9 +86,9 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgsT<real
   // ---------------- terminal stage: P_N = Q_N, p_N = q_N ----------------
   real P[12];
   if (isv) {
-    ld.col(qq + (size_t)N * nx, nx, nx, 0, true, P);
+    ld.col(at(a.q, N + 1, nx, N), nx, nx, 0, true, P);
   } else {
-    ld.col(Qq + (size_t)N * nxx, nx, nx, col, xcol, P);
+    ld.col(at(a.Q, N + 1, nxx, N), nx, nx, col, xcol, P);
   }
   {
     real* rec = rec_at(N);
@@ -90,17 +103,17 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgsT<real
   for (int k = N - 1; k >= 0; --k) {
     real A_[12], B_[12];
     if (isv) {
-      ld.col(bq + (size_t)k * nx, nx, nx, 0, true, A_);
+      ld.col(at(a.b, N, nx, k), nx, nx, 0, true, A_);
       sfor<0, 12>([&](auto i) { B_[decltype(i)::value] = real(0.0); });
     } else {
-      ld.col(Aq + (size_t)k * nxx, nx, nx, col, xcol, A_);
-      ld.col(Bq + (size_t)k * nxu, nx, nx, col, ucol, B_);
+      ld.col(at(a.A, N, nxx, k), nx, nx, col, xcol, A_);
+      ld.col(at(a.B, N, nxu, k), nx, nx, col, ucol, B_);
     }
     auto loadR = [&](real (&Rc)[12]) {
       if (isv) {
         sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = real(0.0); });
       } else {
-        ld.col(Rq + (size_t)k * nuu, nu, nu, col, ucol, Rc);
+        ld.col(at(a.R, N, nuu, k), nu, nu, col, ucol, Rc);
         if constexpr (!FULL) {
           // padded inputs: R = 1 on the diagonal keeps G positive definite
           sfor<0, 12>([&](auto i) {
@@ -112,15 +125,35 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgsT<real
     };
     auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
       if (isv) {
-        ld.col(rq + (size_t)k * nu, nu, nu, 0, true, Sc);
-        ld.col(qq + (size_t)k * nx, nx, nx, 0, true, Qc);
+        ld.col(at(a.r, N, nu, k), nu, nu, 0, true, Sc);
+        ld.col(at(a.q, N + 1, nx, k), nx, nx, 0, true, Qc);
       } else {
-        ld.col(Sq + (size_t)k * nxu, nu, nu, col, xcol, Sc);
-        ld.col(Qq + (size_t)k * nxx, nx, nx, col, xcol, Qc);
+        ld.col(at(a.S, N, nxu, k), nu, nu, col, xcol, Sc);
+        ld.col(at(a.Q, N + 1, nxx, k), nx, nx, col, xcol, Qc);
       }
     };
     StageFactor<real> f;
+#if SRBD_EARLY_LOADS
+    // all five blocks of the stage requested up front: one memory latency per
+    // stage instead of three (R, then S/Q, behind the phase fences)
+    real Re[12], Se[12], Qe[12];
+    loadR(Re);
+    loadSQ(Se, Qe);
+    riccati_step(
+        P, A_, B_,
+        [&](real (&Rc)[12]) {
+          sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = Re[decltype(i)::value]; });
+        },
+        [&](real (&Sc)[12], real (&Qc)[12]) {
+          sfor<0, 12>([&](auto i) {
+            Sc[decltype(i)::value] = Se[decltype(i)::value];
+            Qc[decltype(i)::value] = Qe[decltype(i)::value];
+          });
+        },
+        lane, reg, f);
+#else
     riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
+#endif
 
     real* rec = rec_at(k);
 #ifdef SRBD_DIAG_NO_RECORD  // diagnostic build only: no record traffic

@@ -108,6 +108,10 @@ int srbd_qp_check_settings(const srbd_qp_settings* s) {
 
 static int check_dims(const srbd_qp_dims* d) {
   if (!d) return fail(SRBD_QP_EINVAL, "dims is NULL");
+  if (d->layout != SRBD_QP_LAYOUT_QP_MAJOR && d->layout != SRBD_QP_LAYOUT_STAGE_MAJOR)
+    return fail(SRBD_QP_EINVAL, "unknown layout " + std::to_string(d->layout));
+  if (d->layout == SRBD_QP_LAYOUT_STAGE_MAJOR && (d->has_box_u || d->has_box_x || d->ng > 0))
+    return fail(SRBD_QP_EINVAL, "stage-major inputs are supported by the unconstrained solve only");
   if (d->N < 1 || d->N > 1024)
     return fail(SRBD_QP_EDIM, "N must be in [1, 1024], got " + std::to_string(d->N));
   if (d->nx < 1 || d->nx > SRBD_QP_MAX_NX)
@@ -221,6 +225,7 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   a.nx = h->dims.nx;
   a.nu = h->dims.nu;
   a.ng = h->dims.ng;
+  a.layout = h->dims.layout;
   a.A = d->A; a.B = d->B; a.b = d->b; a.Q = d->Q; a.S = d->S; a.R = d->R; a.q = d->q; a.r = d->r;
   a.x0 = d->x0;
   a.lbu = d->lbu; a.ubu = d->ubu; a.lbu_mask = d->lbu_mask; a.ubu_mask = d->ubu_mask;

@@ -109,7 +109,7 @@ struct OcpQpIpmSolver::Impl {
   void ensure_handle(const Shape& s, int batch) {
     if (handle && s == shape && batch <= capacity) return;
     release();
-    srbd_qp_dims d{s.N, s.nx, s.nu, s.ng, s.box_u ? 1 : 0, s.box_x ? 1 : 0};
+    srbd_qp_dims d{s.N, s.nx, s.nu, s.ng, s.box_u ? 1 : 0, s.box_x ? 1 : 0, SRBD_QP_LAYOUT_QP_MAJOR};
     if (srbd_qp_create(&d, std::max(batch, 1), device, &handle) != SRBD_QP_OK) {
       handle = nullptr;
       abi_error("OcpQpIpmSolver::resize");

@@ -116,3 +116,21 @@ def test_srbd_qps_vs_oracle(pkg, oracle):
     for key in ("x", "u", "pi", "P", "K"):
         for i in range(qp.batch):
             assert helpers.is_approx(out[key][i], ref[key][i], 1e-9), (key, i)
+
+
+def test_stage_major_layout_identical(pkg):
+    """SRBD_QP_LAYOUT_STAGE_MAJOR inputs ([stage][batch][block]) give bit-identical
+    results to the QP-major (Eigen-order) inputs."""
+    import torch
+    qp, x0 = pkg.srbd_model.generate_batch(40, N=20, seed=31, constraints="none")
+    ref = pkg.capi.solve(qp, x0)
+    h = pkg.capi.Handle(qp.N, 12, 12, 0, False, False, capacity=qp.batch, layout=1)
+    dt, st, data, sol = pkg.capi.device_buffers(qp, x0)
+    keep = {}
+    for k in ("A", "B", "b", "Q", "S", "R", "q", "r"):
+        keep[k] = dt[k].transpose(0, 1).contiguous()
+        setattr(data, k, keep[k].data_ptr())
+    h.solve_device(qp.batch, pkg.capi.settings_struct(None), data, sol)
+    h.synchronize()
+    for k in ("x", "u", "pi"):
+        np.testing.assert_array_equal(st[k].cpu().numpy(), ref[k])
