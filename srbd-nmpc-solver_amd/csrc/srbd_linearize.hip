@@ -16,6 +16,10 @@
 
 #include <hip/hip_runtime.h>
 
+#ifndef SRBD_LIN_PER_STAGE_THREAD
+#define SRBD_LIN_PER_STAGE_THREAD 0
+#endif
+
 namespace srbd {
 namespace {
 
@@ -194,6 +198,29 @@ struct Model {
       jfu[(6 + i) * 12 + (9 + i)] = 1.0 / p.mass;
     }
   }
+  // Jacobian blocks of f (the nonzero 3x3 blocks of jfx / jfu, :104-176):
+  // jfx[0:3,0:3] = J00, jfx[0:3,3:6] = J01, jfx[3:6,6:9] = [f0 + f1]x,
+  // jfx[6:9,9:12] = I; jfu[3:6,0:3] = [p0]x, jfu[3:6,6:9] = [p1]x,
+  // jfu[3:6,3:6] = jfu[3:6,9:12] = I, jfu[9:12,0:3] = jfu[9:12,6:9] = I / m
+  __device__ void jac_blocks(const double* x, const double* u, M3& J00, M3& J01, M3& Sf, M3& S0,
+                             M3& S1) const {
+    const V3 r = seg(x, 0), l = seg(x, 3), pos = seg(x, 6);
+    const M3 R = expm(r), Jlt = jlt(r);
+    M3 Lb = zero3();
+    for (int i = 0; i < 3; ++i) Lb.a[i][i] = 1.0 / p.Lbody[i];
+    const M3 RLR = mul(mul(R, Lb), tr(R));
+    const V3 w = mv(RLR, l);
+    const M3 mid = mul(mul(Jlt, add(mul(RLR, skew(l)), lin(-1.0, skew(w), 0.0, Lb))), jl(r));
+    for (int a = 0; a < 3; ++a) {
+      const M3 dJ = lin(-1.0, mul(mul(Jlt, djl(r, a)), Jlt), 0.0, Jlt);
+      const V3 col = mv(dJ, w);
+      for (int i = 0; i < 3; ++i) J00.a[i][a] = col.v[i] + mid.a[i][a];
+    }
+    J01 = mul(Jlt, RLR);
+    Sf = skew(V3{{u[0] + u[6], u[1] + u[7], u[2] + u[8]}});
+    S0 = skew(V3{{p.foot_r[0] - pos.v[0], p.foot_r[1] - pos.v[1], p.foot_r[2] - pos.v[2]}});
+    S1 = skew(V3{{p.foot_l[0] - pos.v[0], p.foot_l[1] - pos.v[1], p.foot_l[2] - pos.v[2]}});
+  }
   // relaxed log barrier (Barrier, :262-295): db, ddb
   __device__ void barrier(double v, double& db, double& ddb) const {
     if (v > p.theta_b) {
@@ -306,6 +333,187 @@ __global__ void __launch_bounds__(64) srbd_linearize_kernel(Model m, LinArgs a) 
     for (int j = 0; j < 12; ++j)
       for (int c = 0; c < 24; ++c) D[j * 24 + c] = m.ac(c, j);
     const size_t o = ((size_t)qp * (N + 1) + k) * 24;
+    for (int c = 0; c < 24; ++c) {
+      const_cast<double*>(a.out.lg)[o + c] = -fc[c];
+      const_cast<double*>(a.out.ug)[o + c] = 1e10;
+      const_cast<double*>(a.out.lg_mask)[o + c] = 1.0;
+      const_cast<double*>(a.out.ug_mask)[o + c] = 0.0;
+    }
+  }
+}
+
+// Per-stage thread, written for the compute it does: the Jacobians come as
+// their 3x3 blocks and every output element is stored once (no read-modify-
+// write of global memory); the friction-cone rows have two nonzeros each, so
+// fc, r and the barrier Hessian Ac' diag(ddb) Ac are formed from that sparsity
+// (a leg's R block has 10 distinct nonzeros) instead of dense 24 x 12 loops.
+__global__ void __launch_bounds__(64) srbd_linearize_fast_kernel(Model m, LinArgs a) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = a.N;
+  if (t >= (long long)a.batch * (N + 1)) return;
+  const int qp = (int)(t / (N + 1)), k = (int)(t % (N + 1));
+  const srbd_model_params& p = m.p;
+  double* Q = const_cast<double*>(a.out.Q) + ((size_t)qp * (N + 1) + k) * 144;
+  double* q = const_cast<double*>(a.out.q) + ((size_t)qp * (N + 1) + k) * 12;
+  const double* x = a.xs + ((size_t)qp * (N + 1) + k) * 12;
+  const double* wdiag = k < N ? p.Q : p.Qf;
+  const double sc = k < N ? 1.0 : a.qf_scale;
+#pragma unroll
+  for (int j = 0; j < 12; ++j)
+#pragma unroll
+    for (int i = 0; i < 12; ++i) Q[j * 12 + i] = i == j ? sc * wdiag[i] : 0.0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) q[i] = sc * wdiag[i] * (x[i] - p.x_ref[i]);
+  if (a.mode == 2) {
+    double* C = const_cast<double*>(a.out.C) + ((size_t)qp * (N + 1) + k) * 24 * 12;
+    for (int i = 0; i < 24 * 12; ++i) C[i] = 0.0;
+  }
+  if (k == N) {
+    if (a.mode == 2) {
+      const size_t o = ((size_t)qp * (N + 1) + N) * 24;
+      for (int c = 0; c < 24; ++c) {
+        const_cast<double*>(a.out.lg)[o + c] = 0.0;
+        const_cast<double*>(a.out.ug)[o + c] = 1e10;
+        const_cast<double*>(a.out.lg_mask)[o + c] = 0.0;
+        const_cast<double*>(a.out.ug_mask)[o + c] = 0.0;
+      }
+    }
+    return;
+  }
+  const double* u = a.us + ((size_t)qp * N + k) * 12;
+  const double* xn = a.xs + ((size_t)qp * (N + 1) + k + 1) * 12;
+  const double dt = p.dt;
+  // ---- b = RK4(x, u) - x_next ----
+  {
+    double k1[12], k2[12], k3[12], k4[12], xt[12];
+    m.f(x, u, k1, nullptr, nullptr);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) xt[i] = x[i] + 0.5 * dt * k1[i];
+    m.f(xt, u, k2, nullptr, nullptr);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) xt[i] = x[i] + 0.5 * dt * k2[i];
+    m.f(xt, u, k3, nullptr, nullptr);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) xt[i] = x[i] + dt * k3[i];
+    m.f(xt, u, k4, nullptr, nullptr);
+    double* b = const_cast<double*>(a.out.b) + ((size_t)qp * N + k) * 12;
+#pragma unroll
+    for (int i = 0; i < 12; ++i)
+      b[i] = (x[i] + (dt / 6.0) * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i])) - xn[i];
+  }
+  // ---- A = I + dt jfx, B = dt jfu from the 3x3 blocks, one store per element ----
+  {
+    M3 J00, J01, Sf, S0, S1;
+    m.jac_blocks(x, u, J00, J01, Sf, S0, S1);
+    double* A = const_cast<double*>(a.out.A) + ((size_t)qp * N + k) * 144;
+    double* B = const_cast<double*>(a.out.B) + ((size_t)qp * N + k) * 144;
+    const double im = 1.0 / p.mass;
+#pragma unroll
+    for (int j = 0; j < 12; ++j)
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        double jf = 0.0;
+        if (i < 3 && j < 3) jf = J00.a[i][j];
+        else if (i < 3 && j < 6) jf = J01.a[i][j - 3];
+        else if (i >= 3 && i < 6 && j >= 6 && j < 9) jf = Sf.a[i - 3][j - 6];
+        else if (i >= 6 && i < 9 && j == i + 3) jf = 1.0;
+        A[j * 12 + i] = (i == j ? 1.0 : 0.0) + dt * jf;
+        double ju = 0.0;
+        if (i >= 3 && i < 6) {
+          if (j < 3) ju = S0.a[i - 3][j];
+          else if (j < 6) ju = (j == i) ? 1.0 : 0.0;
+          else if (j < 9) ju = S1.a[i - 3][j - 6];
+          else ju = (j - 9 == i - 3) ? 1.0 : 0.0;
+        } else if (i >= 9) {
+          if (j == i - 9 || j == i - 3) ju = im;
+        }
+        B[j * 12 + i] = dt * ju;
+      }
+  }
+  // ---- friction cone (two nonzeros per row) as a barrier in the cost ----
+  double Rm[12][12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j)
+#pragma unroll
+    for (int i = 0; i < 12; ++i) Rm[j][i] = i == j ? p.R : 0.0;
+  double rv[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) rv[i] = p.R * u[i];
+  double fc[24];
+#pragma unroll
+  for (int leg = 0; leg < 2; ++leg) {
+    const int o = 6 * leg;
+    const double fx = u[o], fy = u[o + 1], fz = u[o + 2], tx = u[o + 3], ty = u[o + 4], tz = u[o + 5];
+    const double mu = p.mu, Lx = p.Lfx, Lz = p.Lfz;
+    double v[12], db[12], ddb[12];
+    v[0] = -fx + mu * fz;
+    v[1] = -fy + mu * fz;
+    v[2] = fx + mu * fz;
+    v[3] = fy + mu * fz;
+    v[4] = -fz + p.fmax;
+    v[5] = fz - p.fmin;
+    v[6] = Lx * fz - ty;
+    v[7] = Lx * fz + ty;
+    v[8] = Lz * fz - tz;
+    v[9] = Lz * fz + tz;
+    v[10] = -tx;
+    v[11] = tx;
+#pragma unroll
+    for (int c = 0; c < 12; ++c) {
+      m.barrier(v[c], db[c], ddb[c]);
+      fc[12 * leg + c] = v[c];
+    }
+    rv[o + 0] += -db[0] + db[2];
+    rv[o + 1] += -db[1] + db[3];
+    rv[o + 2] += mu * (db[0] + db[1] + db[2] + db[3]) - db[4] + db[5] + Lx * (db[6] + db[7]) +
+                 Lz * (db[8] + db[9]);
+    rv[o + 3] += -db[10] + db[11];
+    rv[o + 4] += -db[6] + db[7];
+    rv[o + 5] += -db[8] + db[9];
+    Rm[o + 0][o + 0] += ddb[0] + ddb[2];
+    Rm[o + 1][o + 1] += ddb[1] + ddb[3];
+    Rm[o + 2][o + 2] += mu * mu * (ddb[0] + ddb[1] + ddb[2] + ddb[3]) + ddb[4] + ddb[5] +
+                        Lx * Lx * (ddb[6] + ddb[7]) + Lz * Lz * (ddb[8] + ddb[9]);
+    Rm[o + 3][o + 3] += ddb[10] + ddb[11];
+    Rm[o + 4][o + 4] += ddb[6] + ddb[7];
+    Rm[o + 5][o + 5] += ddb[8] + ddb[9];
+    const double r02 = mu * (ddb[2] - ddb[0]), r12 = mu * (ddb[3] - ddb[1]);
+    const double r24 = Lx * (ddb[7] - ddb[6]), r25 = Lz * (ddb[9] - ddb[8]);
+    Rm[o + 2][o + 0] += r02;
+    Rm[o + 0][o + 2] += r02;
+    Rm[o + 2][o + 1] += r12;
+    Rm[o + 1][o + 2] += r12;
+    Rm[o + 4][o + 2] += r24;
+    Rm[o + 2][o + 4] += r24;
+    Rm[o + 5][o + 2] += r25;
+    Rm[o + 2][o + 5] += r25;
+  }
+  double* R = const_cast<double*>(a.out.R) + ((size_t)qp * N + k) * 144;
+  double* rr = const_cast<double*>(a.out.r) + ((size_t)qp * N + k) * 12;
+  double* S = const_cast<double*>(a.out.S) + ((size_t)qp * N + k) * 144;
+#pragma unroll
+  for (int j = 0; j < 12; ++j)
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      R[j * 12 + i] = Rm[j][i];
+      S[j * 12 + i] = 0.0;
+    }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) rr[i] = rv[i];
+  if (a.mode == 1) {
+    double* lbu = const_cast<double*>(a.out.lbu) + ((size_t)qp * N + k) * 12;
+    double* ubu = const_cast<double*>(a.out.ubu) + ((size_t)qp * N + k) * 12;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      lbu[i] = p.u_lo[i] - u[i];
+      ubu[i] = p.u_hi[i] - u[i];
+    }
+  } else if (a.mode == 2) {
+    double* D = const_cast<double*>(a.out.D) + ((size_t)qp * N + k) * 24 * 12;
+    for (int j = 0; j < 12; ++j)
+      for (int c = 0; c < 24; ++c) D[j * 24 + c] = m.ac(c, j);
+    const size_t o = ((size_t)qp * (N + 1) + k) * 24;
+#pragma unroll
     for (int c = 0; c < 24; ++c) {
       const_cast<double*>(a.out.lg)[o + c] = -fc[c];
       const_cast<double*>(a.out.ug)[o + c] = 1e10;
@@ -480,10 +688,17 @@ hipError_t launch_srbd_linearize(const srbd_model_params& p, int batch, int N, i
   if (batch <= 0) return hipSuccess;
   Model m{p};
   LinArgs a{batch, N, mode, xs, us, out, p.qf_scale};
+#if SRBD_LIN_PER_STAGE_THREAD
   const long long n = (long long)batch * (N + 1);
   const int threads = 64;
   hipLaunchKernelGGL(srbd_linearize_kernel, dim3((unsigned)((n + threads - 1) / threads)),
                      dim3(threads), 0, stream, m, a);
+#else
+  const long long n = (long long)batch * (N + 1);
+  const int threads = 64;
+  hipLaunchKernelGGL(srbd_linearize_fast_kernel, dim3((unsigned)((n + threads - 1) / threads)),
+                     dim3(threads), 0, stream, m, a);
+#endif
   return hipGetLastError();
 }
 
