@@ -137,6 +137,8 @@ def main():
     ap.add_argument("--layout", choices=("qp", "stage"), default="qp",
                     help="input layout handed to the solver (stage: [stage][batch][block], "
                          "unconstrained workloads only)")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip the on-device SQP-iteration measurement (linearise + solve + line search)")
     args = ap.parse_args()
@@ -215,6 +217,11 @@ def main():
     if not args.no_pipeline and dtype == "f64" and not stage_major:
         pipeline = sqp_pipeline(pkg, h, N, constraints, batch, args.seed, args.pool, rank, device, settings)
 
+    # ---- host buffers in, host buffers out (secondary; PCIe-inclusive, not `value`) ----
+    host = None
+    if not args.no_host_path and not stage_major and rank == 0:
+        host = host_path(capi, h, dt, batch, N, settings, dtype)
+
     # ---- solution gather to rank 0 over RCCL (BASELINE config 4) ----
     gather_ms = None
     if distributed and not args.no_gather:
@@ -279,6 +286,8 @@ def main():
     }
     if pipeline is not None:
         line["sqp_pipeline"] = pipeline
+    if host is not None:
+        line["host_buffers"] = host
     if gather_ms is not None:
         line["gather"] = {"ms": gather_ms, "bytes_per_rank": batch * (2 * (N + 1) * 12 + N * 12) * 8,
                           "value_with_gather": total_qps / (t_max / args.steps + gather_ms * 1e-3)}
@@ -286,6 +295,32 @@ def main():
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def host_path(capi, h, dt, batch, N, settings, dtype, max_batch=16384, reps=2):
+    """srbd_qp_solve_host_*: the caller hands over pageable host buffers (the
+    hpipm-cpp shim's situation, ocp_qp_ipm_solver.cpp:181-414); the library
+    stages them H2D, solves and copies x, u, pi, status, iter back.  Timed on
+    min(batch, max_batch) QPs after one warm call."""
+    import torch
+    nb = min(batch, max_batch)
+    host = {k: (None if v is None else np.ascontiguousarray(v[:nb].cpu().numpy())) for k, v in dt.items()}
+    npt = np.float32 if dtype == "f32" else np.float64
+    out = {"x": np.zeros((nb, N + 1, 12), npt), "u": np.zeros((nb, N, 12), npt),
+           "pi": np.zeros((nb, N + 1, 12), npt), "status": np.zeros(nb, np.int32),
+           "iter": np.zeros(nb, np.int32)}
+    DataT, SolT = (capi.Data32, capi.Solution32) if dtype == "f32" else (capi.Data, capi.Solution)
+    data = DataT(**{k: (None if host.get(k) is None else host[k].ctypes.data) for k in capi.DATA_FIELDS})
+    sol = SolT(**{k: (out[k].ctypes.data if k in out else None) for k in capi.SOL_FIELDS})
+    h.solve_host(nb, settings, data, sol)
+    t = time.perf_counter()
+    for _ in range(reps):
+        h.solve_host(nb, settings, data, sol)
+    ms = (time.perf_counter() - t) / reps * 1e3
+    nbytes = sum(v.nbytes for v in host.values() if v is not None) + sum(v.nbytes for v in out.values())
+    return {"what": "srbd_qp_solve_host: pageable host buffers -> H2D -> solve -> D2H (PCIe-inclusive)",
+            "batch": nb, "ms_per_call": ms, "qps_per_s": nb / (ms * 1e-3),
+            "host_bytes_moved": nbytes, "status_ok": float((out["status"] == 0).mean())}
 
 
 def sqp_pipeline(pkg, h, N, constraints, batch, seed, pool, rank, device, settings, iters=3):
@@ -380,18 +415,18 @@ def cpu_baseline(pkg, qp, x0, settings, budget_s):
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
     threads = max(1, min(threads, avail, 64))
-    cal = qp.subset(slice(0, min(qp.batch, 4 * threads)))
+    # calibrate on a slice big enough that thread start-up does not dominate,
+    # then repeat the slice until the budget is spent
+    cal = qp.subset(slice(0, min(qp.batch, 64 * threads)))
     _, dt = oracle.solve_batch_threaded(cal, settings, x0[:cal.batch], threads)
     rate = cal.batch / max(dt, 1e-9)
-    n = int(min(qp.batch, max(cal.batch, rate * budget_s)))
-    reps = 1
+    n = int(min(qp.batch, max(cal.batch, rate * budget_s / 4)))
     sample = qp.subset(slice(0, n))
-    if n == qp.batch and rate * budget_s > n:
-        reps = max(1, int(rate * budget_s / n))
-    t = 0.0
-    for _ in range(reps):
+    t, reps = 0.0, 0
+    while t < budget_s:
         _, d = oracle.solve_batch_threaded(sample, settings, x0[:n], threads)
         t += d
+        reps += 1
     return {"value": n * reps / t, "unit": "QP solves/s", "cores": threads, "kind": "port",
             "sample": f"{n} QPs x {reps} reps of the same workload ({t:.1f} s, {threads} threads, "
                       f"oracle/ocp_qp_oracle.c)"}

@@ -3,6 +3,9 @@
 // generates its d_ and s_ solvers from one source.  No include guard: included twice.
 // The kernel code is documented in ipm_box.hip.
 
+#ifndef SRBD_IPM_FUSE
+#define SRBD_IPM_FUSE 1
+#endif
 #ifndef SRBD_RES_FENCE
 #define SRBD_RES_FENCE() SRBD_PHASE_FENCE()
 #endif
@@ -335,7 +338,7 @@ __device__ __forceinline__ void gather12(real v, real (&out)[12]) {
 }
 
 template <bool FULL, bool GEN, int PH>
-__global__ void __launch_bounds__(256, 2) ipm_phase_kernel(ProblemArgsT<real> a) {
+__device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int qp = gid >> 4;
   const int lane = threadIdx.x & (kGroup - 1);
@@ -1257,6 +1260,23 @@ __global__ void __launch_bounds__(256, 2) ipm_phase_kernel(ProblemArgsT<real> a)
 }
 
 
+template <bool FULL, bool GEN, int PH>
+__global__ void __launch_bounds__(256, 2) ipm_phase_kernel(ProblemArgsT<real> a) {
+  ipm_phase<FULL, GEN, PH>(a);
+}
+
+// Two consecutive sweeps of one iteration in one launch (RB -> F1, B2 -> F2):
+// the forward sweep starts on the stages the backward sweep touched last, while
+// their records are still in L2 / the Infinity Cache, and the launch count halves.
+// The second phase re-reads the per-QP state the first one wrote (same wave:
+// visible after the workgroup-scope fence).
+template <bool FULL, bool GEN, int PH1, int PH2>
+__global__ void __launch_bounds__(256, 2) ipm_phase2_kernel(ProblemArgsT<real> a) {
+  ipm_phase<FULL, GEN, PH1>(a);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  ipm_phase<FULL, GEN, PH2>(a);
+}
+
 template <bool FULL, bool GEN>
 static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream) {
   const int threads = 256;
@@ -1267,6 +1287,17 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
   // at the top of every later launch.  iter_max + 1 factorization sweeps at
   // most: the last one always decides (converged or MaxIterReached).
   hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhInit>), grid, block, 0, stream, a);
+#if SRBD_IPM_FUSE
+  for (int it = 0;; ++it) {
+    if (it >= a.iter_max) {
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB>), grid, block, 0, stream, a);
+      break;
+    }
+    hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1>), grid, block, 0, stream, a);
+    if (a.pred_corr)
+      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhB2, kPhF2>), grid, block, 0, stream, a);
+  }
+#else
   for (int it = 0;; ++it) {
     hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB>), grid, block, 0, stream, a);
     if (it >= a.iter_max) break;
@@ -1276,6 +1307,7 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
       hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF2>), grid, block, 0, stream, a);
     }
   }
+#endif
   hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut>), grid, block, 0, stream, a);
   return hipGetLastError();
 }
