@@ -6,6 +6,9 @@
 #ifndef SRBD_IPM_FUSE
 #define SRBD_IPM_FUSE 1
 #endif
+#ifndef SRBD_RB_LDS
+#define SRBD_RB_LDS 0
+#endif
 #ifndef SRBD_RES_FENCE
 #define SRBD_RES_FENCE() SRBD_PHASE_FENCE()
 #endif
@@ -203,6 +206,26 @@ struct Ctx {
     return s;
   }
 };
+
+// LDS staging of one 12 x 12 block per QP group (lane j < 12 writes column j)
+__device__ __forceinline__ void lds_put_col(real* blk, int lane, const real (&v)[12]) {
+  if (lane < kMaxDim) store12(blk + lane * 12, v);
+}
+__device__ __forceinline__ void lds_get_col(const real* blk, int c, real (&v)[12]) {
+  load12(blk + c * 12, v);
+}
+__device__ __forceinline__ void lds_get_row(const real* blk, int r, real (&v)[12]) {
+  sfor<0, 12>([&](auto j) {
+    constexpr int J = decltype(j)::value;
+    v[J] = blk[J * 12 + r];
+  });
+}
+// the group's lanes exchange data through LDS inside one wave: keep the
+// compiler from moving the reads above the writes (no instruction emitted)
+__device__ __forceinline__ void lds_wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // barrier state of one variable: lam_l, lam_u, t_l, t_u
 struct Bar {
@@ -686,6 +709,23 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     // and factorizes its barrier-augmented block right away, so the QP data is
     // streamed once per iteration.  If the exit test after the sweep fires, this
     // sweep's factorization is simply not used (outputs read the other parity).
+#if SRBD_RB_LDS
+    // A, B, S of the current stage, staged once per stage through LDS: the
+    // residuals read them row-owned, the factorization column-owned, and the
+    // second pass no longer goes back to L2 / HBM (one QP group: 3 x 144 reals)
+    // (addresses re-derived through an opaque copy at every use, like c.oq(),
+    // so the LDS reads cannot be hoisted into one long-lived register block)
+    __shared__ real rb_lds[(256 / kGroup) * 3 * 144];
+    const int lds_off = (threadIdx.x / kGroup) * 3 * 144;
+    auto lds_at = [&](int blk) {
+      int o = lds_off + blk * 144;
+      asm volatile("" : "+v"(o));
+      return rb_lds + o;
+    };
+#define ldsA lds_at(0)
+#define ldsB lds_at(1)
+#define ldsS lds_at(2)
+#endif
     real mg = real(0.0), mb = real(0.0), md = real(0.0), mm = real(0.0), musum = real(0.0), objl = real(0.0);
     real xn = real(0.0), pin = real(0.0);  // updated x_{k+1}, pi_{k+1} (element-owned), from stage k+1
     real P[12];
@@ -751,26 +791,42 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           SRBD_RES_FENCE();
           {
             real M[12];
-            c.row(c.S() + (size_t)k * c.nxu(), nu, nx, li, uel, M);
-            sx_ = dot12(M, bxk, real(0.0));
-          }
-          SRBD_RES_FENCE();
-          {
-            real M[12];
             c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, M);
             stu = dot12(M, buk, real(0.0));
+#if SRBD_RB_LDS
+            lds_put_col(ldsS, lane, M);
+#endif
           }
           SRBD_RES_FENCE();
           {
             real M[12];
             c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, M);
             btp = dot12(M, bpn, real(0.0));
+#if SRBD_RB_LDS
+            lds_put_col(ldsB, lane, M);
+#endif
           }
           SRBD_RES_FENCE();
           {
             real M[12];
             c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, M);
             atp = dot12(M, bpn, real(0.0));
+#if SRBD_RB_LDS
+            lds_put_col(ldsA, lane, M);
+#endif
+          }
+          SRBD_RES_FENCE();
+#if SRBD_RB_LDS
+          lds_wave_fence();
+#endif
+          {
+            real M[12];
+#if SRBD_RB_LDS
+            lds_get_row(ldsS, li, M);
+#else
+            c.row(c.S() + (size_t)k * c.nxu(), nu, nx, li, uel, M);
+#endif
+            sx_ = dot12(M, bxk, real(0.0));
           }
           SRBD_RES_FENCE();
           const real rk = c.el(c.r() + (size_t)k * nu, nu, li);
@@ -781,13 +837,21 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           real ax;
           {
             real M[12];
+#if SRBD_RB_LDS
+            lds_get_row(ldsA, li, M);
+#else
             c.row(c.A() + (size_t)k * c.nxx(), nx, nx, li, xel, M);
+#endif
             ax = dot12(M, bxk, real(0.0));
           }
           SRBD_RES_FENCE();
           {
             real M[12];
+#if SRBD_RB_LDS
+            lds_get_row(ldsB, li, M);
+#else
             c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, M);
+#endif
             ax = dot12(M, buk, ax);
           }
           SRBD_RES_FENCE();
@@ -908,8 +972,13 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         real bv[12];
         gather12(rb, bv);
         real A_[12], B_[12];
+#if SRBD_RB_LDS >= 2
+        lds_get_col(ldsA, col, A_);
+        lds_get_col(ldsB, col, B_);
+#else
         c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, A_);
         c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, B_);
+#endif
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
           if (c.isv) {
@@ -927,7 +996,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           });
         };
         auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
+#if SRBD_RB_LDS >= 2
+          lds_get_col(ldsS, col, Sc);
+#else
           c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, Sc);
+#endif
           c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
           if constexpr (GEN) g_hess(k, 1, Sc, Qc);
           sfor<0, 12>([&](auto i) {
@@ -1007,6 +1080,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       qs[kQsStatus] = (real)status;
     }
 
+#if SRBD_RB_LDS
+#undef ldsA
+#undef ldsB
+#undef ldsS
+#endif
     return;
   }
   const real mu = qs[kQsMu], musum_all = qs[kQsMuSum];

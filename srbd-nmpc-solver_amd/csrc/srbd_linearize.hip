@@ -16,9 +16,6 @@
 
 #include <hip/hip_runtime.h>
 
-#ifndef SRBD_LIN_PER_STAGE_THREAD
-#define SRBD_LIN_PER_STAGE_THREAD 0
-#endif
 
 namespace srbd {
 namespace {
@@ -146,8 +143,8 @@ struct Model {
     const int r = c % 12;
     return r == 4 ? p.fmax : (r == 5 ? -p.fmin : 0.0);
   }
-  // continuous dynamics f(x, u) (GetContinuousDynamic), optional Jacobians
-  __device__ void f(const double* x, const double* u, double* dx, double* jfx, double* jfu) const {
+  // continuous dynamics f(x, u) (GetContinuousDynamic)
+  __device__ void f(const double* x, const double* u, double* dx) const {
     const V3 r = seg(x, 0), l = seg(x, 3), pos = seg(x, 6);
     const M3 R = expm(r), Jlt = jlt(r);
     const M3 Lb = [&] {
@@ -166,36 +163,6 @@ struct Model {
       dx[3 + i] = u[3 + i] + u[9 + i] + t0.v[i] + t1.v[i];
       dx[6 + i] = x[9 + i];
       dx[9 + i] = (u[i] + u[6 + i]) / p.mass + (i == 2 ? -9.8 : 0.0);
-    }
-    if (!jfx) return;
-    for (int i = 0; i < 144; ++i) {
-      jfx[i] = 0.0;
-      jfu[i] = 0.0;
-    }
-    // d/dr: (d jlt / d r_a) w + jlt (RLR [l]x - [w]x) jl
-    const M3 Jl = jl(r);
-    const M3 mid = mul(mul(Jlt, add(mul(RLR, skew(l)), lin(-1.0, skew(w), 0.0, Lb))), Jl);
-    for (int a = 0; a < 3; ++a) {
-      const M3 dJ = lin(-1.0, mul(mul(Jlt, djl(r, a)), Jlt), 0.0, Jlt);  // d jlt = -jlt d(jl) jlt
-      const V3 col = mv(dJ, w);
-      for (int i = 0; i < 3; ++i) jfx[(0 + a) * 12 + i] = col.v[i] + mid.a[i][a];  // col-major
-    }
-    const M3 JR = mul(Jlt, RLR);
-    V3 fs{{u[0] + u[6], u[1] + u[7], u[2] + u[8]}};
-    const M3 Sf = skew(fs), S0 = skew(p0), S1 = skew(p1);
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) {
-        jfx[(3 + j) * 12 + i] = JR.a[i][j];
-        jfx[(6 + j) * 12 + (3 + i)] = Sf.a[i][j];
-        jfu[(0 + j) * 12 + (3 + i)] = S0.a[i][j];
-        jfu[(6 + j) * 12 + (3 + i)] = S1.a[i][j];
-      }
-    for (int i = 0; i < 3; ++i) {
-      jfx[(9 + i) * 12 + (6 + i)] = 1.0;
-      jfu[(3 + i) * 12 + (3 + i)] = 1.0;
-      jfu[(9 + i) * 12 + (3 + i)] = 1.0;
-      jfu[(0 + i) * 12 + (9 + i)] = 1.0 / p.mass;
-      jfu[(6 + i) * 12 + (9 + i)] = 1.0 / p.mass;
     }
   }
   // Jacobian blocks of f (the nonzero 3x3 blocks of jfx / jfu, :104-176):
@@ -240,6 +207,11 @@ struct LinArgs {
   double qf_scale;
 };
 
+// Per-stage thread, written for the compute it does: the Jacobians come as
+// their 3x3 blocks and every output element is stored once (no read-modify-
+// write of global memory); the friction-cone rows have two nonzeros each, so
+// fc, r and the barrier Hessian Ac' diag(ddb) Ac are formed from that sparsity
+// (a leg's R block has 10 distinct nonzeros) instead of dense 24 x 12 loops.
 __global__ void __launch_bounds__(64) srbd_linearize_kernel(Model m, LinArgs a) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int N = a.N;
@@ -250,112 +222,6 @@ __global__ void __launch_bounds__(64) srbd_linearize_kernel(Model m, LinArgs a) 
   double* q = const_cast<double*>(a.out.q) + ((size_t)qp * (N + 1) + k) * 12;
   const double* x = a.xs + ((size_t)qp * (N + 1) + k) * 12;
   // cost (prepareQpStructures, NMPC_solver.cpp:286-313): Q = diag, q = Q (x - x_ref)
-  const double* wdiag = k < N ? p.Q : p.Qf;
-  const double sc = k < N ? 1.0 : a.qf_scale;
-  for (int j = 0; j < 12; ++j)
-    for (int i = 0; i < 12; ++i) Q[j * 12 + i] = i == j ? sc * wdiag[i] : 0.0;
-  for (int i = 0; i < 12; ++i) q[i] = sc * wdiag[i] * (x[i] - p.x_ref[i]);
-  if (a.mode == 2) {  // cone rows at stage N: none (masked), C = 0
-    double* C = const_cast<double*>(a.out.C) + ((size_t)qp * (N + 1) + k) * 24 * 12;
-    for (int i = 0; i < 24 * 12; ++i) C[i] = 0.0;
-  }
-  if (k == N) {
-    if (a.mode == 2) {
-      const size_t o = ((size_t)qp * (N + 1) + N) * 24;
-      for (int c = 0; c < 24; ++c) {
-        const_cast<double*>(a.out.lg)[o + c] = 0.0;
-        const_cast<double*>(a.out.ug)[o + c] = 1e10;
-        const_cast<double*>(a.out.lg_mask)[o + c] = 0.0;
-        const_cast<double*>(a.out.ug_mask)[o + c] = 0.0;
-      }
-    }
-    return;
-  }
-  const double* u = a.us + ((size_t)qp * N + k) * 12;
-  const double* xn = a.xs + ((size_t)qp * (N + 1) + k + 1) * 12;
-  // shooting dynamics (GetShootingDynamic): RK4 defect, Euler Jacobians
-  double k1[12], k2[12], k3[12], k4[12], xt[12];
-  double* A = const_cast<double*>(a.out.A) + ((size_t)qp * N + k) * 144;
-  double* B = const_cast<double*>(a.out.B) + ((size_t)qp * N + k) * 144;
-  m.f(x, u, k1, A, B);  // jfx, jfu written straight into A, B, then scaled
-  const double dt = p.dt;
-  for (int i = 0; i < 12; ++i) xt[i] = x[i] + 0.5 * dt * k1[i];
-  m.f(xt, u, k2, nullptr, nullptr);
-  for (int i = 0; i < 12; ++i) xt[i] = x[i] + 0.5 * dt * k2[i];
-  m.f(xt, u, k3, nullptr, nullptr);
-  for (int i = 0; i < 12; ++i) xt[i] = x[i] + dt * k3[i];
-  m.f(xt, u, k4, nullptr, nullptr);
-  double* b = const_cast<double*>(a.out.b) + ((size_t)qp * N + k) * 12;
-  for (int i = 0; i < 12; ++i) {
-    const double xg = x[i] + (dt / 6.0) * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
-    b[i] = xg - xn[i];
-  }
-  for (int j = 0; j < 12; ++j)
-    for (int i = 0; i < 12; ++i) {
-      A[j * 12 + i] = (i == j ? 1.0 : 0.0) + dt * A[j * 12 + i];
-      B[j * 12 + i] = dt * B[j * 12 + i];
-    }
-  // friction cone as a barrier in the cost: R = R_ I + Ac' diag(ddb) Ac, r = R_ u + Ac' db
-  double* R = const_cast<double*>(a.out.R) + ((size_t)qp * N + k) * 144;
-  double* r = const_cast<double*>(a.out.r) + ((size_t)qp * N + k) * 12;
-  double* S = const_cast<double*>(a.out.S) + ((size_t)qp * N + k) * 144;
-  for (int i = 0; i < 144; ++i) {
-    R[i] = (i % 13 == 0) ? p.R : 0.0;
-    S[i] = 0.0;
-  }
-  for (int i = 0; i < 12; ++i) r[i] = p.R * u[i];
-  double fc[24];
-  for (int c = 0; c < 24; ++c) {
-    double v = m.bc(c);
-    for (int j = 0; j < 12; ++j) v = fma(m.ac(c, j), u[j], v);
-    fc[c] = v;
-    double db, ddb;
-    m.barrier(v, db, ddb);
-    for (int j = 0; j < 12; ++j) {
-      const double aj = m.ac(c, j);
-      if (aj == 0.0) continue;
-      r[j] += aj * db;
-      for (int i = 0; i < 12; ++i) {
-        const double ai = m.ac(c, i);
-        if (ai != 0.0) R[j * 12 + i] += ai * ddb * aj;
-      }
-    }
-  }
-  if (a.mode == 1) {  // box on u in delta form: u + du inside the per-foot boxes
-    double* lbu = const_cast<double*>(a.out.lbu) + ((size_t)qp * N + k) * 12;
-    double* ubu = const_cast<double*>(a.out.ubu) + ((size_t)qp * N + k) * 12;
-    for (int i = 0; i < 12; ++i) {
-      lbu[i] = p.u_lo[i] - u[i];
-      ubu[i] = p.u_hi[i] - u[i];
-    }
-  } else if (a.mode == 2) {  // lg <= Ac du with lg = -f(u) (du keeps f(u + du) >= 0)
-    double* D = const_cast<double*>(a.out.D) + ((size_t)qp * N + k) * 24 * 12;
-    for (int j = 0; j < 12; ++j)
-      for (int c = 0; c < 24; ++c) D[j * 24 + c] = m.ac(c, j);
-    const size_t o = ((size_t)qp * (N + 1) + k) * 24;
-    for (int c = 0; c < 24; ++c) {
-      const_cast<double*>(a.out.lg)[o + c] = -fc[c];
-      const_cast<double*>(a.out.ug)[o + c] = 1e10;
-      const_cast<double*>(a.out.lg_mask)[o + c] = 1.0;
-      const_cast<double*>(a.out.ug_mask)[o + c] = 0.0;
-    }
-  }
-}
-
-// Per-stage thread, written for the compute it does: the Jacobians come as
-// their 3x3 blocks and every output element is stored once (no read-modify-
-// write of global memory); the friction-cone rows have two nonzeros each, so
-// fc, r and the barrier Hessian Ac' diag(ddb) Ac are formed from that sparsity
-// (a leg's R block has 10 distinct nonzeros) instead of dense 24 x 12 loops.
-__global__ void __launch_bounds__(64) srbd_linearize_fast_kernel(Model m, LinArgs a) {
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int N = a.N;
-  if (t >= (long long)a.batch * (N + 1)) return;
-  const int qp = (int)(t / (N + 1)), k = (int)(t % (N + 1));
-  const srbd_model_params& p = m.p;
-  double* Q = const_cast<double*>(a.out.Q) + ((size_t)qp * (N + 1) + k) * 144;
-  double* q = const_cast<double*>(a.out.q) + ((size_t)qp * (N + 1) + k) * 12;
-  const double* x = a.xs + ((size_t)qp * (N + 1) + k) * 12;
   const double* wdiag = k < N ? p.Q : p.Qf;
   const double sc = k < N ? 1.0 : a.qf_scale;
 #pragma unroll
@@ -383,19 +249,19 @@ __global__ void __launch_bounds__(64) srbd_linearize_fast_kernel(Model m, LinArg
   const double* u = a.us + ((size_t)qp * N + k) * 12;
   const double* xn = a.xs + ((size_t)qp * (N + 1) + k + 1) * 12;
   const double dt = p.dt;
-  // ---- b = RK4(x, u) - x_next ----
+  // ---- shooting dynamics (GetShootingDynamic, SRBD_model.cpp:178-235): b = RK4(x, u) - x_next ----
   {
     double k1[12], k2[12], k3[12], k4[12], xt[12];
-    m.f(x, u, k1, nullptr, nullptr);
+    m.f(x, u, k1);
 #pragma unroll
     for (int i = 0; i < 12; ++i) xt[i] = x[i] + 0.5 * dt * k1[i];
-    m.f(xt, u, k2, nullptr, nullptr);
+    m.f(xt, u, k2);
 #pragma unroll
     for (int i = 0; i < 12; ++i) xt[i] = x[i] + 0.5 * dt * k2[i];
-    m.f(xt, u, k3, nullptr, nullptr);
+    m.f(xt, u, k3);
 #pragma unroll
     for (int i = 0; i < 12; ++i) xt[i] = x[i] + dt * k3[i];
-    m.f(xt, u, k4, nullptr, nullptr);
+    m.f(xt, u, k4);
     double* b = const_cast<double*>(a.out.b) + ((size_t)qp * N + k) * 12;
 #pragma unroll
     for (int i = 0; i < 12; ++i)
@@ -430,7 +296,8 @@ __global__ void __launch_bounds__(64) srbd_linearize_fast_kernel(Model m, LinArg
         B[j * 12 + i] = dt * ju;
       }
   }
-  // ---- friction cone (two nonzeros per row) as a barrier in the cost ----
+  // ---- friction cone (GetConstrain :237-260, two nonzeros per row) as a barrier in the cost
+  // (Barrier :262-295): R = R_ I + Ac' diag(ddb) Ac, r = R_ u + Ac' db ----
   double Rm[12][12];
 #pragma unroll
   for (int j = 0; j < 12; ++j)
@@ -500,7 +367,7 @@ __global__ void __launch_bounds__(64) srbd_linearize_fast_kernel(Model m, LinArg
     }
 #pragma unroll
   for (int i = 0; i < 12; ++i) rr[i] = rv[i];
-  if (a.mode == 1) {
+  if (a.mode == 1) {  // box on u in delta form: u + du inside the per-foot boxes
     double* lbu = const_cast<double*>(a.out.lbu) + ((size_t)qp * N + k) * 12;
     double* ubu = const_cast<double*>(a.out.ubu) + ((size_t)qp * N + k) * 12;
 #pragma unroll
@@ -508,7 +375,7 @@ __global__ void __launch_bounds__(64) srbd_linearize_fast_kernel(Model m, LinArg
       lbu[i] = p.u_lo[i] - u[i];
       ubu[i] = p.u_hi[i] - u[i];
     }
-  } else if (a.mode == 2) {
+  } else if (a.mode == 2) {  // lg <= Ac du with lg = -f(u) (du keeps f(u + du) >= 0)
     double* D = const_cast<double*>(a.out.D) + ((size_t)qp * N + k) * 24 * 12;
     for (int j = 0; j < 12; ++j)
       for (int c = 0; c < 24; ++c) D[j * 24 + c] = m.ac(c, j);
@@ -573,13 +440,13 @@ __device__ void stage_merit(const Model& m, const LsArgs& a, int qp, int k, doub
   for (int i = 0; i < 12; ++i) ua[i] = u[i] + al * du[i];
   // shooting defect f = x_next - RK4(x, u) (GetShootingDynamic)
   const double dt = p.dt;
-  m.f(xa, ua, k1, nullptr, nullptr);
+  m.f(xa, ua, k1);
   for (int i = 0; i < 12; ++i) xt[i] = xa[i] + 0.5 * dt * k1[i];
-  m.f(xt, ua, k2, nullptr, nullptr);
+  m.f(xt, ua, k2);
   for (int i = 0; i < 12; ++i) xt[i] = xa[i] + 0.5 * dt * k2[i];
-  m.f(xt, ua, k3, nullptr, nullptr);
+  m.f(xt, ua, k3);
   for (int i = 0; i < 12; ++i) xt[i] = xa[i] + dt * k3[i];
-  m.f(xt, ua, k4, nullptr, nullptr);
+  m.f(xt, ua, k4);
   for (int i = 0; i < 12; ++i) {
     const double xg = xa[i] + (dt / 6.0) * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
     const double f = (xn[i] + al * dxn[i]) - xg;
@@ -688,17 +555,10 @@ hipError_t launch_srbd_linearize(const srbd_model_params& p, int batch, int N, i
   if (batch <= 0) return hipSuccess;
   Model m{p};
   LinArgs a{batch, N, mode, xs, us, out, p.qf_scale};
-#if SRBD_LIN_PER_STAGE_THREAD
   const long long n = (long long)batch * (N + 1);
   const int threads = 64;
   hipLaunchKernelGGL(srbd_linearize_kernel, dim3((unsigned)((n + threads - 1) / threads)),
                      dim3(threads), 0, stream, m, a);
-#else
-  const long long n = (long long)batch * (N + 1);
-  const int threads = 64;
-  hipLaunchKernelGGL(srbd_linearize_fast_kernel, dim3((unsigned)((n + threads - 1) / threads)),
-                     dim3(threads), 0, stream, m, a);
-#endif
   return hipGetLastError();
 }
 
