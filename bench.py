@@ -433,7 +433,8 @@ def cpu_baseline(pkg, qp, x0, settings, budget_s):
 
 
 def pmc_traffic(workload, batch):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    """HBM bytes per launch (unconstrained: the one kernel; IPM: one whole solve)
+    from the committed rocprofv3 PMC summary, if any."""
     f = REPO / "profiles" / "pmc_traffic.json"
     if not f.exists():
         return None
@@ -441,6 +442,9 @@ def pmc_traffic(workload, batch):
         d = json.loads(f.read_text())
         e = d.get(workload)
         if e and int(e.get("batch", -1)) == batch:
+            # IPM workloads: the whole solve (every phase launch of it) is the unit
+            if WORKLOADS[workload][1] != "none" and e.get("per_solve"):
+                return e["per_solve"].get("hbm_bytes")
             return e.get("hbm_bytes_per_launch")
     except Exception:
         return None

@@ -47,6 +47,8 @@
  *     lbx, ubx, lbx_mask, ubx_mask [batch][N+1][nx]      (NULL lbx: no box)
  *   General constraints (ng rows per stage, pad with masked rows):
  *     C [batch][N+1][ng*nx]  D [batch][N][ng*nu]  lg, ug, lg_mask, ug_mask [batch][N+1][ng]
+ *   C = NULL means C = 0 (rows on u only, e.g. the friction cone) and selects
+ *   the kernels without the C products; D = NULL means D = 0.
  * Outputs:
  *     x [batch][N+1][nx]  u [batch][N][nu]  pi [batch][N+1][nx]   (required)
  *     P [batch][N+1][nx*nx]  p [batch][N+1][nx]  K [batch][N][nu*nx]  k [batch][N][nu]
@@ -239,8 +241,9 @@ void srbd_qp_srbd_default_params(srbd_model_params* p);
 
 /* Linearise `batch` SRBD trajectories on the handle's device and stream (or
  * `stream`): xs [batch][N+1][12], us [batch][N][12] (device).  Fills A, B, b,
- * Q, S, R, q, r of `out` and, per `constraints`, lbu/ubu (BOX_U) or C, D, lg,
- * ug, lg_mask, ug_mask (CONE: ng = 24, lg = -f(u), ug masked).  The handle's
+ * Q, S, R, q, r of `out` and, per `constraints`, lbu/ubu (BOX_U) or D, lg,
+ * ug, lg_mask, ug_mask (CONE: ng = 24, lg = -f(u), ug masked; C = 0 is
+ * written only if out->C is given -- pass C = NULL to the solve).  The handle's
  * dims must be N, nx = nu = 12 (and ng = 24 for CONE).  Asynchronous.       */
 int srbd_qp_srbd_linearize_f64(srbd_qp_handle h, int batch, const srbd_model_params* params,
                                int constraints, const double* xs, const double* us,

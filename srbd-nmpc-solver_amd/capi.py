@@ -331,7 +331,6 @@ def srbd_linearize(handle: Handle, xs, us, constraints: str = "none",
         t["lbu"] = torch.empty(B, N, 12, **f)
         t["ubu"] = torch.empty(B, N, 12, **f)
     elif constraints == "cone":
-        t["C"] = torch.empty(B, N + 1, 24 * 12, **f)
         t["D"] = torch.empty(B, N, 24 * 12, **f)
         for k in ("lg", "ug", "lg_mask", "ug_mask"):
             t[k] = torch.empty(B, N + 1, 24, **f)

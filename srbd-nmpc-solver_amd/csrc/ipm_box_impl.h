@@ -52,13 +52,22 @@ __device__ __forceinline__ real gmin(real v) {
 // |v| propagating NaN (max with NaN would drop it)
 __device__ __forceinline__ real nabs(real v) { return v == v ? fabs(v) : real(__builtin_inf()); }
 
+template <typename T>
+__device__ __forceinline__ T dot12(const T (&a)[12], const T (&b)[12], T acc) {
+  sfor<0, 12>([&](auto j) {
+    constexpr int J = decltype(j)::value;
+    acc = fmadd(a[J], b[J], acc);
+  });
+  return acc;
+}
+
 // One inequality side on one variable (box bound, dense per variable).
 struct Side {
   real lb, ub;   // bounds
   real ml, mu;   // 1 if the lower / upper bound is active, else 0
 };
 
-template <bool FULL, bool GEN>
+template <bool FULL, int GEN>
 struct Ctx {
   int N, nx, nu, lane, qp;
   bool isv;
@@ -134,7 +143,7 @@ struct Ctx {
   __device__ void g_row(int k, int ch, int i, real (&Cr)[12], real (&Dr)[12]) const {
     const int r = ch * kMaxDim + i;
     const bool ok = i < kMaxDim && r < ng;
-    const bool cok = ok && bC && k > 0, dok = ok && bD && k < N;
+    const bool cok = GEN == 2 && ok && bC && k > 0, dok = ok && bD && k < N;
     const real* cb = C() ? C() + (size_t)k * ng * nx + r : nullptr;
     const real* db = D() ? D() + (size_t)k * ng * nu + r : nullptr;
     sfor<0, 12>([&](auto j) {
@@ -143,10 +152,17 @@ struct Ctx {
       Dr[J] = (dok && J < nu) ? db[(size_t)J * ng] : real(0.0);
     });
   }
+  // value of row i of chunk ch: C_k x + D_k u (GEN == 1: no C, the product is skipped)
+  __device__ real g_row_dot(int k, int ch, int i, const real (&bx)[12], const real (&bu)[12]) const {
+    real Cr[12], Dr[12];
+    g_row(k, ch, i, Cr, Dr);
+    if constexpr (GEN == 2) return dot12(Dr, bu, dot12(Cr, bx, real(0.0)));
+    return dot12(Dr, bu, real(0.0));
+  }
   // column-owned C / D columns restricted to chunk ch (lane j = column)
   __device__ void g_col(int k, int ch, int j, real (&Cc)[12], real (&Dc)[12]) const {
     const int r0 = ch * kMaxDim;
-    const bool cok = bC && k > 0 && j < nx, dok = bD && k < N && j < nu;
+    const bool cok = GEN == 2 && bC && k > 0 && j < nx, dok = bD && k < N && j < nu;
     const real* cb = C() ? C() + (size_t)k * ng * nx + (size_t)j * ng + r0 : nullptr;
     const real* db = D() ? D() + (size_t)k * ng * nu + (size_t)j * ng + r0 : nullptr;
     sfor<0, 12>([&](auto i) {
@@ -279,14 +295,6 @@ __device__ __forceinline__ void store_gstep(real* g, int i, const BarStep& d) {
 }
 constexpr int kGenVal = 96;
 
-template <typename T>
-__device__ __forceinline__ T dot12(const T (&a)[12], const T (&b)[12], T acc) {
-  sfor<0, 12>([&](auto j) {
-    constexpr int J = decltype(j)::value;
-    acc = fmadd(a[J], b[J], acc);
-  });
-  return acc;
-}
 
 // Gamma (Hessian add) and gamma (gradient add) of one variable:
 // Gamma = lam_l/t_l + lam_u/t_u,
@@ -360,7 +368,7 @@ __device__ __forceinline__ void gather12(real v, real (&out)[12]) {
   });
 }
 
-template <bool FULL, bool GEN, int PH>
+template <bool FULL, int GEN, int PH>
 __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int qp = gid >> 4;
@@ -418,7 +426,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       g_gamma(k, ch, corr, smu, G, gg);
       gather12(gg, bg);
       c.g_col(k, ch, col, Cc, Dc);
-      qadd = dot12(Cc, bg, qadd);
+      if constexpr (GEN == 2) qadd = dot12(Cc, bg, qadd);
       radd = dot12(Dc, bg, radd);
     }
   };
@@ -550,9 +558,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       gather12(xi, bxi);
       gather12(ui, bui);
       for (int ch = 0; ch < c.nch; ++ch) {
-        real Cr[12], Dr[12];
-        c.g_row(k, ch, lane, Cr, Dr);
-        const real v = dot12(Dr, bui, dot12(Cr, bxi, real(0.0)));
+        const real v = c.g_row_dot(k, ch, lane, bxi, bui);
         const Side s = c.side_g(k, ch, lane);
         Bar bb{real(0.0), real(0.0), real(1.0), real(1.0)};
         if (s.ml != real(0.0)) {
@@ -872,9 +878,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
               bg.lu += alpha_d * d.dlu;
               store_gbar(g, lane, bg);
             }
-            real Cr[12], Dr[12];
-            c.g_row(k, ch, lane, Cr, Dr);
-            const real v = dot12(Dr, buk, dot12(Cr, bxk, real(0.0)));
+            const real v = c.g_row_dot(k, ch, lane, bxk, buk);
             if (lane < kMaxDim) g[kGenVal + lane] = v;
             if (sg.ml != real(0.0)) {
               const real rd = v - sg.lb - bg.tl, rm = bg.ll * bg.tl;
@@ -891,7 +895,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             real bdl[12], Cc[12], Dc[12];
             gather12(lane < kMaxDim ? bg.lu - bg.ll : real(0.0), bdl);
             c.g_col(k, ch, col, Cc, Dc);
-            rgx = dot12(Cc, bdl, rgx);
+            if constexpr (GEN == 2) rgx = dot12(Cc, bdl, rgx);
             rgu = dot12(Dc, bdl, rgu);
           }
         }
@@ -960,7 +964,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         real qv[12];
         gather12(qt, qv);
         c.col(c.Q() + (size_t)N * c.nxx(), nx, col, xel, P);
-        if constexpr (GEN) g_hess(N, 2, P, P);
+        if constexpr (GEN == 2) g_hess(N, 2, P, P);
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
           if (lane == I) P[I] += Gx;
@@ -1002,7 +1006,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, Sc);
 #endif
           c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
-          if constexpr (GEN) g_hess(k, 1, Sc, Qc);
+          if constexpr (GEN == 2) g_hess(k, 1, Sc, Qc);  // C = 0: D'Gamma C = C'Gamma C = 0
           sfor<0, 12>([&](auto i) {
             constexpr int I = decltype(i)::value;
             const real rI = bc<I>(rt), qI = bc<I>(qt);
@@ -1245,9 +1249,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           gather12(du, bdu);
           for (int ch = 0; ch < c.nch; ++ch) {
             real* g = c.gs(k, ch);
-            real Cr[12], Dr[12];
-            c.g_row(k, ch, lane, Cr, Dr);
-            const real dv = dot12(Dr, bdu, dot12(Cr, bdx, real(0.0)));
+            const real dv = c.g_row_dot(k, ch, lane, bdx, bdu);
             if (lane < kMaxDim) {
               const Side sg = c.side_g(k, ch, lane);
               const Bar bg = load_gbar(g, lane);
@@ -1338,7 +1340,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 }
 
 
-template <bool FULL, bool GEN, int PH>
+template <bool FULL, int GEN, int PH>
 __global__ void __launch_bounds__(256, 2) ipm_phase_kernel(ProblemArgsT<real> a) {
   ipm_phase<FULL, GEN, PH>(a);
 }
@@ -1348,14 +1350,14 @@ __global__ void __launch_bounds__(256, 2) ipm_phase_kernel(ProblemArgsT<real> a)
 // their records are still in L2 / the Infinity Cache, and the launch count halves.
 // The second phase re-reads the per-QP state the first one wrote (same wave:
 // visible after the workgroup-scope fence).
-template <bool FULL, bool GEN, int PH1, int PH2>
+template <bool FULL, int GEN, int PH1, int PH2>
 __global__ void __launch_bounds__(256, 2) ipm_phase2_kernel(ProblemArgsT<real> a) {
   ipm_phase<FULL, GEN, PH1>(a);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   ipm_phase<FULL, GEN, PH2>(a);
 }
 
-template <bool FULL, bool GEN>
+template <bool FULL, int GEN>
 static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream) {
   const int threads = 256;
   const long long lanes = (long long)a.batch * kGroup;
@@ -1393,8 +1395,12 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
 hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {
   if (a.batch <= 0) return hipSuccess;
   const bool full = a.nx == 12 && a.nu == 12;
-  if (a.ng > 0) return full ? launch_phases<true, true>(a, stream) : launch_phases<false, true>(a, stream);
-  return full ? launch_phases<true, false>(a, stream) : launch_phases<false, false>(a, stream);
+  // general rows: GEN 2 with C, GEN 1 when C is absent (NULL = 0, e.g. the friction
+  // cone, SRBD_model.cpp:237-260, which constrains u only)
+  if (a.ng > 0 && a.C)
+    return full ? launch_phases<true, 2>(a, stream) : launch_phases<false, 2>(a, stream);
+  if (a.ng > 0) return full ? launch_phases<true, 1>(a, stream) : launch_phases<false, 1>(a, stream);
+  return full ? launch_phases<true, 0>(a, stream) : launch_phases<false, 0>(a, stream);
 }
 
 }  // namespace SRBD_NS

@@ -230,7 +230,7 @@ __global__ void __launch_bounds__(64) srbd_linearize_kernel(Model m, LinArgs a) 
     for (int i = 0; i < 12; ++i) Q[j * 12 + i] = i == j ? sc * wdiag[i] : 0.0;
 #pragma unroll
   for (int i = 0; i < 12; ++i) q[i] = sc * wdiag[i] * (x[i] - p.x_ref[i]);
-  if (a.mode == 2) {
+  if (a.mode == 2 && a.out.C) {  // the cone has C = 0; NULL C is left out
     double* C = const_cast<double*>(a.out.C) + ((size_t)qp * (N + 1) + k) * 24 * 12;
     for (int i = 0; i < 24 * 12; ++i) C[i] = 0.0;
   }

@@ -440,8 +440,8 @@ int srbd_qp_srbd_linearize_f64(srbd_qp_handle h, int batch, const srbd_model_par
   if (constraints == SRBD_QP_SRBD_BOX_U && (!out->lbu || !out->ubu))
     return fail(SRBD_QP_EINVAL, "BOX_U needs lbu / ubu outputs");
   if (constraints == SRBD_QP_SRBD_CONE &&
-      (d.ng != 24 || !out->C || !out->D || !out->lg || !out->ug || !out->lg_mask || !out->ug_mask))
-    return fail(SRBD_QP_EINVAL, "CONE needs ng = 24 and C, D, lg, ug, lg_mask, ug_mask outputs");
+      (d.ng != 24 || !out->D || !out->lg || !out->ug || !out->lg_mask || !out->ug_mask))
+    return fail(SRBD_QP_EINVAL, "CONE needs ng = 24 and D, lg, ug, lg_mask, ug_mask outputs (C optional)");
   srbd_model_params p = *params;
   if (p.qf_scale <= 0.0) p.qf_scale = (double)d.N;
   hipStream_t strm = stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;

@@ -412,7 +412,11 @@ std::vector<HpipmStatus> OcpQpIpmSolver::solveBatch(
     d.lbx = ptr(m.lbx); d.ubx = ptr(m.ubx); d.lbx_mask = ptr(m.lbx_m); d.ubx_mask = ptr(m.ubx_m);
   }
   if (s.ng) {
-    d.C = ptr(m.C); d.D = ptr(m.D); d.lg = ptr(m.lg); d.ug = ptr(m.ug);
+    // an all-zero C (e.g. the friction cone, which constrains u only) goes in as
+    // NULL: the kernel then skips the C products instead of multiplying zeros
+    const bool c_zero = std::all_of(m.C.begin(), m.C.end(), [](double v) { return v == 0.0; });
+    d.C = c_zero ? nullptr : ptr(m.C);
+    d.D = ptr(m.D); d.lg = ptr(m.lg); d.ug = ptr(m.ug);
     d.lg_mask = ptr(m.lg_m); d.ug_mask = ptr(m.ug_m);
   }
   srbd_qp_solution_f64 o{};

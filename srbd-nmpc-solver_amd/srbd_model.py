@@ -269,7 +269,7 @@ def build_qp(xs, us, p: Optional[SrbdParams] = None, constraints: str = "none", 
     elif constraints == "cone":
         qp.ng = 24
         qp.D = np.broadcast_to(Ac, (batch, N, 24, 12)).copy()
-        qp.C = np.zeros((batch, N + 1, 24, 12))
+        qp.C = None  # the cone constrains u only (C = 0): passed as NULL, the C-free kernel path
         qp.lg = np.zeros((batch, N + 1, 24))
         qp.lg[:, :N] = -fc
         qp.ug = np.full((batch, N + 1, 24), 1e10)

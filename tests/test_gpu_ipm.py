@@ -207,3 +207,18 @@ def test_srbd_friction_cone_vs_oracle(pkg, oracle):
     for i in range(qp.batch):
         assert helpers.is_approx(out["u"][i], ref["u"][i], 1e-7), i
         assert helpers.is_approx(out["x"][i], ref["x"][i], 1e-7), i
+
+
+def test_cone_without_c_equals_zero_c(pkg):
+    """C = NULL (rows on u only) selects the kernels without the C products; an
+    explicit all-zero C runs the general ones.  Same iterates either way."""
+    qp, x0 = pkg.srbd_model.generate_batch(16, N=10, seed=21, constraints="cone")
+    assert qp.C is None
+    st = dict(iter_max=40)
+    a = pkg.capi.solve(qp, x0, st, stats=True)
+    qp.C = np.zeros((qp.batch, qp.N + 1, qp.ng, qp.nx))
+    b = pkg.capi.solve(qp, x0, st, stats=True)
+    np.testing.assert_array_equal(a["status"], b["status"])
+    np.testing.assert_array_equal(a["iter"], b["iter"])
+    for key in ("x", "u", "pi", "stat"):
+        np.testing.assert_allclose(a[key], b[key], rtol=1e-12, atol=1e-12 * np.abs(b[key]).max())
