@@ -77,7 +77,7 @@ def alg_bytes_per_qp(N, nx=12, nu=12, constraints="none", elem=8, ng=24):
     if constraints == "box_u":
         vals += N * 2 * nu
     if constraints == "cone":
-        vals += N * (ng * nx + ng * nu + 2 * ng)  # C, D, lg, ug per stage
+        vals += N * (ng * nu + 2 * ng)  # D, lg, ug per stage (C = 0 is passed as NULL)
     out = (N + 1) * nx + N * nu + (N + 1) * nx
     return elem * (vals + out)
 
