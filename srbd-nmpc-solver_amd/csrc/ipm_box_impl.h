@@ -61,6 +61,37 @@ __device__ __forceinline__ T dot12(const T (&a)[12], const T (&b)[12], T acc) {
   return acc;
 }
 
+// barrier state of one variable: lam_l, lam_u, t_l, t_u
+struct Bar {
+  real ll, lu, tl, tu;
+};
+__device__ __forceinline__ Bar load_bar(const real* stk, int which, int i) {
+  const real* p = stk + kStLam + which * 48;
+  return Bar{p[i], p[12 + i], p[24 + i], p[36 + i]};
+}
+__device__ __forceinline__ void store_bar(real* stk, int which, int i, const Bar& b) {
+  real* p = stk + kStLam + which * 48;
+  p[i] = b.ll;
+  p[12 + i] = b.lu;
+  p[24 + i] = b.tl;
+  p[36 + i] = b.tu;
+}
+// step of one variable's barrier pair: dt_l, dt_u, dlam_l, dlam_u
+struct BarStep {
+  real dtl, dtu, dll, dlu;
+};
+__device__ __forceinline__ BarStep load_bstep(const real* stk, int which, int i) {
+  const real* p = stk + kStDlt + which * 48;
+  return BarStep{p[i], p[12 + i], p[24 + i], p[36 + i]};
+}
+__device__ __forceinline__ void store_bstep(real* stk, int which, int i, const BarStep& d) {
+  real* p = stk + kStDlt + which * 48;
+  p[i] = d.dtl;
+  p[12 + i] = d.dtu;
+  p[24 + i] = d.dll;
+  p[36 + i] = d.dlu;
+}
+
 // One inequality side on one variable (box bound, dense per variable).
 struct Side {
   real lb, ub;   // bounds
@@ -199,6 +230,26 @@ struct Ctx {
       return i < n ? v[i] : real(0.0);
     }
   }
+  // per-variable barrier state exists only for the bound families that are given
+  // (which 0: u, 1: x): absent ones are neither loaded nor stored
+  // (FULL only: the generic-size kernels keep the unconditional accesses, their
+  // spill-heavy code generation faulted with the uniform branches added)
+  __device__ bool has_bars(int which) const {
+    if constexpr (!FULL) return true;
+    return which ? blbx != nullptr : blbu != nullptr;
+  }
+  __device__ Bar bar(const real* stk, int which, int i) const {
+    return has_bars(which) ? load_bar(stk, which, i) : Bar{real(0.0), real(0.0), real(1.0), real(1.0)};
+  }
+  __device__ void put_bar(real* stk, int which, int i, const Bar& b) const {
+    if (has_bars(which)) store_bar(stk, which, i, b);
+  }
+  __device__ BarStep bstep(const real* stk, int which, int i) const {
+    return has_bars(which) ? load_bstep(stk, which, i) : BarStep{real(0.0), real(0.0), real(0.0), real(0.0)};
+  }
+  __device__ void put_bstep(real* stk, int which, int i, const BarStep& d) const {
+    if (has_bars(which)) store_bstep(stk, which, i, d);
+  }
   __device__ Side side_u(int k, int i) const {
     Side s{real(0.0), real(0.0), real(0.0), real(0.0)};
     if (blbu && i < nu && k < N) {
@@ -241,37 +292,6 @@ __device__ __forceinline__ void lds_get_row(const real* blk, int r, real (&v)[12
 __device__ __forceinline__ void lds_wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
-}
-
-// barrier state of one variable: lam_l, lam_u, t_l, t_u
-struct Bar {
-  real ll, lu, tl, tu;
-};
-__device__ __forceinline__ Bar load_bar(const real* stk, int which, int i) {
-  const real* p = stk + kStLam + which * 48;
-  return Bar{p[i], p[12 + i], p[24 + i], p[36 + i]};
-}
-__device__ __forceinline__ void store_bar(real* stk, int which, int i, const Bar& b) {
-  real* p = stk + kStLam + which * 48;
-  p[i] = b.ll;
-  p[12 + i] = b.lu;
-  p[24 + i] = b.tl;
-  p[36 + i] = b.tu;
-}
-// step of one variable's barrier pair: dt_l, dt_u, dlam_l, dlam_u
-struct BarStep {
-  real dtl, dtu, dll, dlu;
-};
-__device__ __forceinline__ BarStep load_bstep(const real* stk, int which, int i) {
-  const real* p = stk + kStDlt + which * 48;
-  return BarStep{p[i], p[12 + i], p[24 + i], p[36 + i]};
-}
-__device__ __forceinline__ void store_bstep(real* stk, int which, int i, const BarStep& d) {
-  real* p = stk + kStDlt + which * 48;
-  p[i] = d.dtl;
-  p[12 + i] = d.dtu;
-  p[24 + i] = d.dll;
-  p[36 + i] = d.dlu;
 }
 
 // general-constraint chunk state (see kGenChunk)
@@ -757,9 +777,9 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       Bar bu{0, 0, 1, 1}, bx{0, 0, 1, 1};
       const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
       if (lane < kMaxDim) {
-        bu = load_bar(stk, 0, lane);
-        bx = load_bar(stk, 1, lane);
-        const BarStep du = load_bstep(stk, 0, lane), dx = load_bstep(stk, 1, lane);
+        bu = c.bar(stk, 0, lane);
+        bx = c.bar(stk, 1, lane);
+        const BarStep du = c.bstep(stk, 0, lane), dx = c.bstep(stk, 1, lane);
         bu.tl += alpha_p * du.dtl;
         bu.tu += alpha_p * du.dtu;
         bu.ll += alpha_d * du.dll;
@@ -768,8 +788,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         bx.tu += alpha_p * dx.dtu;
         bx.ll += alpha_d * dx.dll;
         bx.lu += alpha_d * dx.dlu;
-        store_bar(stk, 0, lane, bu);
-        store_bar(stk, 1, lane, bx);
+        c.put_bar(stk, 0, lane, bu);
+        c.put_bar(stk, 1, lane, bx);
       }
       // ---- residuals of stage k (element-owned) ----
       real rgx = real(0.0), rgu = real(0.0), rb = real(0.0);
@@ -1099,11 +1119,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         {
           real* stN = c.st(N);
           const Side sx = c.side_x(N, lane);
-          const real xv = xel ? c.x()[(size_t)N * nx + lane] : real(0.0);
+          const real xv = xel && c.has_bars(1) ? c.x()[(size_t)N * nx + lane] : real(0.0);
           real G = real(0.0), g = real(0.0);
           if (lane < kMaxDim) {
-            const BarStep dx = load_bstep(stN, 1, lane);
-            gamma_of(sx, load_bar(stN, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, G, g);
+            const BarStep dx = c.bstep(stN, 1, lane);
+            gamma_of(sx, c.bar(stN, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, G, g);
           }
           pnext = lane < kMaxDim && xel ? stN[kStRes + 12 + lane] + g : real(0.0);
           if constexpr (GEN) {
@@ -1118,13 +1138,14 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           real* rec = stk + par * kRecSize;
           const real* recn = c.st(k + 1) + par * kRecSize;
           const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
-          const real uv = uel ? c.u()[(size_t)k * nu + lane] : real(0.0);
-          const real xv = xel ? c.x()[(size_t)k * nx + lane] : real(0.0);
+          // x, u enter only through the barrier terms of the bound families present
+          const real uv = uel && c.has_bars(0) ? c.u()[(size_t)k * nu + lane] : real(0.0);
+          const real xv = xel && c.has_bars(1) ? c.x()[(size_t)k * nx + lane] : real(0.0);
           real Gu = real(0.0), gu = real(0.0), Gx = real(0.0), gx = real(0.0);
           if (lane < kMaxDim) {
-            const BarStep du = load_bstep(stk, 0, lane), dx = load_bstep(stk, 1, lane);
-            gamma_of(su, load_bar(stk, 0, lane), uv, du.dll * du.dtl, du.dlu * du.dtu, sigma_mu, Gu, gu);
-            gamma_of(sx, load_bar(stk, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, Gx, gx);
+            const BarStep du = c.bstep(stk, 0, lane), dx = c.bstep(stk, 1, lane);
+            gamma_of(su, c.bar(stk, 0, lane), uv, du.dll * du.dtl, du.dlu * du.dtu, sigma_mu, Gu, gu);
+            gamma_of(sx, c.bar(stk, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, Gx, gx);
           }
           real rt = lane < kMaxDim && uel ? stk[kStRes + lane] + gu : real(0.0);
           real qt = lane < kMaxDim && xel ? stk[kStRes + 12 + lane] + gx : real(0.0);
@@ -1269,12 +1290,12 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         }
         if (lane < kMaxDim) {
           const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
-          const Bar bu = load_bar(stk, 0, lane), bx = load_bar(stk, 1, lane);
-          const real uv = (uel && k < N) ? c.u()[(size_t)k * nu + lane] : real(0.0);
-          const real xv = xel ? c.x()[(size_t)k * nx + lane] : real(0.0);
+          const Bar bu = c.bar(stk, 0, lane), bx = c.bar(stk, 1, lane);
+          const real uv = (uel && k < N && c.has_bars(0)) ? c.u()[(size_t)k * nu + lane] : real(0.0);
+          const real xv = xel && c.has_bars(1) ? c.x()[(size_t)k * nx + lane] : real(0.0);
           real eul = real(0.0), euu = real(0.0), exl = real(0.0), exu = real(0.0), smu = real(0.0);
           if (corr) {
-            const BarStep pu = load_bstep(stk, 0, lane), px = load_bstep(stk, 1, lane);
+            const BarStep pu = c.bstep(stk, 0, lane), px = c.bstep(stk, 1, lane);
             eul = pu.dll * pu.dtl;
             euu = pu.dlu * pu.dtu;
             exl = px.dll * px.dtl;
@@ -1289,8 +1310,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             aff_sums(su, bu, nu_, s1, s2);
             aff_sums(sx, bx, nx_, s1, s2);
           }
-          store_bstep(stk, 0, lane, nu_);
-          store_bstep(stk, 1, lane, nx_);
+          c.put_bstep(stk, 0, lane, nu_);
+          c.put_bstep(stk, 1, lane, nx_);
           stk[kStStep + lane] = du;
           stk[kStStep + 12 + lane] = dxk;
           stk[kStStep + 24 + lane] = k > 0 ? dpi : real(0.0);
@@ -1341,7 +1362,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 
 
 template <bool FULL, int GEN, int PH>
-__global__ void __launch_bounds__(256, 2) ipm_phase_kernel(ProblemArgsT<real> a) {
+__global__ void __launch_bounds__(256, FULL ? 2 : 1) ipm_phase_kernel(ProblemArgsT<real> a) {
   ipm_phase<FULL, GEN, PH>(a);
 }
 
@@ -1351,7 +1372,7 @@ __global__ void __launch_bounds__(256, 2) ipm_phase_kernel(ProblemArgsT<real> a)
 // The second phase re-reads the per-QP state the first one wrote (same wave:
 // visible after the workgroup-scope fence).
 template <bool FULL, int GEN, int PH1, int PH2>
-__global__ void __launch_bounds__(256, 2) ipm_phase2_kernel(ProblemArgsT<real> a) {
+__global__ void __launch_bounds__(256, FULL ? 2 : 1) ipm_phase2_kernel(ProblemArgsT<real> a) {
   ipm_phase<FULL, GEN, PH1>(a);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   ipm_phase<FULL, GEN, PH2>(a);
