@@ -1415,13 +1415,13 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
 
 hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {
   if (a.batch <= 0) return hipSuccess;
-  const bool full = a.nx == 12 && a.nu == 12;
+  // 12 x 12 stages only: smaller problems arrive embedded by pad.hip
+  if (a.nx != 12 || a.nu != 12) return hipErrorInvalidValue;
   // general rows: GEN 2 with C, GEN 1 when C is absent (NULL = 0, e.g. the friction
   // cone, SRBD_model.cpp:237-260, which constrains u only)
-  if (a.ng > 0 && a.C)
-    return full ? launch_phases<true, 2>(a, stream) : launch_phases<false, 2>(a, stream);
-  if (a.ng > 0) return full ? launch_phases<true, 1>(a, stream) : launch_phases<false, 1>(a, stream);
-  return full ? launch_phases<true, 0>(a, stream) : launch_phases<false, 0>(a, stream);
+  if (a.ng > 0 && a.C) return launch_phases<true, 2>(a, stream);
+  if (a.ng > 0) return launch_phases<true, 1>(a, stream);
+  return launch_phases<true, 0>(a, stream);
 }
 
 }  // namespace SRBD_NS

@@ -82,6 +82,16 @@ size_t ws_doubles_unconstr(int N);
 template <typename T>
 hipError_t launch_riccati_unconstr(const ProblemArgsT<T>& a, hipStream_t stream);
 
+// nx < 12 or nu < 12: embed the problem in 12 x 12 stages (pad.hip).  pad_elems
+// is the pad buffer size (elements of T); pad_problem fills it from `a` and
+// returns the padded arguments in `o` (solution pointers into the buffer);
+// unpad_solution copies the solution back into `a`'s buffers.
+size_t pad_elems(int batch, int N, int ng);
+template <typename T>
+hipError_t pad_problem(const ProblemArgsT<T>& a, T* buf, ProblemArgsT<T>& o, hipStream_t s);
+template <typename T>
+hipError_t unpad_solution(const ProblemArgsT<T>& a, const ProblemArgsT<T>& o, hipStream_t s);
+
 }  // namespace srbd
 #include "../../include/srbd_qp.h"
 namespace srbd {

@@ -264,11 +264,9 @@ hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {
   const int threads = 256;
   const long long lanes = (long long)a.batch * kGroup;
   const int blocks = (int)((lanes + threads - 1) / threads);
-  if (a.nx == 12 && a.nu == 12) {
-    hipLaunchKernelGGL(riccati_unconstr_kernel<true>, dim3(blocks), dim3(threads), 0, stream, a);
-  } else {
-    hipLaunchKernelGGL(riccati_unconstr_kernel<false>, dim3(blocks), dim3(threads), 0, stream, a);
-  }
+  // 12 x 12 stages only: smaller problems arrive embedded by pad.hip
+  if (a.nx != 12 || a.nu != 12) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(riccati_unconstr_kernel<true>, dim3(blocks), dim3(threads), 0, stream, a);
   return hipGetLastError();
 }
 

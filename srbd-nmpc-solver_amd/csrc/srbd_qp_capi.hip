@@ -41,6 +41,9 @@ struct srbd_qp_handle_s {
   // host-solve staging (device)
   double* stage = nullptr;
   size_t stage_bytes = 0;
+  // nx < 12 or nu < 12: the 12 x 12 embedding (pad.hip), allocated on first use
+  void* pad = nullptr;
+  size_t pad_bytes = 0;
 };
 
 extern "C" {
@@ -110,8 +113,9 @@ static int check_dims(const srbd_qp_dims* d) {
   if (!d) return fail(SRBD_QP_EINVAL, "dims is NULL");
   if (d->layout != SRBD_QP_LAYOUT_QP_MAJOR && d->layout != SRBD_QP_LAYOUT_STAGE_MAJOR)
     return fail(SRBD_QP_EINVAL, "unknown layout " + std::to_string(d->layout));
-  if (d->layout == SRBD_QP_LAYOUT_STAGE_MAJOR && (d->has_box_u || d->has_box_x || d->ng > 0))
-    return fail(SRBD_QP_EINVAL, "stage-major inputs are supported by the unconstrained solve only");
+  if (d->layout == SRBD_QP_LAYOUT_STAGE_MAJOR &&
+      (d->has_box_u || d->has_box_x || d->ng > 0 || d->nx != 12 || d->nu != 12))
+    return fail(SRBD_QP_EINVAL, "stage-major inputs are supported by the unconstrained 12 x 12 solve only");
   if (d->N < 1 || d->N > 1024)
     return fail(SRBD_QP_EDIM, "N must be in [1, 1024], got " + std::to_string(d->N));
   if (d->nx < 1 || d->nx > SRBD_QP_MAX_NX)
@@ -169,6 +173,7 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->ws) hipFree(h->ws);
   if (h->stage) hipFree(h->stage);
+  if (h->pad) hipFree(h->pad);
   if (h->stream) hipStreamDestroy(h->stream);
   hipSetDevice(prev);
   delete h;
@@ -252,11 +257,27 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   if (s->stat)
     e = hipMemsetAsync(s->stat, 0,
                        sizeof(T) * srbd::kStatCols * (size_t)(st->iter_max + 2) * (size_t)batch, strm);
+  // nx < 12 or nu < 12: solve the problem embedded in 12 x 12 stages
+  const bool padded = a.nx != 12 || a.nu != 12;
+  srbd::ProblemArgsT<T> run = a;
+  if (e == hipSuccess && padded) {
+    const size_t need = srbd::pad_elems(h->capacity, a.N, a.ng) * sizeof(T);
+    if (need > h->pad_bytes) {
+      if (h->pad) hipFree(h->pad);
+      h->pad = nullptr;
+      h->pad_bytes = 0;
+      e = hipMalloc(&h->pad, need);
+      if (e == hipSuccess) h->pad_bytes = need;
+    }
+    if (e == hipSuccess) e = srbd::pad_problem<T>(a, reinterpret_cast<T*>(h->pad), run, strm);
+  }
   if (e != hipSuccess) {
   } else if (constrained(h->dims)) {
-    e = srbd::launch_ipm_box(a, strm);
+    e = srbd::launch_ipm_box(run, strm);
+    if (e == hipSuccess && padded) e = srbd::unpad_solution<T>(a, run, strm);
   } else {
-    e = srbd::launch_riccati_unconstr(a, strm);
+    e = srbd::launch_riccati_unconstr(run, strm);
+    if (e == hipSuccess && padded) e = srbd::unpad_solution<T>(a, run, strm);
     if (e == hipSuccess && (s->res || s->obj)) {
       // an unconstrained solve reports zero residual norms / objective unless
       // computed (compute_residuals is not implemented for nc == 0 yet)
