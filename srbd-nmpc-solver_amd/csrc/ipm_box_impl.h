@@ -190,6 +190,13 @@ struct Ctx {
     if constexpr (GEN == 2) return dot12(Dr, bu, dot12(Cr, bx, real(0.0)));
     return dot12(Dr, bu, real(0.0));
   }
+  // the same with x, u element-owned (broadcast inside the FMAs)
+  __device__ real g_row_dot_b(int k, int ch, int i, real x, real u) const {
+    real Cr[12], Dr[12];
+    g_row(k, ch, i, Cr, Dr);
+    if constexpr (GEN == 2) return dot_bcast(Dr, u, dot_bcast(Cr, x, real(0.0)));
+    return dot_bcast(Dr, u, real(0.0));
+  }
   // column-owned C / D columns restricted to chunk ch (lane j = column)
   __device__ void g_col(int k, int ch, int j, real (&Cc)[12], real (&Dc)[12]) const {
     const int r0 = ch * kMaxDim;
@@ -794,14 +801,10 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       // ---- residuals of stage k (element-owned) ----
       real rgx = real(0.0), rgu = real(0.0), rb = real(0.0);
       {
-        real bxk[12], buk[12], bpn[12];
-        gather12(xk, bxk);
-        gather12(uk, buk);
-        gather12(pin, bpn);
         {
           real Qc[12];
           c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
-          const real qx = dot12(Qc, bxk, real(0.0));
+          const real qx = dot_bcast(Qc, xk, real(0.0));
           const real qk = c.el(c.q() + (size_t)k * nx, nx, li);
           rgx = qx + qk - pik;
           if (k > 0) objl += xk * (real(0.5) * qx + qk);
@@ -812,13 +815,13 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           {
             real M[12];
             c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, M);
-            ru = dot12(M, buk, real(0.0));
+            ru = dot_bcast(M, uk, real(0.0));
           }
           SRBD_RES_FENCE();
           {
             real M[12];
             c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, M);
-            stu = dot12(M, buk, real(0.0));
+            stu = dot_bcast(M, uk, real(0.0));
 #if SRBD_RB_LDS
             lds_put_col(ldsS, lane, M);
 #endif
@@ -827,7 +830,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           {
             real M[12];
             c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, M);
-            btp = dot12(M, bpn, real(0.0));
+            btp = dot_bcast(M, pin, real(0.0));
 #if SRBD_RB_LDS
             lds_put_col(ldsB, lane, M);
 #endif
@@ -836,7 +839,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           {
             real M[12];
             c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, M);
-            atp = dot12(M, bpn, real(0.0));
+            atp = dot_bcast(M, pin, real(0.0));
 #if SRBD_RB_LDS
             lds_put_col(ldsA, lane, M);
 #endif
@@ -852,7 +855,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 #else
             c.row(c.S() + (size_t)k * c.nxu(), nu, nx, li, uel, M);
 #endif
-            sx_ = dot12(M, bxk, real(0.0));
+            sx_ = dot_bcast(M, xk, real(0.0));
           }
           SRBD_RES_FENCE();
           const real rk = c.el(c.r() + (size_t)k * nu, nu, li);
@@ -868,7 +871,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 #else
             c.row(c.A() + (size_t)k * c.nxx(), nx, nx, li, xel, M);
 #endif
-            ax = dot12(M, bxk, real(0.0));
+            ax = dot_bcast(M, xk, real(0.0));
           }
           SRBD_RES_FENCE();
           {
@@ -878,7 +881,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 #else
             c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, M);
 #endif
-            ax = dot12(M, buk, ax);
+            ax = dot_bcast(M, uk, ax);
           }
           SRBD_RES_FENCE();
           rb = ax + c.el(c.b() + (size_t)k * nx, nx, li) - xn;
@@ -898,7 +901,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
               bg.lu += alpha_d * d.dlu;
               store_gbar(g, lane, bg);
             }
-            const real v = c.g_row_dot(k, ch, lane, bxk, buk);
+            const real v = c.g_row_dot_b(k, ch, lane, xk, uk);
             if (lane < kMaxDim) g[kGenVal + lane] = v;
             if (sg.ml != real(0.0)) {
               const real rd = v - sg.lb - bg.tl, rm = bg.ll * bg.tl;
@@ -912,11 +915,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
               mm = fmax(mm, nabs(rm));
               musum += rm;
             }
-            real bdl[12], Cc[12], Dc[12];
-            gather12(lane < kMaxDim ? bg.lu - bg.ll : real(0.0), bdl);
+            real Cc[12], Dc[12];
+            const real dl = lane < kMaxDim ? bg.lu - bg.ll : real(0.0);
             c.g_col(k, ch, col, Cc, Dc);
-            if constexpr (GEN == 2) rgx = dot12(Cc, bdl, rgx);
-            rgu = dot12(Dc, bdl, rgu);
+            if constexpr (GEN == 2) rgx = dot_bcast(Cc, dl, rgx);
+            rgu = dot_bcast(Dc, dl, rgu);
           }
         }
       }
@@ -1157,35 +1160,20 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           }
           const real bt = lane < kMaxDim ? stk[kStRes + 24 + lane] : real(0.0);
           // w = P_{k+1} b~ + p_{k+1}
-          real Pc[12], bb[12];
+          real Pc[12];
           load_packed_sym(recn + kRecP, col, Pc);
-          gather12(bt, bb);
-          real w = pnext;
-          sfor<0, 12>([&](auto j) {
-            constexpr int J = decltype(j)::value;
-            w = fmadd(Pc[J], bb[J], w);
-          });
+          const real w = dot_bcast(Pc, bt, pnext);
           // g = r~ + B'w ; f = q~ + A'w
-          real Bc[12], Ac[12], bw[12];
+          real Bc[12], Ac[12];
           c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, Bc);
           c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, Ac);
-          gather12(w, bw);
           real g = rt, f = qt;
-          sfor<0, 12>([&](auto j) {
-            constexpr int J = decltype(j)::value;
-            g = fmadd(Bc[J], bw[J], g);
-            f = fmadd(Ac[J], bw[J], f);
-          });
+          dot_bcast2(Bc, Ac, w, g, f);
           if (lane >= kMaxDim) g = real(0.0);
           // p = f + K'g  (K column-owned: lane j holds K[:, j])
-          real Kc[12], bg[12];
+          real Kc[12];
           load12(rec + kRecK + col * 12, Kc);
-          gather12(g, bg);
-          real pv = f;
-          sfor<0, 12>([&](auto j) {
-            constexpr int J = decltype(j)::value;
-            pv = fmadd(Kc[J], bg[J], pv);
-          });
+          const real pv = dot_bcast(Kc, g, f);
           // y = L^-1 g (row-owned L), then z = L^-T y (column-owned L), k = -z
           real Lr[12], Lc[12];
           load_packed_lrow(rec + kRecL, li, Lr);
@@ -1206,14 +1194,9 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           });
           const real kv = lane < kMaxDim && uel ? -y : real(0.0);
           // bcl = b~ + B k (row-owned B)
-          real Br[12], bk[12];
+          real Br[12];
           c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
-          gather12(kv, bk);
-          real bcl = bt;
-          sfor<0, 12>([&](auto j) {
-            constexpr int J = decltype(j)::value;
-            bcl = fmadd(Br[J], bk[J], bcl);
-          });
+          const real bcl = dot_bcast(Br, kv, bt);
           if (lane < kMaxDim) {
             rec[kRecKv + lane] = kv;
             rec[kRecBcl + lane] = xel ? bcl : real(0.0);
@@ -1234,15 +1217,13 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       for (int k = 0; k <= N; ++k) {
         real* stk = c.st(k);
         const real* rec = stk + par * kRecSize;
-        real bdx[12];
-        gather12(dxk, bdx);
-        real Pc[12];
-        load_packed_sym(rec + kRecP, col, Pc);
-        real dpi = rec[kRecPv + li];
-        sfor<0, 12>([&](auto j) {
-          constexpr int J = decltype(j)::value;
-          dpi = fmadd(Pc[J], bdx[J], dpi);
-        });
+        // dpi = P dx + p is part of the final step only (F2, or F1 without corrector)
+        real dpi = real(0.0);
+        if (corr || !a.pred_corr) {
+          real Pc[12];
+          load_packed_sym(rec + kRecP, col, Pc);
+          dpi = dot_bcast(Pc, dxk, rec[kRecPv + li]);
+        }
         real du = real(0.0), dxn = real(0.0);
         if (k < N) {
           real Kr[12], Ar[12];
@@ -1253,11 +1234,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           });
           du = rec[kRecKv + li];
           dxn = rec[kRecBcl + li];
-          sfor<0, 12>([&](auto j) {
-            constexpr int J = decltype(j)::value;
-            du = fmadd(Kr[J], bdx[J], du);
-            dxn = fmadd(Ar[J], bdx[J], dxn);
-          });
+          dot_bcast2(Kr, Ar, dxk, du, dxn);
         }
         if (!uel || k == N) du = real(0.0);
         if (!xel) {
@@ -1266,11 +1243,9 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         }
         if constexpr (GEN) {
           // general rows: dv = C dx + D du, dt / dlam, step ratios
-          real bdu[12];
-          gather12(du, bdu);
           for (int ch = 0; ch < c.nch; ++ch) {
             real* g = c.gs(k, ch);
-            const real dv = c.g_row_dot(k, ch, lane, bdx, bdu);
+            const real dv = c.g_row_dot_b(k, ch, lane, dxk, du);
             if (lane < kMaxDim) {
               const Side sg = c.side_g(k, ch, lane);
               const Bar bg = load_gbar(g, lane);
@@ -1312,9 +1287,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           }
           c.put_bstep(stk, 0, lane, nu_);
           c.put_bstep(stk, 1, lane, nx_);
-          stk[kStStep + lane] = du;
-          stk[kStStep + 12 + lane] = dxk;
-          stk[kStStep + 24 + lane] = k > 0 ? dpi : real(0.0);
+          if (corr || !a.pred_corr) {  // the predictor's du / dx / dpi are not used
+            stk[kStStep + lane] = du;
+            stk[kStStep + 12 + lane] = dxk;
+            stk[kStStep + 24 + lane] = k > 0 ? dpi : real(0.0);
+          }
         }
         dxk = dxn;
       }

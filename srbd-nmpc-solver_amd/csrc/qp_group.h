@@ -181,6 +181,115 @@ __device__ __forceinline__ void fma_bcast_lanes(float (&C)[12], float x, float y
       : "v"(x), "v"(y));
 }
 
+// acc + sum_j M[j] * bc<j>(x): a lane's dot product with the row's element-owned
+// vector x (lane j holds x_j), the broadcast riding on src0 of each FMA -- no
+// gathered 12-register copy of x.  Same rounding as fma(M[j], x_j, acc) in
+// order j = 0..11.
+__device__ __forceinline__ double dot_bcast(const double (&M)[12], double x, double acc) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %3 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %4 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %5 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %6 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %7 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %8 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %9 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %10 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %12 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %13 row_newbcast:11 row_mask:0xf bank_mask:0xf"
+      : "+&v"(acc)
+      : "v"(x), "v"(M[0]), "v"(M[1]), "v"(M[2]), "v"(M[3]), "v"(M[4]), "v"(M[5]), "v"(M[6]), "v"(M[7]), "v"(M[8]), "v"(M[9]), "v"(M[10]), "v"(M[11]));
+  return acc;
+}
+__device__ __forceinline__ float dot_bcast(const float (&M)[12], float x, float acc) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f32_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %1, %3 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %1, %4 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %1, %5 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %1, %6 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %1, %7 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %1, %8 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %1, %9 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %1, %10 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %1, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %1, %12 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %1, %13 row_newbcast:11 row_mask:0xf bank_mask:0xf"
+      : "+&v"(acc)
+      : "v"(x), "v"(M[0]), "v"(M[1]), "v"(M[2]), "v"(M[3]), "v"(M[4]), "v"(M[5]), "v"(M[6]), "v"(M[7]), "v"(M[8]), "v"(M[9]), "v"(M[10]), "v"(M[11]));
+  return acc;
+}
+
+// two such dots on the same x, interleaved (two independent FMA chains)
+__device__ __forceinline__ void dot_bcast2(const double (&M1)[12], const double (&M2)[12], double x,
+                                           double& acc1, double& acc2) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %2, %3 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %15 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %4 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %5 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %17 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %6 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %18 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %7 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %19 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %20 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %9 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %21 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %10 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %22 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %23 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %24 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %25 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %14 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %26 row_newbcast:11 row_mask:0xf bank_mask:0xf"
+      : "+&v"(acc1), "+&v"(acc2)
+      : "v"(x), "v"(M1[0]), "v"(M1[1]), "v"(M1[2]), "v"(M1[3]), "v"(M1[4]), "v"(M1[5]), "v"(M1[6]), "v"(M1[7]), "v"(M1[8]), "v"(M1[9]), "v"(M1[10]), "v"(M1[11]),
+        "v"(M2[0]), "v"(M2[1]), "v"(M2[2]), "v"(M2[3]), "v"(M2[4]), "v"(M2[5]), "v"(M2[6]), "v"(M2[7]), "v"(M2[8]), "v"(M2[9]), "v"(M2[10]), "v"(M2[11]));
+}
+__device__ __forceinline__ void dot_bcast2(const float (&M1)[12], const float (&M2)[12], float x,
+                                           float& acc1, float& acc2) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f32_dpp %0, %2, %3 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %15 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %4 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %5 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %17 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %6 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %18 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %7 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %19 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %20 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %9 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %21 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %10 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %22 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %23 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %24 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %25 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %14 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %26 row_newbcast:11 row_mask:0xf bank_mask:0xf"
+      : "+&v"(acc1), "+&v"(acc2)
+      : "v"(x), "v"(M1[0]), "v"(M1[1]), "v"(M1[2]), "v"(M1[3]), "v"(M1[4]), "v"(M1[5]), "v"(M1[6]), "v"(M1[7]), "v"(M1[8]), "v"(M1[9]), "v"(M1[10]), "v"(M1[11]),
+        "v"(M2[0]), "v"(M2[1]), "v"(M2[2]), "v"(M2[3]), "v"(M2[4]), "v"(M2[5]), "v"(M2[6]), "v"(M2[7]), "v"(M2[8]), "v"(M2[9]), "v"(M2[10]), "v"(M2[11]));
+}
+
 template <typename T>
 __device__ __forceinline__ T fmadd(T a, T b, T c) {
   return __builtin_fma(a, b, c);
