@@ -90,36 +90,38 @@ def alg_flops_per_qp(N, nx=12, nu=12):
     return N * (back + fwd)
 
 
-def make_shard(pkg, N, constraints, batch, rank, seed, pool):
-    """Distinct QPs for this rank: a pool of `pool` QPs generated from
-    seed + global index, tiled to `batch` (addresses distinct, data repeats)."""
-    pool = min(pool, batch)
+def make_cpu_sample(pkg, N, constraints, n, rank, batch, seed):
+    """Host copy (numpy) of the first `n` QPs of this rank's shard, for the CPU
+    baseline: the same seed + global index as the device batch."""
     first, _ = pkg.dist.shard_range(rank, batch)
-    qp, x0 = pkg.srbd_model.generate_batch(pool, N=N, seed=seed, constraints=constraints,
-                                           first=first)
-    return qp, x0
+    return pkg.srbd_model.generate_batch(n, N=N, seed=seed, constraints=constraints, first=first)
 
 
-def to_device(pkg, qp, x0, batch, device, np_dtype=np.float64, stage_major=False):
+def device_shard(pkg, h, N, constraints, batch, rank, seed, device, np_dtype=np.float64,
+                 stage_major=False):
+    """Every QP of this rank's shard distinct: linearisation points sampled from
+    seed + global QP index, then linearised on the device by
+    srbd_qp_srbd_linearize_f64 (= prepareQpStructures, NMPC_solver.cpp:276-314;
+    parity with the numpy model at 1e-11, tests/test_gpu_linearize.py).
+    Returns (dict of device tensors in the C-ABI layout incl. x0, xs, us, x0 numpy)."""
     import torch
-    p = {k: (None if v is None else np.ascontiguousarray(v, dtype=np_dtype))
-         for k, v in qp.packed().items()}
-    p["x0"] = np.ascontiguousarray(x0, dtype=np_dtype)
-    pool = qp.batch
-    reps = (batch + pool - 1) // pool
+    first, _ = pkg.dist.shard_range(rank, batch)
+    xs, us, x0 = pkg.srbd_model.sample_trajectories(batch, N, seed, pkg.srbd_model.SrbdParams(), first)
+    xs_t = torch.from_numpy(xs).to(device)
+    us_t = torch.from_numpy(us).to(device)
+    t, _ = pkg.capi.srbd_linearize(h, xs_t, us_t, constraints)
+    h.synchronize()
+    del xs_t, us_t
+    t["x0"] = torch.from_numpy(np.ascontiguousarray(x0)).to(device)
+    tdt = torch.float32 if np_dtype == np.float32 else torch.float64
     dt = {}
-    for k, v in p.items():
-        if v is None:
-            dt[k] = None
-            continue
-        t = torch.from_numpy(v).to(device)
-        if reps > 1:
-            t = t.repeat((reps,) + (1,) * (t.dim() - 1))
-        t = t[:batch]
+    for k, v in t.items():
+        v = v.to(tdt)
         if stage_major and k != "x0":  # [batch][stage][...] -> [stage][batch][...]
-            t = t.transpose(0, 1)
-        dt[k] = t.contiguous()
-    return dt
+            v = v.transpose(0, 1)
+        dt[k] = v.contiguous()
+    torch.cuda.synchronize()
+    return dt, xs, us, x0
 
 
 def main():
@@ -129,7 +131,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default=DEFAULT_WORKLOAD, choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="QPs per rank (default: workload's)")
-    ap.add_argument("--pool", type=int, default=4096, help="distinct QPs generated per rank")
+    ap.add_argument("--cpu-pool", type=int, default=4096, help="QPs in the cpu_baseline sample")
     ap.add_argument("--seed", type=int, default=1003)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -164,15 +166,17 @@ def main():
     batch = args.batch or default_batch
     log(f"[rank {rank}] workload={args.workload} batch/rank={batch} N={N} world={world}")
     t0 = time.perf_counter()
-    qp, x0 = make_shard(pkg, N, constraints, batch, rank, args.seed, args.pool)
     stage_major = args.layout == "stage"
     if stage_major and constraints != "none":
         raise SystemExit("--layout stage: unconstrained workloads only")
-    dt = to_device(pkg, qp, x0, batch, device, np_dtype, stage_major)
-    log(f"[rank {rank}] generated + uploaded in {time.perf_counter() - t0:.1f}s")
-
-    h = capi.Handle(N, 12, 12, qp.ng, qp.has_box_u, qp.has_box_x, capacity=batch, device=local_rank,
+    ng = 24 if constraints == "cone" else 0
+    h = capi.Handle(N, 12, 12, ng, constraints == "box_u", False, capacity=batch, device=local_rank,
                     layout=1 if stage_major else 0)
+    dt, xs_np, us_np, x0_np = device_shard(pkg, h, N, constraints, batch, rank, args.seed, device,
+                                           np_dtype, stage_major)
+    log(f"[rank {rank}] {batch} distinct QPs generated (linearised on device) in "
+        f"{time.perf_counter() - t0:.1f}s")
+
     f64 = dict(dtype=torch.float32 if dtype == "f32" else torch.float64, device=device)
     sol_t = {"x": torch.zeros(batch, N + 1, 12, **f64), "u": torch.zeros(batch, N, 12, **f64),
              "pi": torch.zeros(batch, N + 1, 12, **f64),
@@ -215,7 +219,7 @@ def main():
     # ---- the whole SQP iteration on the device (secondary; not `value`) ----
     pipeline = None
     if not args.no_pipeline and dtype == "f64" and not stage_major:
-        pipeline = sqp_pipeline(pkg, h, N, constraints, batch, args.seed, args.pool, rank, device, settings)
+        pipeline = sqp_pipeline(pkg, h, N, constraints, batch, xs_np, us_np, x0_np, device, settings)
 
     # ---- host buffers in, host buffers out (secondary; PCIe-inclusive, not `value`) ----
     host = None
@@ -250,6 +254,7 @@ def main():
 
     cpu = None
     if not args.no_cpu_baseline:
+        qp, x0 = make_cpu_sample(pkg, N, constraints, min(batch, args.cpu_pool), rank, batch, args.seed)
         cpu = cpu_baseline(pkg, qp, x0, settings_dict(settings), args.cpu_seconds)
         if dtype == "f32":
             cpu["sample"] += " (the oracle computes in fp64)"
@@ -267,8 +272,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": dtype,
-        "data": f"synthetic SRBD linearisations (seed {args.seed}; pool of {min(args.pool, batch)} "
-                f"distinct QPs per rank tiled to the batch), generated per rank",
+        "data": f"synthetic SRBD linearisations (seed {args.seed} + global QP index; every QP of "
+                f"the batch distinct, linearised on the device), generated per rank",
         "config": {"workload": args.workload, "description": desc, "batch_per_gpu": batch,
                    "global_batch": total_qps, "N": N, "nx": 12, "nu": 12, "constraints": constraints,
                    "parallelism": f"dp{world} (independent QP shards)",
@@ -323,20 +328,14 @@ def host_path(capi, h, dt, batch, N, settings, dtype, max_batch=16384, reps=2):
             "host_bytes_moved": nbytes, "status_ok": float((out["status"] == 0).mean())}
 
 
-def sqp_pipeline(pkg, h, N, constraints, batch, seed, pool, rank, device, settings, iters=3):
+def sqp_pipeline(pkg, h, N, constraints, batch, xs, us, x0, device, settings, iters=3):
     """One SQP iteration of NMPCSolver::controlLoop (NMPC_solver.cpp:362-372) for the
     whole batch on the device: srbd_qp_srbd_linearize_f64 -> solve ->
     srbd_qp_srbd_linesearch_f64, timed with HIP events on the handle's stream."""
     import torch
     capi = pkg.capi
-    p = pkg.srbd_model.SrbdParams()
-    pool = min(pool, batch)
-    first, _ = pkg.dist.shard_range(rank, batch)
-    xs, us, x0 = pkg.srbd_model.sample_trajectories(pool, N, seed, p, first)
-    reps = (batch + pool - 1) // pool
-    tile = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device).repeat(
-        (reps,) + (1,) * (a.ndim - 1))[:batch].contiguous()
-    xs_t, us_t, x0_t = tile(xs), tile(us), tile(x0)
+    up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    xs_t, us_t, x0_t = up(xs), up(us), up(x0)
     alpha = torch.ones(batch, dtype=torch.float64, device=device)
     f64 = dict(dtype=torch.float64, device=device)
     sol = {"x": torch.zeros(batch, N + 1, 12, **f64), "u": torch.zeros(batch, N, 12, **f64),
