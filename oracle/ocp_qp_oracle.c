@@ -761,7 +761,28 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
     if (!set->split_step) { ap = fmin(ap, ad); ad = ap; }
     ap = fmin(1.0, IPM_STEP_TAU * ap);
     ad = fmin(1.0, IPM_STEP_TAU * ad);
+    /* a step with a NaN component, or one too large to square (a factorization
+     * that broke down), is not a direction: no step, and the next exit test
+     * stops with MinStepLengthReached (the HIP kernel's rule, ipm_box_impl.h) */
+    {
+      int bad = 0;
+#define HUGE_STEP(v) (!(fabs(v) < 1.3e150))
+      for (int s = 0; s <= N; ++s) {
+        for (int i = 0; i < nx; ++i)
+          bad |= HUGE_STEP(dx[(size_t)s * nx + i]) | HUGE_STEP(dpi[(size_t)s * nx + i]);
+        if (s < N)
+          for (int i = 0; i < nu; ++i) bad |= HUGE_STEP(du[(size_t)s * nu + i]);
+        for (int i = 0; i < st[s].nrow; ++i) {
+          row_t* rw = &st[s].rows[i];
+          if (rw->has_l) bad |= HUGE_STEP(rw->dt_l) | HUGE_STEP(rw->dlam_l);
+          if (rw->has_u) bad |= HUGE_STEP(rw->dt_u) | HUGE_STEP(rw->dlam_u);
+        }
+      }
+#undef HUGE_STEP
+      if (bad) ap = ad = 0.0;
+    }
     alpha_prim = ap; alpha_dual = ad;
+    if (ap == 0.0 && ad == 0.0) { ++iter; continue; }
     /* update */
     for (int s = 1; s <= N; ++s)
       for (int i = 0; i < nx; ++i) x[(size_t)s * nx + i] += ap * dx[(size_t)s * nx + i];

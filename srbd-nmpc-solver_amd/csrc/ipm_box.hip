@@ -9,23 +9,27 @@
 // (:60).  The arithmetic is restated in oracle/ocp_qp_oracle.c (ipm loop), the
 // parity reference.
 //
-// One 16-lane group per QP runs the whole IPM; a wavefront advances four QPs
-// and idles groups that have exited.  Each iteration is six sweeps over the
-// horizon (k = stage):
-//   RU  k = 0..N  apply the previous step, residuals res_g / res_b / res_d /
-//                 res_m at the new iterate (element-owned), norms, mu, obj
-//   B1  k = N..0  Gamma / gamma (predictor), factorize the barrier-augmented
-//                 KKT system with riccati_step (column-owned), write the stage
-//                 record {L, K, Acl, P, 1/diag L, k, bcl, p}
+// One 16-lane group per QP runs the whole IPM; a wavefront advances four QPs.
+// The iteration is host-driven, one launch per pair of sweeps over the horizon
+// (k = stage), with per-QP state in the workspace (a QP that has exited returns
+// at the top of every later launch):
+//   RB  k = N..0  apply the previous step to stage k, its residuals res_g /
+//                 res_b / res_d / res_m (norms, mu, obj), Gamma / gamma, and the
+//                 barrier-augmented factorization (riccati_step) writing the
+//                 stage record {L, K, Acl, P, 1/diag L, k, bcl, p}.  Every QP
+//                 block is read from global memory once per iteration; the
+//                 row-owned residual products go through LDS.  After the sweep:
+//                 exit test (NaN, converged, iter_max, min step).
 //   F1  k = 0..N  predictor step (row-owned from the record), dt / dlam,
-//                 alpha_aff
-//   M   k = 0..N  mu_aff -> sigma = (mu_aff / mu)^3
+//                 alpha_aff and the mu_aff sums -> sigma = (mu_aff / mu)^3
 //   B2  k = N..0  corrector right-hand side, vector-only Riccati recursion
 //                 reusing the record (element-owned)
 //   F2  k = 0..N  corrector step, dt / dlam, alpha_prim / alpha_dual
+// RB + F1 and B2 + F2 run as one launch each (ipm_phase2_kernel).
 // Box bounds are dense per variable (include/srbd_qp.h), so bound i of u_k /
 // x_k lives on lane i next to u_k[i] / x_k[i]: every constraint operation is
 // lane-local and the barrier Hessian only touches the diagonals of R and Q.
+// General rows (D u + C x, ng <= 64) go in 12-row chunks, lane i = row i.
 #include "kernels.h"
 #include "riccati.h"
 

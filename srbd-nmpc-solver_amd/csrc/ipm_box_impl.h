@@ -6,12 +6,6 @@
 #ifndef SRBD_IPM_FUSE
 #define SRBD_IPM_FUSE 1
 #endif
-#ifndef SRBD_RB_LDS
-#define SRBD_RB_LDS 0
-#endif
-#ifndef SRBD_RES_FENCE
-#define SRBD_RES_FENCE() SRBD_PHASE_FENCE()
-#endif
 namespace srbd {
 namespace SRBD_NS {
 
@@ -49,6 +43,13 @@ __device__ __forceinline__ real gmin(real v) {
   v = fmin(v, __shfl_xor(v, 1, kGroup));
   return v;
 }
+// NaN, or too large to square in this precision (sqrt(max) / 1e4: 1.8e15 in fp32)
+__device__ __forceinline__ bool huge(real v) {
+  constexpr real kHuge = sizeof(real) == 4 ? real(1.8e15) : real(1.3e150);
+  return !(__builtin_fabs(v) < kHuge);
+}
+// v + a d, with a = 0 (no step taken) leaving v as it is whatever d holds
+__device__ __forceinline__ real step(real v, real a, real d) { return a != real(0.0) ? fmadd(a, d, v) : v; }
 // |v| propagating NaN (max with NaN would drop it)
 __device__ __forceinline__ real nabs(real v) { return v == v ? fabs(v) : real(__builtin_inf()); }
 
@@ -742,23 +743,16 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     // and factorizes its barrier-augmented block right away, so the QP data is
     // streamed once per iteration.  If the exit test after the sweep fires, this
     // sweep's factorization is simply not used (outputs read the other parity).
-#if SRBD_RB_LDS
-    // A, B, S of the current stage, staged once per stage through LDS: the
-    // residuals read them row-owned, the factorization column-owned, and the
-    // second pass no longer goes back to L2 / HBM (one QP group: 3 x 144 reals)
-    // (addresses re-derived through an opaque copy at every use, like c.oq(),
-    // so the LDS reads cannot be hoisted into one long-lived register block)
+    // Every 12 x 12 block of stage k is read from global memory once: column-owned,
+    // as the factorization needs it.  The residual products take the same
+    // registers where they are column-shaped (Q x, R u, S'u, A'pi, B'pi: symmetric
+    // or transposed) and a row-owned copy through LDS where they are not (A x, B u,
+    // S x); S stays in LDS until the factorization's second phase asks for it.
+    // LDS per QP group: A, B, S columns (3 x 144 reals).
     __shared__ real rb_lds[(256 / kGroup) * 3 * 144];
-    const int lds_off = (threadIdx.x / kGroup) * 3 * 144;
-    auto lds_at = [&](int blk) {
-      int o = lds_off + blk * 144;
-      asm volatile("" : "+v"(o));
-      return rb_lds + o;
-    };
-#define ldsA lds_at(0)
-#define ldsB lds_at(1)
-#define ldsS lds_at(2)
-#endif
+    real* const ldsA = rb_lds + (threadIdx.x / kGroup) * 3 * 144;
+    real* const ldsB = ldsA + 144;
+    real* const ldsS = ldsA + 288;
     real mg = real(0.0), mb = real(0.0), md = real(0.0), mm = real(0.0), musum = real(0.0), objl = real(0.0);
     real xn = real(0.0), pin = real(0.0);  // updated x_{k+1}, pi_{k+1} (element-owned), from stage k+1
     real P[12];
@@ -768,15 +762,15 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       // ---- apply the previous step to stage k ----
       real uk = real(0.0), xk = real(0.0), pik = real(0.0);
       if (k < N && uel) {
-        uk = c.u()[(size_t)k * nu + lane] + alpha_p * stk[kStStep + lane];
+        uk = step(c.u()[(size_t)k * nu + lane], alpha_p, stk[kStStep + lane]);
         c.u()[(size_t)k * nu + lane] = uk;
       }
       if (xel) {
         if (k == 0) {
           xk = c.x()[li];  // x_0 = x0 (never updated); pi_0 is not an iterate
         } else {
-          xk = c.x()[(size_t)k * nx + lane] + alpha_p * stk[kStStep + 12 + lane];
-          pik = c.pi()[(size_t)k * nx + lane] + alpha_d * stk[kStStep + 24 + lane];
+          xk = step(c.x()[(size_t)k * nx + lane], alpha_p, stk[kStStep + 12 + lane]);
+          pik = step(c.pi()[(size_t)k * nx + lane], alpha_d, stk[kStStep + 24 + lane]);
           c.x()[(size_t)k * nx + lane] = xk;
           c.pi()[(size_t)k * nx + lane] = pik;
         }
@@ -787,140 +781,55 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         bu = c.bar(stk, 0, lane);
         bx = c.bar(stk, 1, lane);
         const BarStep du = c.bstep(stk, 0, lane), dx = c.bstep(stk, 1, lane);
-        bu.tl += alpha_p * du.dtl;
-        bu.tu += alpha_p * du.dtu;
-        bu.ll += alpha_d * du.dll;
-        bu.lu += alpha_d * du.dlu;
-        bx.tl += alpha_p * dx.dtl;
-        bx.tu += alpha_p * dx.dtu;
-        bx.ll += alpha_d * dx.dll;
-        bx.lu += alpha_d * dx.dlu;
+        bu.tl = step(bu.tl, alpha_p, du.dtl);
+        bu.tu = step(bu.tu, alpha_p, du.dtu);
+        bu.ll = step(bu.ll, alpha_d, du.dll);
+        bu.lu = step(bu.lu, alpha_d, du.dlu);
+        bx.tl = step(bx.tl, alpha_p, dx.dtl);
+        bx.tu = step(bx.tu, alpha_p, dx.dtu);
+        bx.ll = step(bx.ll, alpha_d, dx.dll);
+        bx.lu = step(bx.lu, alpha_d, dx.dlu);
         c.put_bar(stk, 0, lane, bu);
         c.put_bar(stk, 1, lane, bx);
       }
-      // ---- residuals of stage k (element-owned) ----
-      real rgx = real(0.0), rgu = real(0.0), rb = real(0.0);
-      {
-        {
-          real Qc[12];
-          c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
-          const real qx = dot_bcast(Qc, xk, real(0.0));
-          const real qk = c.el(c.q() + (size_t)k * nx, nx, li);
-          rgx = qx + qk - pik;
-          if (k > 0) objl += xk * (real(0.5) * qx + qk);
-        }
-        if (k < N) {
-          // one block at a time (fenced) so that at most two 12-arrays are in flight
-          real ru, sx_, stu, btp, atp;
-          {
-            real M[12];
-            c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, M);
-            ru = dot_bcast(M, uk, real(0.0));
+      // ---- residual terms without the stage blocks (element-owned) ----
+      const real qk = c.el(c.q() + (size_t)k * nx, nx, li);
+      const real rk = k < N ? c.el(c.r() + (size_t)k * nu, nu, li) : real(0.0);
+      real rgx = qk - pik, rgu = rk;
+      if constexpr (GEN) {
+        // general rows: apply the step, residuals, res_g += C'(lam_u - lam_l), D'(..)
+        for (int ch = 0; ch < c.nch; ++ch) {
+          real* g = c.gs(k, ch);
+          const Side sg = c.side_g(k, ch, lane);
+          Bar bg{0, 0, 1, 1};
+          if (lane < kMaxDim) {
+            bg = load_gbar(g, lane);
+            const BarStep d = load_gstep(g, lane);
+            bg.tl = step(bg.tl, alpha_p, d.dtl);
+            bg.tu = step(bg.tu, alpha_p, d.dtu);
+            bg.ll = step(bg.ll, alpha_d, d.dll);
+            bg.lu = step(bg.lu, alpha_d, d.dlu);
+            store_gbar(g, lane, bg);
           }
-          SRBD_RES_FENCE();
-          {
-            real M[12];
-            c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, M);
-            stu = dot_bcast(M, uk, real(0.0));
-#if SRBD_RB_LDS
-            lds_put_col(ldsS, lane, M);
-#endif
+          const real v = c.g_row_dot_b(k, ch, lane, xk, uk);
+          if (lane < kMaxDim) g[kGenVal + lane] = v;
+          if (sg.ml != real(0.0)) {
+            const real rd = v - sg.lb - bg.tl, rm = bg.ll * bg.tl;
+            md = fmax(md, nabs(rd));
+            mm = fmax(mm, nabs(rm));
+            musum += rm;
           }
-          SRBD_RES_FENCE();
-          {
-            real M[12];
-            c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, M);
-            btp = dot_bcast(M, pin, real(0.0));
-#if SRBD_RB_LDS
-            lds_put_col(ldsB, lane, M);
-#endif
+          if (sg.mu != real(0.0)) {
+            const real rd = sg.ub - v - bg.tu, rm = bg.lu * bg.tu;
+            md = fmax(md, nabs(rd));
+            mm = fmax(mm, nabs(rm));
+            musum += rm;
           }
-          SRBD_RES_FENCE();
-          {
-            real M[12];
-            c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, M);
-            atp = dot_bcast(M, pin, real(0.0));
-#if SRBD_RB_LDS
-            lds_put_col(ldsA, lane, M);
-#endif
-          }
-          SRBD_RES_FENCE();
-#if SRBD_RB_LDS
-          lds_wave_fence();
-#endif
-          {
-            real M[12];
-#if SRBD_RB_LDS
-            lds_get_row(ldsS, li, M);
-#else
-            c.row(c.S() + (size_t)k * c.nxu(), nu, nx, li, uel, M);
-#endif
-            sx_ = dot_bcast(M, xk, real(0.0));
-          }
-          SRBD_RES_FENCE();
-          const real rk = c.el(c.r() + (size_t)k * nu, nu, li);
-          rgu = ru + sx_ + rk + btp;
-          rgx += stu + atp;
-          objl += uk * (real(0.5) * ru + rk + sx_);
-          // res_b = A x + B u + b - x_{k+1} (row-owned A, B)
-          real ax;
-          {
-            real M[12];
-#if SRBD_RB_LDS
-            lds_get_row(ldsA, li, M);
-#else
-            c.row(c.A() + (size_t)k * c.nxx(), nx, nx, li, xel, M);
-#endif
-            ax = dot_bcast(M, xk, real(0.0));
-          }
-          SRBD_RES_FENCE();
-          {
-            real M[12];
-#if SRBD_RB_LDS
-            lds_get_row(ldsB, li, M);
-#else
-            c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, M);
-#endif
-            ax = dot_bcast(M, uk, ax);
-          }
-          SRBD_RES_FENCE();
-          rb = ax + c.el(c.b() + (size_t)k * nx, nx, li) - xn;
-        }
-        if constexpr (GEN) {
-          // general rows: apply the step, residuals, res_g += C'(lam_u - lam_l), D'(..)
-          for (int ch = 0; ch < c.nch; ++ch) {
-            real* g = c.gs(k, ch);
-            const Side sg = c.side_g(k, ch, lane);
-            Bar bg{0, 0, 1, 1};
-            if (lane < kMaxDim) {
-              bg = load_gbar(g, lane);
-              const BarStep d = load_gstep(g, lane);
-              bg.tl += alpha_p * d.dtl;
-              bg.tu += alpha_p * d.dtu;
-              bg.ll += alpha_d * d.dll;
-              bg.lu += alpha_d * d.dlu;
-              store_gbar(g, lane, bg);
-            }
-            const real v = c.g_row_dot_b(k, ch, lane, xk, uk);
-            if (lane < kMaxDim) g[kGenVal + lane] = v;
-            if (sg.ml != real(0.0)) {
-              const real rd = v - sg.lb - bg.tl, rm = bg.ll * bg.tl;
-              md = fmax(md, nabs(rd));
-              mm = fmax(mm, nabs(rm));
-              musum += rm;
-            }
-            if (sg.mu != real(0.0)) {
-              const real rd = sg.ub - v - bg.tu, rm = bg.lu * bg.tu;
-              md = fmax(md, nabs(rd));
-              mm = fmax(mm, nabs(rm));
-              musum += rm;
-            }
-            real Cc[12], Dc[12];
-            const real dl = lane < kMaxDim ? bg.lu - bg.ll : real(0.0);
-            c.g_col(k, ch, col, Cc, Dc);
-            if constexpr (GEN == 2) rgx = dot_bcast(Cc, dl, rgx);
-            rgu = dot_bcast(Dc, dl, rgu);
-          }
+          real Cc[12], Dc[12];
+          const real dl = lane < kMaxDim ? bg.lu - bg.ll : real(0.0);
+          c.g_col(k, ch, col, Cc, Dc);
+          if constexpr (GEN == 2) rgx = dot_bcast(Cc, dl, rgx);
+          rgu = dot_bcast(Dc, dl, rgu);
         }
       }
       // box terms
@@ -952,41 +861,49 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         mm = fmax(mm, nabs(rm));
         musum += rm;
       }
-      if (!xel) rgx = real(0.0);
-      if (!uel) rgu = real(0.0);
-      if (k < N) {
-        mg = fmax(mg, nabs(rgu));
-        mb = fmax(mb, nabs(xel ? rb : real(0.0)));
-      }
-      if (k > 0) mg = fmax(mg, nabs(rgx));
-      if (!xel) rb = real(0.0);
-      if (lane < kMaxDim) {
-        stk[kStRes + lane] = rgu;
-        stk[kStRes + 12 + lane] = rgx;
-        stk[kStRes + 24 + lane] = rb;
-      }
-      SRBD_PHASE_FENCE();
-      // ---- predictor Gamma / gamma, factorization of stage k ----
+      // predictor Gamma / gamma of the bounds and general rows
       real Gu = real(0.0), gu = real(0.0), Gx = real(0.0), gx = real(0.0);
       if (lane < kMaxDim) {
         gamma_of(su, bu, uk, real(0.0), real(0.0), real(0.0), Gu, gu);
         gamma_of(sx, bx, xk, real(0.0), real(0.0), real(0.0), Gx, gx);
       }
-      real rt = lane < kMaxDim ? rgu + gu : real(0.0);
-      real qt = lane < kMaxDim ? rgx + gx : real(0.0);
       if constexpr (GEN) {
         real ra, qa;
         g_grad(k, false, real(0.0), ra, qa);
-        if (lane < kMaxDim) {
-          rt += ra;
-          qt += qa;
-        }
+        gu += ra;
+        gx += qa;
       }
+      // residuals -> stk[kStRes] and the norms, each as soon as it is complete;
+      // the Newton right-hand sides are r~ = res_g,u + gamma_u, q~ = res_g,x + gamma_x
+      auto finish_u = [&](real rgu_) -> real {
+        if (!uel) rgu_ = real(0.0);
+        mg = fmax(mg, nabs(rgu_));
+        if (lane < kMaxDim) stk[kStRes + lane] = rgu_;
+        return lane < kMaxDim ? rgu_ + gu : real(0.0);
+      };
+      auto finish_x = [&](real rgx_) -> real {
+        if (!xel) rgx_ = real(0.0);
+        if (k > 0) mg = fmax(mg, nabs(rgx_));
+        if (lane < kMaxDim) stk[kStRes + 12 + lane] = rgx_;
+        return lane < kMaxDim ? rgx_ + gx : real(0.0);
+      };
+      auto finish_b = [&](real rb_) -> real {
+        if (!xel) rb_ = real(0.0);
+        if (k < N) mb = fmax(mb, nabs(rb_));
+        if (lane < kMaxDim) stk[kStRes + 24 + lane] = rb_;
+        return rb_;
+      };
+      SRBD_PHASE_FENCE();
       if (k == N) {
         // terminal stage: P_N = Q_N + diag(Gamma_x) (+ C'Gamma C), p_N = q~_N
+        c.col(c.Q() + (size_t)N * c.nxx(), nx, col, xel, P);
+        const real qx = dot_bcast(P, xk, real(0.0));
+        if (k > 0) objl += xk * (real(0.5) * qx + qk);
+        finish_u(real(0.0));  // no u_N: res_g,u = 0
+        finish_b(real(0.0));
+        const real qt = finish_x(rgx + qx);
         real qv[12];
         gather12(qt, qv);
-        c.col(c.Q() + (size_t)N * c.nxx(), nx, col, xel, P);
         if constexpr (GEN == 2) g_hess(N, 2, P, P);
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
@@ -996,16 +913,36 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
         if (c.isv) store12(rec + kRecPv, P);
       } else {
-        real bv[12];
-        gather12(rb, bv);
+        // ---- A, B (kept by the factorization), S (kept in LDS): residual products ----
         real A_[12], B_[12];
-#if SRBD_RB_LDS >= 2
-        lds_get_col(ldsA, col, A_);
-        lds_get_col(ldsB, col, B_);
-#else
         c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, A_);
         c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, B_);
-#endif
+        rgx = dot_bcast(A_, pin, rgx);  // + A'pi_{k+1}
+        rgu = dot_bcast(B_, pin, rgu);  // + B'pi_{k+1}
+        lds_put_col(ldsA, lane, A_);
+        lds_put_col(ldsB, lane, B_);
+        real sxu;  // (S x)_l
+        {
+          real Sc[12];
+          c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, Sc);
+          rgx = dot_bcast(Sc, uk, rgx);  // + S'u
+          lds_put_col(ldsS, lane, Sc);
+        }
+        lds_wave_fence();
+        real rb;  // res_b = A x + B u + b - x_{k+1}
+        {
+          real M[12];
+          lds_get_row(ldsA, li, M);
+          rb = dot_bcast(M, xk, c.el(c.b() + (size_t)k * nx, nx, li) - xn);
+          lds_get_row(ldsB, li, M);
+          rb = dot_bcast(M, uk, rb);
+          lds_get_row(ldsS, li, M);
+          sxu = dot_bcast(M, xk, real(0.0));
+        }
+        rgu += sxu;
+        rb = finish_b(rb);
+        real bv[12];
+        gather12(rb, bv);
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
           if (c.isv) {
@@ -1013,8 +950,13 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             B_[I] = real(0.0);
           }
         });
+        SRBD_PHASE_FENCE();
+        real rt = real(0.0);
         auto loadR = [&](real (&Rc)[12]) {
           c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, Rc);
+          const real ru = dot_bcast(Rc, uk, real(0.0));  // R u, before the barrier Hessian goes in
+          objl += uk * (real(0.5) * ru + rk + sxu);
+          rt = finish_u(rgu + ru);
           if constexpr (GEN) g_hess(k, 0, Rc, Rc);
           sfor<0, 12>([&](auto i) {
             constexpr int I = decltype(i)::value;
@@ -1023,12 +965,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           });
         };
         auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
-#if SRBD_RB_LDS >= 2
           lds_get_col(ldsS, col, Sc);
-#else
-          c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, Sc);
-#endif
           c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
+          const real qx = dot_bcast(Qc, xk, real(0.0));
+          if (k > 0) objl += xk * (real(0.5) * qx + qk);
+          const real qt = finish_x(rgx + qx);
           if constexpr (GEN == 2) g_hess(k, 1, Sc, Qc);  // C = 0: D'Gamma C = C'Gamma C = 0
           sfor<0, 12>([&](auto i) {
             constexpr int I = decltype(i)::value;
@@ -1058,6 +999,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           constexpr int I = decltype(i)::value;
           P[I] = f.F[I];
         });
+        // the next stage overwrites this group's LDS blocks: reads done first
+        lds_wave_fence();
       }
       xn = xk;
       pin = pik;
@@ -1107,11 +1050,6 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       qs[kQsStatus] = (real)status;
     }
 
-#if SRBD_RB_LDS
-#undef ldsA
-#undef ldsB
-#undef ldsS
-#endif
     return;
   }
   const real mu = qs[kQsMu], musum_all = qs[kQsMuSum];
@@ -1210,6 +1148,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     constexpr bool corr = PH == kPhF2;
     real ap = real(1e30), ad = real(1e30);
     real s1 = real(0.0), s2 = real(0.0);  // predictor sums lam dt + t dlam, dlam dt (element-owned)
+    bool bad = false;  // a non-finite component in the final step (fp32 breakdown)
       // ---- forward step (F1 predictor / F2 corrector), row-owned ----
       ap = real(1e30);
       ad = real(1e30);
@@ -1257,6 +1196,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
                 sm = sigma_mu;
               }
               const BarStep d = bar_step(sg, bg, g[kGenVal + lane], dv, el, eu, sm);
+              bad |= huge(d.dtl) || huge(d.dtu) || huge(d.dll) || huge(d.dlu);
               ratio(sg, bg, d, ap, ad);
               if (!corr) aff_sums(sg, bg, d, s1, s2);
               store_gstep(g, lane, d);
@@ -1288,6 +1228,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           c.put_bstep(stk, 0, lane, nu_);
           c.put_bstep(stk, 1, lane, nx_);
           if (corr || !a.pred_corr) {  // the predictor's du / dx / dpi are not used
+            bad |= huge(du) || huge(dxk) || huge(dpi) || huge(nu_.dtl) || huge(nu_.dtu) ||
+                   huge(nu_.dll) || huge(nu_.dlu);
             stk[kStStep + lane] = du;
             stk[kStStep + 12 + lane] = dxk;
             stk[kStStep + 24 + lane] = k > 0 ? dpi : real(0.0);
@@ -1317,6 +1259,14 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       // ---- step length of the iteration ----
       ap = gmin(lane < kMaxDim ? ap : real(1e30));
       ad = gmin(lane < kMaxDim ? ad : real(1e30));
+      // A step with a NaN component, or one whose square overflows the precision (an
+      // fp32 factorization that broke down on a barrier Hessian of ~1e10), is not a
+      // direction: take none, so the iterate stays finite and the next exit test stops
+      // with MinStepLengthReached.
+      if (gmax((lane < kMaxDim && bad) ? real(1.0) : real(0.0)) > real(0.0)) {
+        ap = real(0.0);
+        ad = real(0.0);
+      }
       if (!a.split_step) {
         ap = fmin(ap, ad);
         ad = ap;
