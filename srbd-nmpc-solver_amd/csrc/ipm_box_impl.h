@@ -295,10 +295,11 @@ __device__ __forceinline__ void lds_get_row(const real* blk, int r, real (&v)[12
     v[J] = blk[J * 12 + r];
   });
 }
-// the group's lanes exchange data through LDS inside one wave: keep the
-// compiler from moving the reads above the writes (no instruction emitted)
+// the group's lanes exchange data through LDS inside one wave: LDS executes a
+// wave's instructions in order, so only the compiler must not move the reads
+// above the writes (a compiler-only barrier: no wait on outstanding global loads)
 __device__ __forceinline__ void lds_wave_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  asm volatile("" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -796,8 +797,14 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       const real qk = c.el(c.q() + (size_t)k * nx, nx, li);
       const real rk = k < N ? c.el(c.r() + (size_t)k * nu, nu, li) : real(0.0);
       real rgx = qk - pik, rgu = rk;
+      // general rows, one pass per 12-row chunk with C / D read once: apply the
+      // step, row values (row-owned through LDS), res_d / res_m, res_g += C'(lam_u -
+      // lam_l) / D'(..), predictor Gamma / gamma, gradient adds C'gamma / D'gamma and
+      // (GEN == 1) the Hessian add D'Gamma D, accumulated for the factorization
+      real gra = real(0.0), gqa = real(0.0);  // D'gamma, C'gamma (lane j)
+      real RG[12];                            // D'Gamma D, column j (GEN == 1)
+      sfor<0, 12>([&](auto i) { RG[decltype(i)::value] = real(0.0); });
       if constexpr (GEN) {
-        // general rows: apply the step, residuals, res_g += C'(lam_u - lam_l), D'(..)
         for (int ch = 0; ch < c.nch; ++ch) {
           real* g = c.gs(k, ch);
           const Side sg = c.side_g(k, ch, lane);
@@ -811,7 +818,23 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             bg.lu = step(bg.lu, alpha_d, d.dlu);
             store_gbar(g, lane, bg);
           }
-          const real v = c.g_row_dot_b(k, ch, lane, xk, uk);
+          real Cc[12], Dc[12];
+          c.g_col(k, ch, col, Cc, Dc);
+          // row i of the chunk on lane i: v = C x + D u
+          real v;
+          {
+            real M[12];
+            lds_put_col(ldsA, lane, Dc);
+            if constexpr (GEN == 2) lds_put_col(ldsB, lane, Cc);
+            lds_wave_fence();
+            lds_get_row(ldsA, li, M);
+            v = dot_bcast(M, uk, real(0.0));
+            if constexpr (GEN == 2) {
+              lds_get_row(ldsB, li, M);
+              v = dot_bcast(M, xk, v);
+            }
+            lds_wave_fence();
+          }
           if (lane < kMaxDim) g[kGenVal + lane] = v;
           if (sg.ml != real(0.0)) {
             const real rd = v - sg.lb - bg.tl, rm = bg.ll * bg.tl;
@@ -825,11 +848,24 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             mm = fmax(mm, nabs(rm));
             musum += rm;
           }
-          real Cc[12], Dc[12];
+          real G = real(0.0), gg = real(0.0);
+          if (lane < kMaxDim) gamma_of(sg, bg, v, real(0.0), real(0.0), real(0.0), G, gg);
           const real dl = lane < kMaxDim ? bg.lu - bg.ll : real(0.0);
-          c.g_col(k, ch, col, Cc, Dc);
-          if constexpr (GEN == 2) rgx = dot_bcast(Cc, dl, rgx);
+          if constexpr (GEN == 2) {
+            rgx = dot_bcast(Cc, dl, rgx);
+            gqa = dot_bcast(Cc, gg, gqa);
+          }
           rgu = dot_bcast(Dc, dl, rgu);
+          gra = dot_bcast(Dc, gg, gra);
+          if constexpr (GEN == 1) {
+            real Gb[12], Y[12];
+            gather12(G, Gb);
+            sfor<0, 12>([&](auto i) {
+              constexpr int I = decltype(i)::value;
+              Y[I] = Gb[I] * Dc[I];
+            });
+            tmul_acc(Dc, Y, RG);
+          }
         }
       }
       // box terms
@@ -867,12 +903,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         gamma_of(su, bu, uk, real(0.0), real(0.0), real(0.0), Gu, gu);
         gamma_of(sx, bx, xk, real(0.0), real(0.0), real(0.0), Gx, gx);
       }
-      if constexpr (GEN) {
-        real ra, qa;
-        g_grad(k, false, real(0.0), ra, qa);
-        gu += ra;
-        gx += qa;
-      }
+      gu += gra;
+      gx += gqa;
       // residuals -> stk[kStRes] and the norms, each as soon as it is complete;
       // the Newton right-hand sides are r~ = res_g,u + gamma_u, q~ = res_g,x + gamma_x
       auto finish_u = [&](real rgu_) -> real {
@@ -957,7 +989,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           const real ru = dot_bcast(Rc, uk, real(0.0));  // R u, before the barrier Hessian goes in
           objl += uk * (real(0.5) * ru + rk + sxu);
           rt = finish_u(rgu + ru);
-          if constexpr (GEN) g_hess(k, 0, Rc, Rc);
+          if constexpr (GEN == 1) {
+            sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] += RG[decltype(i)::value]; });
+          } else if constexpr (GEN == 2) {
+            g_hess(k, 0, Rc, Rc);
+          }
           sfor<0, 12>([&](auto i) {
             constexpr int I = decltype(i)::value;
             if (lane == I) Rc[I] += (I < nu) ? Gu : real(1.0);  // padded inputs: R = 1
