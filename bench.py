@@ -141,6 +141,8 @@ def main():
                          "unconstrained workloads only)")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the host-buffer (PCIe-inclusive) measurement")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the IPM workloads (configs 3 and 5) measured beside the default line")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip the on-device SQP-iteration measurement (linearise + solve + line search)")
     args = ap.parse_args()
@@ -259,6 +261,14 @@ def main():
         if dtype == "f32":
             cpu["sample"] += " (the oracle computes in fp64)"
 
+    # ---- the IPM configurations (BASELINE configs 3 and 5) beside the default line ----
+    secondary = None
+    if not args.no_secondary and world == 1 and args.workload == DEFAULT_WORKLOAD:
+        del h, dt, data, sol, sol_t
+        torch.cuda.empty_cache()
+        secondary = {w: secondary_workload(pkg, capi, w, device, args.seed)
+                     for w in ("box_u_n20", "cone_n40_f32")}
+
     traffic = pmc_traffic(args.workload, batch)
     line = {
         "metric": METRIC,
@@ -289,6 +299,8 @@ def main():
         "iters_mean": float(iters.mean()), "iters_max": int(iters.max()),
         "cpu_baseline": cpu,
     }
+    if secondary is not None:
+        line["ipm_workloads"] = secondary
     if pipeline is not None:
         line["sqp_pipeline"] = pipeline
     if host is not None:
@@ -300,6 +312,63 @@ def main():
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1):
+    """One IPM workload (its own handle and synthetic shard) timed the same way as
+    the main line: kernel time from HIP events on the handle's stream, wall time
+    around `steps` solves.  Reported beside `value`, never as it."""
+    import torch
+    N, constraints, batch, desc = WORKLOADS[name][:4]
+    dtype = WORKLOADS[name][4] if len(WORKLOADS[name]) > 4 else "f64"
+    ng = 24 if constraints == "cone" else 0
+    h = capi.Handle(N, 12, 12, ng, constraints == "box_u", False, capacity=batch,
+                    device=device.index or 0)
+    dt, _, _, _ = device_shard(pkg, h, N, constraints, batch, 0, seed, device,
+                               np.float32 if dtype == "f32" else np.float64)
+    tt = dict(dtype=torch.float32 if dtype == "f32" else torch.float64, device=device)
+    sol_t = {"x": torch.zeros(batch, N + 1, 12, **tt), "u": torch.zeros(batch, N, 12, **tt),
+             "pi": torch.zeros(batch, N + 1, 12, **tt),
+             "status": torch.zeros(batch, dtype=torch.int32, device=device),
+             "iter": torch.zeros(batch, dtype=torch.int32, device=device)}
+    DataT, SolT = (capi.Data32, capi.Solution32) if dtype == "f32" else (capi.Data, capi.Solution)
+    data = DataT(**{k: (None if dt.get(k) is None else dt[k].data_ptr()) for k in capi.DATA_FIELDS})
+    sol = SolT(**{k: (sol_t[k].data_ptr() if k in sol_t else None) for k in capi.SOL_FIELDS})
+    settings = capi.settings_struct(F32_SETTINGS if dtype == "f32" else NMPC_SETTINGS)
+    ext = torch.cuda.ExternalStream(h.stream(), device=device)
+    for _ in range(warmup):
+        h.solve_device(batch, settings, data, sol)
+    h.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(ext)
+    for _ in range(steps):
+        h.solve_device(batch, settings, data, sol)
+    ev1.record(ext)
+    h.synchronize()
+    t_wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / steps
+    status = sol_t["status"].cpu().numpy()
+    iters = sol_t["iter"].cpu().numpy()
+    elem = 4 if dtype == "f32" else 8
+    bytes_qp = alg_bytes_per_qp(N, constraints=constraints, elem=elem)
+    it = float(iters.mean())
+    traffic = pmc_traffic(name, batch)
+    out = {"description": desc, "dtype": dtype, "batch": batch, "N": N, "steps": steps,
+           "value": batch * steps / t_wall, "unit": "QP solves/s", "kernel_ms": kernel_ms,
+           "success_rate": float((status == 0).mean()), "iters_mean": it,
+           "iters_max": int(iters.max()),
+           # the QP data must be streamed from HBM once per IPM iteration (it does not fit
+           # on-chip): algorithmic bytes x iterations taken, against the 8 TB/s peak
+           "hbm_alg_bytes_per_iter_frac": bytes_qp * it * batch / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+           "hbm_traffic_per_solve": traffic,
+           "hbm_actual_tbs": None if traffic is None else traffic / (kernel_ms * 1e-3) / 1e12}
+    log(f"[secondary] {name}: kernel {kernel_ms:.2f} ms, {out['value']:.4g} QP/s, "
+        f"success {out['success_rate']:.3f}, iters {it:.2f}")
+    del h
+    torch.cuda.empty_cache()
+    return out
 
 
 def host_path(capi, h, dt, batch, N, settings, dtype, max_batch=16384, reps=2):

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${1:-dev}; shift
-timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/bench_${TAG}_unconstr_n20.json 2> gpurun_out/bench_${TAG}_unconstr_n20.log || exit $?
+timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-secondary > gpurun_out/bench_${TAG}_unconstr_n20.json 2> gpurun_out/bench_${TAG}_unconstr_n20.log || exit $?
 for W in box_u_n20 cone_n40_f32 unconstr_n10_b4096; do
   timeout -k 10 300 python bench.py --workload $W --steps 5 --warmup 1 --no-cpu-baseline --no-pipeline --no-host-path "$@" \
     > gpurun_out/bench_${TAG}_${W}.json 2> gpurun_out/bench_${TAG}_${W}.log || exit $?

@@ -7,6 +7,7 @@ without a GPU works; calling a solve raises :class:`SrbdQpError`.
 from __future__ import annotations
 
 import ctypes as C
+import sys
 import os
 from pathlib import Path
 from typing import Dict, Optional
@@ -205,10 +206,24 @@ class Handle:
     def synchronize(self) -> None:
         check(lib().srbd_qp_synchronize(self._h), "srbd_qp_synchronize")
 
-    def solve_device(self, batch: int, settings: Settings, data, sol, stream: int = 0) -> None:
+    def torch_stream(self):
+        """The handle's HIP stream as a torch.cuda.ExternalStream (cached)."""
+        import torch
+        if getattr(self, "_ext", None) is None:
+            self._ext = torch.cuda.ExternalStream(self.stream(), device=torch.device("cuda", self.device))
+        return self._ext
+
+    def solve_device(self, batch: int, settings: Settings, data, sol, stream: int = 0,
+                     order: bool = True) -> None:
+        """Launch on `stream` (0: the handle's own stream).  With order=True and no
+        explicit stream, the launch is ordered like a torch op: after the work
+        already queued on torch's current stream (which produced the inputs and
+        zero-filled the outputs), and torch's stream waits for it in turn."""
         f = lib().srbd_qp_solve_f32 if isinstance(data, Data32) else lib().srbd_qp_solve_f64
+        o = _order_before(self, stream, order)
         check(f(self._h, int(batch), C.byref(settings), C.byref(data), C.byref(sol),
                 C.c_void_p(stream or None)), f.__name__)
+        _order_after(o)
 
     def solve_host(self, batch: int, settings: Settings, data, sol) -> None:
         f = lib().srbd_qp_solve_host_f32 if isinstance(data, Data32) else lib().srbd_qp_solve_host_f64
@@ -224,6 +239,27 @@ class Handle:
             self.close()
         except Exception:
             pass
+
+
+def _order_before(handle: "Handle", stream: int, order: bool):
+    """Make the handle's stream wait for torch's current stream (inputs produced and
+    outputs allocated / filled there).  No-op with an explicit stream or without an
+    initialised torch CUDA context."""
+    if stream or not order:
+        return None
+    torch = sys.modules.get("torch")
+    if torch is None or not torch.cuda.is_initialized():
+        return None
+    ext = handle.torch_stream()
+    cur = torch.cuda.current_stream(torch.device("cuda", handle.device))
+    ext.wait_stream(cur)
+    return cur, ext
+
+
+def _order_after(o) -> None:
+    """torch's current stream waits for the launch just queued on the handle's stream."""
+    if o is not None:
+        o[0].wait_stream(o[1])
 
 
 def _tensor_ptr(t) -> int:
@@ -318,10 +354,12 @@ def srbd_linearize(handle: Handle, xs, us, constraints: str = "none",
         t = out
         data = Data(**{k: _tensor_ptr(t.get(k)) or None for k in DATA_FIELDS})
         p = params or default_model_params()
+        o = _order_before(handle, stream, True)
         check(lib().srbd_qp_srbd_linearize_f64(handle.ptr, int(B), C.byref(p),
                                                SRBD_CONSTRAINTS[constraints], C.c_void_p(xs.data_ptr()),
                                                C.c_void_p(us.data_ptr()), C.byref(data),
                                                C.c_void_p(stream or None)), "srbd_qp_srbd_linearize_f64")
+        _order_after(o)
         return t, data
     t = {"A": torch.empty(B, N, 144, **f), "B": torch.empty(B, N, 144, **f),
          "b": torch.empty(B, N, 12, **f), "Q": torch.empty(B, N + 1, 144, **f),
@@ -336,10 +374,12 @@ def srbd_linearize(handle: Handle, xs, us, constraints: str = "none",
             t[k] = torch.empty(B, N + 1, 24, **f)
     data = Data(**{k: _tensor_ptr(t.get(k)) or None for k in DATA_FIELDS})
     p = params or default_model_params()
+    o = _order_before(handle, stream, True)
     check(lib().srbd_qp_srbd_linearize_f64(handle.ptr, int(B), C.byref(p), SRBD_CONSTRAINTS[constraints],
                                            C.c_void_p(xs.data_ptr()), C.c_void_p(us.data_ptr()),
                                            C.byref(data), C.c_void_p(stream or None)),
           "srbd_qp_srbd_linearize_f64")
+    _order_after(o)
     return t, data
 
 
@@ -361,8 +401,10 @@ def srbd_linesearch(handle: Handle, xs, us, dx, du, alpha, params: Optional[Mode
     p = params or default_model_params()
     lp = ls or default_linesearch()
     ptr = lambda t: C.c_void_p(t.data_ptr())
+    o = _order_before(handle, stream, True)
     check(lib().srbd_qp_srbd_linesearch_f64(handle.ptr, int(B), C.byref(p), C.byref(lp), ptr(xs),
                                             ptr(us), ptr(dx), ptr(du), ptr(alpha), ptr(merit),
                                             ptr(conv), C.c_void_p(stream or None)),
           "srbd_qp_srbd_linesearch_f64")
+    _order_after(o)
     return merit, conv

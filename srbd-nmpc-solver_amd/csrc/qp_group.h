@@ -309,6 +309,27 @@ __device__ __forceinline__ void load12(const double* __restrict__ p, double (&v)
     v[2 * I + 1] = t.y;
   });
 }
+// same, non-temporal (streamed once: global_load_dwordx4 ... nt)
+__device__ __forceinline__ void load12_nt(const double* __restrict__ p, double (&v)[12]) {
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  const dv2* p2 = reinterpret_cast<const dv2*>(p);
+  sfor<0, 6>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    dv2 t = __builtin_nontemporal_load(p2 + I);
+    v[2 * I] = t.x;
+    v[2 * I + 1] = t.y;
+  });
+}
+__device__ __forceinline__ void load12_nt(const float* __restrict__ p, float (&v)[12]) {
+  typedef float fv2 __attribute__((ext_vector_type(2)));
+  const fv2* p2 = reinterpret_cast<const fv2*>(p);
+  sfor<0, 6>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    fv2 t = __builtin_nontemporal_load(p2 + I);
+    v[2 * I] = t.x;
+    v[2 * I + 1] = t.y;
+  });
+}
 __device__ __forceinline__ void store12(double* __restrict__ p, const double (&v)[12]) {
   double2* p2 = reinterpret_cast<double2*>(p);
   sfor<0, 6>([&](auto i) {

@@ -4,6 +4,9 @@
 #ifndef SRBD_EARLY_LOADS
 #define SRBD_EARLY_LOADS 0
 #endif
+#ifndef SRBD_NT_REC
+#define SRBD_NT_REC 0
+#endif
 #ifndef SRBD_NT_INPUTS
 #define SRBD_NT_INPUTS 0
 #endif
@@ -28,7 +31,9 @@ struct StageLoader {
   __device__ __forceinline__ void col(const real* blk, int rows, int ld, int c, bool ok,
                                       real (&v)[12]) const {
     if constexpr (FULL) {
-#if SRBD_NT_INPUTS
+#if SRBD_NT_INPUTS == 2
+      load12_nt(blk + c * 12, v);
+#elif SRBD_NT_INPUTS
       // streamed once: non-temporal, so the records keep the caches
       const real* q = blk + c * 12;
       sfor<0, 12>([&](auto i) {
@@ -199,8 +204,13 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgsT<real
     load_packed_sym(rec + kWsP, row, P_);
     p_ = rec[kWsp + row];
     if (k < N) {
+#if SRBD_NT_REC
+      load12_nt(rec + kWsK + row * 12, K_);
+      load12_nt(rec + kWsAcl + row * 12, A__);
+#else
       load12(rec + kWsK + row * 12, K_);
       load12(rec + kWsAcl + row * 12, A__);
+#endif
       k_ = rec[kWsk + row];
       b_ = rec[kWsbcl + row];
     }
@@ -266,7 +276,11 @@ hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {
   const int blocks = (int)((lanes + threads - 1) / threads);
   // 12 x 12 stages only: smaller problems arrive embedded by pad.hip
   if (a.nx != 12 || a.nu != 12) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(riccati_unconstr_kernel<true>, dim3(blocks), dim3(threads), 0, stream, a);
+#ifndef SRBD_UNC_DYN_LDS
+#define SRBD_UNC_DYN_LDS 0
+#endif
+  // (A/B knob) dynamic LDS the kernel does not use, to cap workgroups per CU
+  hipLaunchKernelGGL(riccati_unconstr_kernel<true>, dim3(blocks), dim3(threads), SRBD_UNC_DYN_LDS, stream, a);
   return hipGetLastError();
 }
 
