@@ -1,3 +1,3 @@
 cd $GRAFT_REPO_ROOT
-timeout -k 10 700 python scripts/dev/ab_variants.py product,ntin,w1,ntin_w1,ntin_ntrec --steps 10 --warmup 2 --no-pipeline --no-host-path > gpurun_out/ab_unc.log 2>&1
+timeout -k 10 700 python scripts/dev/ab_variants.py ${VARIANTS:-product} --steps 10 --warmup 2 --no-pipeline --no-host-path --no-secondary > gpurun_out/ab_unc.log 2>&1
 rc=$?; grep -v " [01] (" gpurun_out/ab_unc.log; exit $rc
