@@ -268,6 +268,8 @@ def main():
         torch.cuda.empty_cache()
         secondary = {w: secondary_workload(pkg, capi, w, device, args.seed)
                      for w in ("box_u_n20", "cone_n40_f32")}
+        secondary["nmpc_step_config1"] = nmpc_config1(pkg, capi, device, args.seed,
+                                                      with_cpu=not args.no_cpu_baseline)
 
     traffic = pmc_traffic(args.workload, batch)
     line = {
@@ -366,6 +368,65 @@ def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1):
            "hbm_actual_tbs": None if traffic is None else traffic / (kernel_ms * 1e-3) / 1e12}
     log(f"[secondary] {name}: kernel {kernel_ms:.2f} ms, {out['value']:.4g} QP/s, "
         f"success {out['success_rate']:.3f}, iters {it:.2f}")
+    del h
+    torch.cuda.empty_cache()
+    return out
+
+
+def nmpc_config1(pkg, capi, device, seed, batch=65536, N=20, sqp_max_loop=15, reps=3,
+                 with_cpu=True):
+    """BASELINE config 1, batched: the reference's NMPC step (the SQP loop of
+    NMPCSolver::controlLoop, NMPC_solver.cpp:362-372: linearise -> QP -> filter line
+    search until converged, at most sqp_max_loop = 15) for `batch` robots, each from
+    the reference's cold start (x_nmpc = 0, u_nmpc = 100, alpha_ = 1,
+    NMPC_solver.cpp:56-64) with its own initial state x0 (the reference's x0 plus a
+    seeded perturbation), on the device through srbd_qp_srbd_nmpc_f64.  Beside it,
+    the same loop for the reference's own single robot on one host core (numpy
+    model + C oracle QP + numpy line search: a port, the reference prints this as
+    'Average NMPC solution time')."""
+    import torch
+    p = pkg.srbd_model.SrbdParams()
+    _, _, dx0 = pkg.srbd_model.sample_trajectories(batch, N, seed + 7, p)
+    x0_ref = np.zeros(12)
+    x0_ref[8] = 1.0  # setupReference (NMPC_solver.cpp:343)
+    x0 = torch.from_numpy(x0_ref + dx0).to(device)
+    xs0 = torch.zeros(batch, N + 1, 12, dtype=torch.float64, device=device)
+    us0 = torch.full((batch, N, 12), 100.0, dtype=torch.float64, device=device)
+    h = capi.Handle(N, 12, 12, 0, False, False, capacity=batch, device=device.index or 0)
+    times, it, cv = [], None, None
+    for r in range(reps + 1):  # the first call allocates the scratch and warms up
+        xs, us = xs0.clone(), us0.clone()
+        al = torch.ones(batch, dtype=torch.float64, device=device)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        it, cv = capi.srbd_nmpc(h, xs, us, x0, al, "none", NMPC_SETTINGS, sqp_max_loop)
+        torch.cuda.synchronize()
+        if r:
+            times.append(time.perf_counter() - t0)
+    t = min(times)
+    itn = it.cpu().numpy()
+    out = {"what": "NMPCSolver::controlLoop SQP loop (config 1) per robot, batched on the device: "
+                   "srbd_qp_srbd_nmpc_f64 (linearise + unconstrained QP + filter line search per "
+                   "SQP iteration, until converged or 15 iterations)",
+           "batch": batch, "N": N, "ms": t * 1e3, "nmpc_steps_per_s": batch / t,
+           "sqp_iters_mean": float(itn.mean()), "sqp_iters_max": int(itn.max()),
+           "converged_frac": float(cv.float().mean().item())}
+    if with_cpu:
+        sys.path.insert(0, str(REPO / "oracle"))
+        import oracle  # test infrastructure: CPU baseline leg only
+        import nmpc_linesearch as LS
+        xs1, us1 = np.zeros((N + 1, 12)), np.full((N, 12), 100.0)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            _, _, _, n_it, ok = LS.sqp_loop(pkg.srbd_model, oracle, p, xs1, us1, x0_ref, 1.0,
+                                            NMPC_SETTINGS, sqp_max_loop)
+            ts.append(time.perf_counter() - t0)
+        out["cpu_chain"] = {"ms_per_nmpc_step": min(ts) * 1e3, "sqp_iters": n_it, "converged": bool(ok),
+                            "cores": 1, "kind": "port",
+                            "sample": "the reference's own robot and start, 1 host core"}
+    log(f"[secondary] nmpc config 1: {batch} robots in {t * 1e3:.1f} ms "
+        f"({out['sqp_iters_mean']:.2f} SQP iterations mean, {out['converged_frac']:.3f} converged)")
     del h
     torch.cuda.empty_cache()
     return out

@@ -71,7 +71,7 @@
 extern "C" {
 #endif
 
-#define SRBD_QP_ABI_VERSION 6
+#define SRBD_QP_ABI_VERSION 7
 #define SRBD_QP_MAX_NX 12
 #define SRBD_QP_MAX_NU 12
 #define SRBD_QP_MAX_NG 64
@@ -265,6 +265,25 @@ int srbd_qp_srbd_linesearch_f64(srbd_qp_handle h, int batch, const srbd_model_pa
                                 const srbd_linesearch_params* ls, double* xs, double* us,
                                 const double* dx, const double* du, double* alpha, double* merit,
                                 int* converged, void* stream);
+
+/* The SQP loop of NMPCSolver::controlLoop (NMPC_solver.cpp:362-372) for a batch
+ * of robots: for it < sqp_max_loop (mpc_option.yaml sqp_max_loop):
+ * prepareQpStructures (srbd_qp_srbd_linearize_f64 at xs, us), solveQpProblems
+ * (srbd_qp_solve_f64 with settings and x0 - xs[:, 0], NMPC_solver.cpp:316-330),
+ * checkConvergence = linearSearch (srbd_qp_srbd_linesearch_f64: xs, us move to
+ * the accepted point, alpha persists); a robot whose line search reports
+ * convergence stops there (`if (checkConvergence()) break;`) and is not changed
+ * again.  xs [batch][N+1][12], us [batch][N][12] (in/out), x0 [batch][12],
+ * alpha [batch] (in/out), sqp_iter [batch] (SQP iterations run) and converged
+ * [batch] (out): device memory.  The QP data, solution and loop state live in
+ * a scratch buffer of the handle (allocated on first use, capacity-sized).
+ * Runs on the handle's stream and returns when every robot has stopped or
+ * sqp_max_loop iterations ran (one 4-byte read-back per iteration).  The
+ * handle's dims: N, nx = nu = 12, and has_box_u / ng = 24 per `constraints`. */
+int srbd_qp_srbd_nmpc_f64(srbd_qp_handle h, int batch, const srbd_model_params* params,
+                          const srbd_linesearch_params* ls, const srbd_qp_settings* settings,
+                          int constraints, int sqp_max_loop, double* xs, double* us,
+                          const double* x0, double* alpha, int* sqp_iter, int* converged);
 
 /* Blocks until all work queued on the handle's stream is done.            */
 int srbd_qp_synchronize(srbd_qp_handle h);

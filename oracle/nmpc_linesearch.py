@@ -89,3 +89,20 @@ def line_search(srbd_model, p, xs, us, dx, du, alpha, ls=None):
         alpha = ls["beta_alpha"] * alpha
     converged = dphi > -1e-3 and theta < 1e-6
     return xs_new, us_new, alpha, phi, theta, dphi, converged
+
+
+def sqp_loop(srbd_model, oracle, p, xs, us, x0, alpha, settings, sqp_max_loop, constraints="none"):
+    """One robot through the SQP loop of NMPCSolver::controlLoop (NMPC_solver.cpp:362-372):
+    prepareQpStructures (srbd_model.build_qp), solveQpProblems (the C oracle with
+    x0 - x_nmpc(:, 0), NMPC_solver.cpp:316-330), `if (checkConvergence()) break;`
+    (line_search above).  Returns (xs, us, alpha, sqp_iterations, converged)."""
+    xs, us = xs.copy(), us.copy()
+    it, conv = 0, False
+    for it in range(1, sqp_max_loop + 1):
+        qp, _ = srbd_model.build_qp(xs[None], us[None], p, constraints)
+        sol = oracle.solve(qp, settings, x0=(x0 - xs[0])[None])
+        xs, us, alpha, _, _, _, conv = line_search(srbd_model, p, xs, us, sol["x"][0], sol["u"][0],
+                                                   alpha)
+        if conv:
+            break
+    return xs, us, alpha, it, conv

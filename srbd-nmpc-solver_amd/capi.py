@@ -144,6 +144,10 @@ def lib():
         L.srbd_qp_srbd_linesearch_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(ModelParams),
                                                   C.POINTER(LsParams)] + [C.c_void_p] * 8
         L.srbd_qp_srbd_linesearch_f64.restype = C.c_int
+        L.srbd_qp_srbd_nmpc_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(ModelParams),
+                                            C.POINTER(LsParams), C.POINTER(Settings), C.c_int,
+                                            C.c_int] + [C.c_void_p] * 6
+        L.srbd_qp_srbd_nmpc_f64.restype = C.c_int
         L.srbd_qp_abi_version.argtypes = []
         L.srbd_qp_abi_version.restype = C.c_int
         _lib = L
@@ -408,3 +412,28 @@ def srbd_linesearch(handle: Handle, xs, us, dx, du, alpha, params: Optional[Mode
           "srbd_qp_srbd_linesearch_f64")
     _order_after(o)
     return merit, conv
+
+
+def srbd_nmpc(handle: Handle, xs, us, x0, alpha, constraints: str = "none",
+              settings: Optional[Dict] = None, sqp_max_loop: int = 15,
+              params: Optional[ModelParams] = None, ls: Optional[LsParams] = None):
+    """The SQP loop of NMPCSolver::controlLoop (NMPC_solver.cpp:362-372) for a batch
+    of robots on the device (srbd_qp_srbd_nmpc_f64): xs [B][N+1][12], us [B][N][12]
+    (torch fp64, updated in place), x0 [B][12], alpha [B] (in place, the persistent
+    alpha_ of NMPC_solver.h:104).  Returns (sqp_iter [B], converged [B]) int32
+    device tensors.  Synchronous."""
+    import torch
+    B = xs.shape[0]
+    it = torch.zeros(B, dtype=torch.int32, device=xs.device)
+    conv = torch.zeros(B, dtype=torch.int32, device=xs.device)
+    p = params or default_model_params()
+    lp = ls or default_linesearch()
+    s = settings_struct(settings)
+    ptr = lambda t: C.c_void_p(t.data_ptr())
+    o = _order_before(handle, 0, True)
+    check(lib().srbd_qp_srbd_nmpc_f64(handle.ptr, int(B), C.byref(p), C.byref(lp), C.byref(s),
+                                      SRBD_CONSTRAINTS[constraints], int(sqp_max_loop), ptr(xs),
+                                      ptr(us), ptr(x0), ptr(alpha), ptr(it), ptr(conv)),
+          "srbd_qp_srbd_nmpc_f64")
+    _order_after(o)
+    return it, conv

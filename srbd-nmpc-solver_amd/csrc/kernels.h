@@ -98,7 +98,12 @@ namespace srbd {
 hipError_t launch_srbd_linesearch(const srbd_model_params& p, const srbd_linesearch_params& ls,
                                   int batch, int N, double* xs, double* us, const double* dx,
                                   const double* du, double* alpha, double* merit, int* converged,
-                                  hipStream_t stream);
+                                  hipStream_t stream, const int* done = nullptr);
+hipError_t launch_nmpc_prep(int batch, int N, int it, const double* xs, const double* x0,
+                            double* dx0, int* done, int* sqp_iter, int* converged,
+                            hipStream_t stream);
+hipError_t launch_nmpc_after(int batch, int it, const int* conv, int* done, int* sqp_iter,
+                             int* converged, int* active, hipStream_t stream);
 hipError_t launch_srbd_linearize(const srbd_model_params& p, int batch, int N, int mode,
                                  const double* xs, const double* us,
                                  const srbd_qp_data_f64& out, hipStream_t stream);

@@ -144,10 +144,17 @@ struct StageFactor {
 // A_ is overwritten with the closed-loop column Acl (VL: bcl) on exit.
 // The S/Q/R columns are fetched through the callables so that their loads
 // are issued late (short live ranges).
-template <typename T, typename LoadR, typename LoadSQ>
+struct NoMid {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// `mid` runs between the products and the triangular solves (MidAt = 1: P is
+// dead there) or after the solves (MidAt = 2: L is dead too): the caller may
+// issue the next stage's loads into registers of its own.
+template <int MidAt = 1, typename T, typename LoadR, typename LoadSQ, typename Mid = NoMid>
 __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&B_)[12],
                                              LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
-                                             const T reg, StageFactor<T>& o) {
+                                             const T reg, StageFactor<T>& o, Mid&& mid = Mid{}) {
   const bool isv = lane == kVecLane;
   // ---- G = R + B'(P B), L = chol(G)
   {
@@ -185,6 +192,10 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
     tmul_acc(A_, W, o.F);
   }
   SRBD_PHASE_FENCE();
+  if constexpr (MidAt == 1) {
+    mid();
+    SRBD_PHASE_FENCE();
+  }
   // ---- Y = L^-1 H, K = -L^-T Y
   trsv_lower(o.Lc, o.rs, o.H);
   SRBD_PHASE_FENCE();
@@ -198,6 +209,10 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
     });
   }
   SRBD_PHASE_FENCE();
+  if constexpr (MidAt == 2) {
+    mid();
+    SRBD_PHASE_FENCE();
+  }
   // ---- P_k = F - Y'Y (VL: p_k = f - Y'y)
   {
     T Hn[12];

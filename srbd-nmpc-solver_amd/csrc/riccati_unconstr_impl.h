@@ -4,6 +4,9 @@
 #ifndef SRBD_EARLY_LOADS
 #define SRBD_EARLY_LOADS 0
 #endif
+#ifndef SRBD_PREFETCH_AB
+#define SRBD_PREFETCH_AB 0
+#endif
 #ifndef SRBD_NT_REC
 #define SRBD_NT_REC 0
 #endif
@@ -50,7 +53,7 @@ struct StageLoader {
 };
 
 template <bool FULL>
-__global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgsT<real> a) {
+__global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<real> a) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int qp = gid >> 4;
   const int lane = threadIdx.x & (kGroup - 1);
@@ -104,16 +107,44 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgsT<real
   }
 
   // ---------------- backward sweep ----------------
+  real A_[12], B_[12];
+  // A, B (VL: b) of stage k: column-owned
+  auto loadAB = [&](int k, real (&Av)[12], real (&Bv)[12]) {
+    if (isv) {
+      ld.col(at(a.b, N, nx, k), nx, nx, 0, true, Av);
+      sfor<0, 12>([&](auto i) { Bv[decltype(i)::value] = real(0.0); });
+    } else {
+      ld.col(at(a.A, N, nxx, k), nx, nx, col, xcol, Av);
+      ld.col(at(a.B, N, nxu, k), nx, nx, col, ucol, Bv);
+    }
+  };
+#if SRBD_PREFETCH_AB == 3
+  // B of stage k only (VL: zeros)
+  auto loadB = [&](int k, real (&Bv)[12]) {
+    if (isv) {
+      sfor<0, 12>([&](auto i) { Bv[decltype(i)::value] = real(0.0); });
+    } else {
+      ld.col(at(a.B, N, nxu, k), nx, nx, col, ucol, Bv);
+    }
+  };
+  auto loadA = [&](int k, real (&Av)[12]) {
+    if (isv) {
+      ld.col(at(a.b, N, nx, k), nx, nx, 0, true, Av);
+    } else {
+      ld.col(at(a.A, N, nxx, k), nx, nx, col, xcol, Av);
+    }
+  };
+  if (N > 0) loadB(N - 1, B_);
+#elif SRBD_PREFETCH_AB
+  if (N > 0) loadAB(N - 1, A_, B_);
+#endif
 #pragma unroll 1
   for (int k = N - 1; k >= 0; --k) {
-    real A_[12], B_[12];
-    if (isv) {
-      ld.col(at(a.b, N, nx, k), nx, nx, 0, true, A_);
-      sfor<0, 12>([&](auto i) { B_[decltype(i)::value] = real(0.0); });
-    } else {
-      ld.col(at(a.A, N, nxx, k), nx, nx, col, xcol, A_);
-      ld.col(at(a.B, N, nxu, k), nx, nx, col, ucol, B_);
-    }
+#if SRBD_PREFETCH_AB == 3
+    loadA(k, A_);
+#elif !SRBD_PREFETCH_AB
+    loadAB(k, A_, B_);
+#endif
     auto loadR = [&](real (&Rc)[12]) {
       if (isv) {
         sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = real(0.0); });
@@ -138,7 +169,23 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgsT<real
       }
     };
     StageFactor<real> f;
-#if SRBD_EARLY_LOADS
+#if SRBD_PREFETCH_AB
+    // the next stage's A, B are requested half-way through this stage (after the
+    // products, before the triangular solves), so their latency hides behind
+    // the solves, the P update and the record stores
+    real An[12], Bn[12];
+#if SRBD_PREFETCH_AB == 3
+    // B only (24 VGPRs): A is requested at the top of the stage and hides
+    // behind P B, G and the Cholesky
+    riccati_step<1>(P, A_, B_, loadR, loadSQ, lane, reg, f, [&]() {
+      if (k > 0) loadB(k - 1, Bn);
+    });
+#else
+    riccati_step<SRBD_PREFETCH_AB>(P, A_, B_, loadR, loadSQ, lane, reg, f, [&]() {
+      if (k > 0) loadAB(k - 1, An, Bn);
+    });
+#endif
+#elif SRBD_EARLY_LOADS
     // all five blocks of the stage requested up front: one memory latency per
     // stage instead of three (R, then S/Q, behind the phase fences)
     real Re[12], Se[12], Qe[12];
@@ -186,6 +233,15 @@ __global__ void __launch_bounds__(256) riccati_unconstr_kernel(ProblemArgsT<real
       constexpr int I = decltype(i)::value;
       P[I] = f.F[I];
     });
+#if SRBD_PREFETCH_AB == 3
+    sfor<0, 12>([&](auto i) { B_[decltype(i)::value] = Bn[decltype(i)::value]; });
+#elif SRBD_PREFETCH_AB
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      A_[I] = An[I];
+      B_[I] = Bn[I];
+    });
+#endif
   }
 
   // ---------------- forward sweep (row-owned) ----------------

@@ -412,6 +412,7 @@ struct LsArgs {
   int* converged;
   srbd_linesearch_params ls;
   double qf_scale;
+  const int* done;  // optional: robots whose SQP loop has stopped are left untouched
 };
 
 // merit terms of stage k at (x + a dx, u + a du): phi_k, theta_k and, when
@@ -481,6 +482,7 @@ __global__ void __launch_bounds__(64) srbd_linesearch_kernel(Model m, LsArgs a) 
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int qp = gid / kLsGroup, lane = gid % kLsGroup;
   if (qp >= a.batch) return;
+  if (a.done && a.done[qp]) return;  // group-uniform
   const int N = a.N;
   const srbd_linesearch_params& ls = a.ls;
   // merit at the current iterate
@@ -538,14 +540,69 @@ __global__ void __launch_bounds__(64) srbd_linesearch_kernel(Model m, LsArgs a) 
 hipError_t launch_srbd_linesearch(const srbd_model_params& p, const srbd_linesearch_params& ls,
                                   int batch, int N, double* xs, double* us, const double* dx,
                                   const double* du, double* alpha, double* merit, int* converged,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, const int* done) {
   if (batch <= 0) return hipSuccess;
   Model m{p};
-  LsArgs a{batch, N, xs, us, dx, du, alpha, merit, converged, ls, p.qf_scale};
+  LsArgs a{batch, N, xs, us, dx, du, alpha, merit, converged, ls, p.qf_scale, done};
   const long long n = (long long)batch * kLsGroup;
   const int threads = 64;
   hipLaunchKernelGGL(srbd_linesearch_kernel, dim3((unsigned)((n + threads - 1) / threads)),
                      dim3(threads), 0, stream, m, a);
+  return hipGetLastError();
+}
+
+// ---- the SQP loop of NMPCSolver::controlLoop (NMPC_solver.cpp:362-372) ----
+// Before iteration `it`: the QP's initial state x0 - x_nmpc(:, 0)
+// (NMPC_solver.cpp:320); at it == 0 every robot is active.
+__global__ void __launch_bounds__(256) nmpc_prep_kernel(int batch, int N, int it, const double* xs,
+                                                         const double* x0, double* dx0, int* done,
+                                                         int* sqp_iter, int* converged) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= batch * 12) return;
+  const int r = gid / 12, i = gid % 12;
+  dx0[gid] = x0[gid] - xs[(size_t)r * (N + 1) * 12 + i];
+  if (it == 0 && i == 0) {
+    done[r] = 0;
+    sqp_iter[r] = 0;
+    converged[r] = 0;
+  }
+}
+
+// After the line search of iteration `it`: `if (checkConvergence()) break;`
+// per robot; counts the robots still iterating.
+__global__ void __launch_bounds__(256) nmpc_after_kernel(int batch, int it, const int* conv,
+                                                          int* done, int* sqp_iter, int* converged,
+                                                          int* active) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  int still = 0;
+  if (r < batch && !done[r]) {
+    sqp_iter[r] = it + 1;
+    converged[r] = conv[r];
+    done[r] = conv[r];
+    still = conv[r] ? 0 : 1;
+  }
+  // one atomic per wave
+  const unsigned long long m = __ballot(still);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(active, (int)__popcll(m));
+}
+
+hipError_t launch_nmpc_prep(int batch, int N, int it, const double* xs, const double* x0,
+                            double* dx0, int* done, int* sqp_iter, int* converged,
+                            hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  const long long n = (long long)batch * 12;
+  hipLaunchKernelGGL(nmpc_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     batch, N, it, xs, x0, dx0, done, sqp_iter, converged);
+  return hipGetLastError();
+}
+
+hipError_t launch_nmpc_after(int batch, int it, const int* conv, int* done, int* sqp_iter,
+                             int* converged, int* active, hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(active, 0, sizeof(int), stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(nmpc_after_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, stream,
+                     batch, it, conv, done, sqp_iter, converged, active);
   return hipGetLastError();
 }
 

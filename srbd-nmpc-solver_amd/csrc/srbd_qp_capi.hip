@@ -44,6 +44,10 @@ struct srbd_qp_handle_s {
   // nx < 12 or nu < 12: the 12 x 12 embedding (pad.hip), allocated on first use
   void* pad = nullptr;
   size_t pad_bytes = 0;
+  // srbd_qp_srbd_nmpc_f64: QP data, solution and loop state, allocated on first use
+  void* nmpc = nullptr;
+  size_t nmpc_bytes = 0;
+  int* nmpc_active_host = nullptr;  // pinned
 };
 
 extern "C" {
@@ -174,6 +178,8 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   if (h->ws) hipFree(h->ws);
   if (h->stage) hipFree(h->stage);
   if (h->pad) hipFree(h->pad);
+  if (h->nmpc) hipFree(h->nmpc);
+  if (h->nmpc_active_host) hipHostFree(h->nmpc_active_host);
   if (h->stream) hipStreamDestroy(h->stream);
   hipSetDevice(prev);
   delete h;
@@ -507,6 +513,98 @@ int srbd_qp_srbd_linesearch_f64(srbd_qp_handle h, int batch, const srbd_model_pa
                                                     merit, converged, strm);
   (void)hipSetDevice(prev);
   if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
+  return SRBD_QP_OK;
+}
+
+int srbd_qp_srbd_nmpc_f64(srbd_qp_handle h, int batch, const srbd_model_params* params,
+                          const srbd_linesearch_params* ls, const srbd_qp_settings* settings,
+                          int constraints, int sqp_max_loop, double* xs, double* us,
+                          const double* x0, double* alpha, int* sqp_iter, int* converged) {
+  if (!h || !params || !ls || !settings || !xs || !us || !x0 || !alpha || !sqp_iter || !converged)
+    return fail(SRBD_QP_EINVAL, "NULL argument");
+  const srbd_qp_dims& d = h->dims;
+  if (d.nx != 12 || d.nu != 12) return fail(SRBD_QP_EDIM, "the SRBD NMPC loop needs nx = nu = 12");
+  if (batch < 0 || batch > h->capacity) return fail(SRBD_QP_ECAPACITY, "batch exceeds capacity");
+  if (sqp_max_loop < 0) return fail(SRBD_QP_EINVAL, "sqp_max_loop must be non-negative");
+  if (constraints < SRBD_QP_SRBD_NONE || constraints > SRBD_QP_SRBD_CONE)
+    return fail(SRBD_QP_EINVAL, "unknown constraints mode");
+  const bool box = constraints == SRBD_QP_SRBD_BOX_U, cone = constraints == SRBD_QP_SRBD_CONE;
+  if ((d.has_box_u != 0) != box || (d.ng > 0) != cone || d.has_box_x || (cone && d.ng != 24))
+    return fail(SRBD_QP_EINVAL, "the handle's dims do not match the constraints mode");
+  int rc = srbd_qp_check_settings(settings);
+  if (rc) return rc;
+  if (batch == 0 || sqp_max_loop == 0) return SRBD_QP_OK;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(h->device);
+  hipStream_t strm = h->stream;
+  // scratch: QP data (linearisation), x0 - x_nmpc(:,0), QP solution, loop state
+  const size_t B = (size_t)h->capacity, N = (size_t)d.N;
+  struct Buf { size_t off, n; };
+  size_t top = 0;
+  auto take = [&](size_t n) { Buf b{top, n}; top += (n + 31) / 32 * 32; return b; };
+  const Buf bA = take(B * N * 144), bB = take(B * N * 144), bb = take(B * N * 12),
+            bQ = take(B * (N + 1) * 144), bS = take(B * N * 144), bR = take(B * N * 144),
+            bq = take(B * (N + 1) * 12), br = take(B * N * 12);
+  const Buf blbu = take(box ? B * N * 12 : 0), bubu = take(box ? B * N * 12 : 0);
+  const Buf bD = take(cone ? B * N * 288 : 0), blg = take(cone ? B * (N + 1) * 24 : 0),
+            bug = take(cone ? B * (N + 1) * 24 : 0), blgm = take(cone ? B * (N + 1) * 24 : 0),
+            bugm = take(cone ? B * (N + 1) * 24 : 0);
+  const Buf bx0 = take(B * 12), bx = take(B * (N + 1) * 12), bu = take(B * N * 12),
+            bpi = take(B * (N + 1) * 12);
+  const Buf bint = take(B * 4 + 8);  // conv, done, status, iter (ints) + active
+  const size_t need = top * sizeof(double);
+  hipError_t e = hipSuccess;
+  if (need > h->nmpc_bytes) {
+    if (h->nmpc) (void)hipFree(h->nmpc);
+    h->nmpc = nullptr;
+    h->nmpc_bytes = 0;
+    e = hipMalloc(&h->nmpc, need);
+    if (e == hipSuccess) h->nmpc_bytes = need;
+  }
+  if (e == hipSuccess && !h->nmpc_active_host)
+    e = hipHostMalloc(reinterpret_cast<void**>(&h->nmpc_active_host), sizeof(int));
+  if (e != hipSuccess) {
+    (void)hipSetDevice(prev);
+    return fail(e == hipErrorOutOfMemory ? SRBD_QP_ENOMEM : SRBD_QP_EDEVICE,
+                std::string("NMPC scratch allocation failed: ") + hipGetErrorString(e));
+  }
+  double* base = reinterpret_cast<double*>(h->nmpc);
+  auto at = [&](const Buf& b) -> double* { return b.n ? base + b.off : nullptr; };
+  srbd_qp_data_f64 qd{};
+  qd.A = at(bA); qd.B = at(bB); qd.b = at(bb); qd.Q = at(bQ); qd.S = at(bS); qd.R = at(bR);
+  qd.q = at(bq); qd.r = at(br); qd.lbu = at(blbu); qd.ubu = at(bubu);
+  qd.D = at(bD); qd.lg = at(blg); qd.ug = at(bug); qd.lg_mask = at(blgm); qd.ug_mask = at(bugm);
+  qd.x0 = at(bx0);
+  int* ints = reinterpret_cast<int*>(at(bint));
+  int *conv = ints, *done = ints + B, *status = ints + 2 * B, *iters = ints + 3 * B,
+      *active = ints + 4 * B;
+  srbd_qp_solution_f64 sol{};
+  sol.x = at(bx); sol.u = at(bu); sol.pi = at(bpi); sol.status = status; sol.iter = iters;
+  srbd_model_params p = *params;
+  if (p.qf_scale <= 0.0) p.qf_scale = (double)d.N;
+  // NMPC_solver.cpp:362-372: prepareQpStructures; solveQpProblems; if (checkConvergence()) break;
+  for (int it = 0; it < sqp_max_loop && e == hipSuccess; ++it) {
+    e = srbd::launch_srbd_linearize(p, batch, d.N, constraints, xs, us, qd, strm);
+    if (e == hipSuccess)
+      e = srbd::launch_nmpc_prep(batch, d.N, it, xs, x0, at(bx0), done, sqp_iter, converged, strm);
+    if (e != hipSuccess) break;
+    (void)hipSetDevice(prev);
+    rc = solve_impl<double>(h, batch, settings, &qd, &sol, strm);
+    (void)hipSetDevice(h->device);
+    if (rc) return rc;
+    e = srbd::launch_srbd_linesearch(p, *ls, batch, d.N, xs, us, at(bx), at(bu), alpha, nullptr,
+                                     conv, strm, done);
+    if (e == hipSuccess)
+      e = srbd::launch_nmpc_after(batch, it, conv, done, sqp_iter, converged, active, strm);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(h->nmpc_active_host, active, sizeof(int), hipMemcpyDeviceToHost, strm);
+    if (e == hipSuccess) e = hipStreamSynchronize(strm);
+    if (e == hipSuccess && *h->nmpc_active_host == 0) break;  // every robot has converged
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(strm);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("NMPC loop: ") + hipGetErrorString(e));
   return SRBD_QP_OK;
 }
 
