@@ -342,6 +342,19 @@ def default_model_params() -> ModelParams:
     return p
 
 
+def model_params(p) -> ModelParams:
+    """srbd_model_params from a srbd_model.SrbdParams (e.g. load_mpc_option's), on top
+    of the library defaults (box limits, qf_scale = N)."""
+    m = default_model_params()
+    for name in ("Q", "Qf", "Lbody", "foot_r", "foot_l", "x_ref"):
+        arr = getattr(m, name)
+        for i, v in enumerate(getattr(p, name)):
+            arr[i] = float(v)
+    for name in ("R", "dt", "mu_b", "theta_b", "mass", "mu", "Lfx", "Lfz", "fmax", "fmin"):
+        setattr(m, name, float(getattr(p, name)))
+    return m
+
+
 def srbd_linearize(handle: Handle, xs, us, constraints: str = "none",
                    params: Optional[ModelParams] = None, stream: int = 0, out=None):
     """Device-side prepareQpStructures: linearise SRBD trajectories xs [B][N+1][12],

@@ -23,7 +23,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 
@@ -54,6 +54,32 @@ class SrbdParams:
     fmin: float = 0.0
     # NMPC_solver.cpp:344-345
     x_ref: Tuple[float, ...] = (0, 0, 0.2, 0, 0, 0, 0.5, 0, 1.0, 0, 0, 0)
+
+
+def load_mpc_option(source) -> Tuple["SrbdParams", Dict]:
+    """The reference's config file (config/mpc_option.yaml), read with the keys of
+    NMPCSolver::readYaml (NMPC_solver.cpp:22-46): MPC.{Q, Qf, R, dt_MPC, horizon_MPC,
+    sqp_max_loop}, Physical.Lbody, mu_b, theta_b, N_rep.  `source` is a path or the
+    YAML text.  Returns (SrbdParams, {"sqp_max_loop", "N_rep"}); a missing key raises
+    KeyError like yaml-cpp's as<>() on an absent node throws."""
+    import os
+    import yaml
+    text = source
+    if isinstance(source, (str, os.PathLike)) and os.path.exists(source):
+        with open(source) as f:
+            text = f.read()
+    cfg = yaml.safe_load(text)
+    mpc, phys = cfg["MPC"], cfg["Physical"]
+    def vec(v, n, name):
+        if len(v) != n:
+            raise ValueError(f"{name} needs {n} values, got {len(v)}")
+        return tuple(float(x) for x in v)
+
+    p = SrbdParams(Q=vec(mpc["Q"], 12, "MPC.Q"), Qf=vec(mpc["Qf"], 12, "MPC.Qf"), R=float(mpc["R"]),
+                   dt=float(mpc["dt_MPC"]), N=int(mpc["horizon_MPC"]),
+                   Lbody=vec(phys["Lbody"], 3, "Physical.Lbody"), mu_b=float(cfg["mu_b"]),
+                   theta_b=float(cfg["theta_b"]))
+    return p, {"sqp_max_loop": int(mpc["sqp_max_loop"]), "N_rep": int(cfg["N_rep"])}
 
 
 # ---------------------------------------------------------------------------
