@@ -6,6 +6,9 @@
 #ifndef SRBD_IPM_FUSE
 #define SRBD_IPM_FUSE 1
 #endif
+#ifndef SRBD_RB_ACC_LDS
+#define SRBD_RB_ACC_LDS 1
+#endif
 namespace srbd {
 namespace SRBD_NS {
 
@@ -754,7 +757,20 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     real* const ldsA = rb_lds + (threadIdx.x / kGroup) * 3 * 144;
     real* const ldsB = ldsA + 144;
     real* const ldsS = ldsA + 288;
-    real mg = real(0.0), mb = real(0.0), md = real(0.0), mm = real(0.0), musum = real(0.0), objl = real(0.0);
+    // The sweep's six accumulators are live across the whole factorization, where the
+    // fp64 register file is at its limit: there they live in one LDS slot per lane
+    // (box-u RB 68 B of scratch -> none, -2.4%); fp32 keeps them in registers (no
+    // spills there, and the LDS round trips cost 1%).
+    constexpr bool kAccLds = SRBD_RB_ACC_LDS && sizeof(real) == 8;
+    __shared__ real rb_acc[kAccLds ? 6 * 256 : 1];
+    real acc_r[6];
+    real& mg = kAccLds ? rb_acc[0 * 256 + threadIdx.x] : acc_r[0];
+    real& mb = kAccLds ? rb_acc[1 * 256 + threadIdx.x] : acc_r[1];
+    real& md = kAccLds ? rb_acc[2 * 256 + threadIdx.x] : acc_r[2];
+    real& mm = kAccLds ? rb_acc[3 * 256 + threadIdx.x] : acc_r[3];
+    real& musum = kAccLds ? rb_acc[4 * 256 + threadIdx.x] : acc_r[4];
+    real& objl = kAccLds ? rb_acc[5 * 256 + threadIdx.x] : acc_r[5];
+    mg = mb = md = mm = musum = objl = real(0.0);
     real xn = real(0.0), pin = real(0.0);  // updated x_{k+1}, pi_{k+1} (element-owned), from stage k+1
     real P[12];
     for (int k = N; k >= 0; --k) {
