@@ -22,8 +22,11 @@ for r in range(rounds):
             print(n, "FAILED", out.stderr[-2000:], flush=True)
             sys.exit(1)
         line = json.loads(out.stdout.strip().splitlines()[-1])
-        res[n].append((line["roofline"]["kernel_avg_ms"], line["value"], line["success_rate"]))
+        res[n].append((line["roofline"]["kernel_avg_ms"], line["value"], line["success_rate"],
+                       line["iters_mean"]))
         print(n, r, res[n][-1], flush=True)
 for n in names:
     ms = [x[0] for x in res[n]]
-    print(f"{n:20s} kernel ms min {min(ms):.3f}  all {['%.3f' % m for m in ms]}  value {max(x[1] for x in res[n]):.4g}")
+    it = res[n][0][3]
+    per_it = f"  per iteration {min(ms) / it:.3f} ms ({it:.2f} it)" if it else ""
+    print(f"{n:20s} kernel ms min {min(ms):.3f}  all {['%.3f' % m for m in ms]}  value {max(x[1] for x in res[n]):.4g}{per_it}")

@@ -122,8 +122,18 @@ struct Ctx {
     asm volatile("" : "+v"(v));
     return (size_t)v;
   }
-  __device__ size_t sN() const { return oq() * N; }
-  __device__ size_t sN1() const { return oq() * (N + 1); }
+  // input QP index (diagnostic build only: every QP reads QP (qp & 63)'s data)
+  __device__ size_t iq() const {
+#ifdef SRBD_DIAG_SHARED_INPUT
+    return oq() & 63;
+#else
+    return oq();
+#endif
+  }
+  __device__ size_t sN() const { return iq() * N; }
+  __device__ size_t sN1() const { return iq() * (N + 1); }
+  __device__ size_t oN() const { return oq() * N; }
+  __device__ size_t oN1() const { return oq() * (N + 1); }
   __device__ const real* A() const { return bA + sN() * nxx(); }
   __device__ const real* B() const { return bB + sN() * nxu(); }
   __device__ const real* b() const { return bb + sN() * nx; }
@@ -132,7 +142,7 @@ struct Ctx {
   __device__ const real* R() const { return bR + sN() * nuu(); }
   __device__ const real* q() const { return bq + sN1() * nx; }
   __device__ const real* r() const { return br + sN() * nu; }
-  __device__ const real* x0() const { return bx0 + oq() * nx; }
+  __device__ const real* x0() const { return bx0 + iq() * nx; }
   __device__ const real* lbu() const { return blbu ? blbu + sN() * nu : nullptr; }
   __device__ const real* ubu() const { return bubu ? bubu + sN() * nu : nullptr; }
   __device__ const real* lbum() const { return blbum ? blbum + sN() * nu : nullptr; }
@@ -147,9 +157,9 @@ struct Ctx {
   __device__ const real* ug() const { return bug + sN1() * ng; }
   __device__ const real* lgm() const { return blgm ? blgm + sN1() * ng : nullptr; }
   __device__ const real* ugm() const { return bugm ? bugm + sN1() * ng : nullptr; }
-  __device__ real* x() const { return bxo + sN1() * nx; }
-  __device__ real* u() const { return buo + sN() * nu; }
-  __device__ real* pi() const { return bpi + sN1() * nx; }
+  __device__ real* x() const { return bxo + oN1() * nx; }
+  __device__ real* u() const { return buo + oN() * nu; }
+  __device__ real* pi() const { return bpi + oN1() * nx; }
   __device__ real* ws() const { return bws + oq() * ws_qp; }
 
   __device__ size_t nxx() const { return FULL ? 144 : (size_t)nx * nx; }
