@@ -255,7 +255,7 @@ def main():
     flops_qp = alg_flops_per_qp(N)
 
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:  # rank 0 at N = 1 only
         qp, x0 = make_cpu_sample(pkg, N, constraints, min(batch, args.cpu_pool), rank, batch, args.seed)
         cpu = cpu_baseline(pkg, qp, x0, settings_dict(settings), args.cpu_seconds)
         if dtype == "f32":
@@ -453,9 +453,16 @@ def host_path(capi, h, dt, batch, N, settings, dtype, max_batch=16384, reps=2):
         h.solve_host(nb, settings, data, sol)
     ms = (time.perf_counter() - t) / reps * 1e3
     nbytes = sum(v.nbytes for v in host.values() if v is not None) + sum(v.nbytes for v in out.values())
+    # the reference's own call pattern: ONE QP per solve() (NMPC_solver.cpp:319), host buffers
+    lat = []
+    for _ in range(51):
+        t1 = time.perf_counter()
+        h.solve_host(1, settings, data, sol)
+        lat.append(time.perf_counter() - t1)
     return {"what": "srbd_qp_solve_host: pageable host buffers -> H2D -> solve -> D2H (PCIe-inclusive)",
             "batch": nb, "ms_per_call": ms, "qps_per_s": nb / (ms * 1e-3),
-            "host_bytes_moved": nbytes, "status_ok": float((out["status"] == 0).mean())}
+            "host_bytes_moved": nbytes, "status_ok": float((out["status"] == 0).mean()),
+            "latency_batch1_ms": float(np.median(lat[1:])) * 1e3}
 
 
 def sqp_pipeline(pkg, h, N, constraints, batch, xs, us, x0, device, settings, iters=3):
