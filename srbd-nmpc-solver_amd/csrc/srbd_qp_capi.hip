@@ -591,8 +591,8 @@ int srbd_qp_srbd_nmpc_f64(srbd_qp_handle h, int batch, const srbd_model_params* 
     if (e != hipSuccess) break;
     (void)hipSetDevice(prev);
     rc = solve_impl<double>(h, batch, settings, &qd, &sol, strm);
+    if (rc) return rc;  // the caller's device is current again
     (void)hipSetDevice(h->device);
-    if (rc) return rc;
     e = srbd::launch_srbd_linesearch(p, *ls, batch, d.N, xs, us, at(bx), at(bu), alpha, nullptr,
                                      conv, strm, done);
     if (e == hipSuccess)
