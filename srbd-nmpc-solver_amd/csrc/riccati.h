@@ -36,6 +36,15 @@
 #ifndef SRBD_FUSED_DPP
 #define SRBD_FUSED_DPP 1
 #endif
+// 1: K = -L^-T Y by column sweeps (12 independent updates per step) instead of
+// dot-product back substitution (a serial chain of up to 11 FMAs per step)
+#ifndef SRBD_TRSV_AXPY
+#define SRBD_TRSV_AXPY 1
+#endif
+// 1: Cholesky pivot reciprocals by v_rcp + two Newton steps instead of IEEE division
+#ifndef SRBD_FAST_RCP
+#define SRBD_FAST_RCP 0
+#endif
 
 namespace srbd {
 
@@ -81,13 +90,27 @@ __device__ __forceinline__ void tmul_acc(const T (&X)[12], const T (&Y)[12], T (
 // G[:,l]); `reg` is added to each pivot.  On exit Lc holds column l of L
 // (rows > l meaningful) and rs = 1 / L[l][l] (0 for a non-positive pivot).
 template <typename T>
+__device__ __forceinline__ T pivot_inv(T d) {
+#if SRBD_FAST_RCP
+  if constexpr (std::is_same_v<T, double>) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
+    return __builtin_fma(r, e, r);
+  }
+#endif
+  return T(1) / d;
+}
+
+template <typename T>
 __device__ __forceinline__ void chol_cols(T (&G)[12], const int lane, const T reg, T (&Lc)[12],
                                           T& rs) {
   T dmine = T(1);
   sfor<0, 12>([&](auto kk) {
     constexpr int K = decltype(kk)::value;
     const T dk = bc<K>(G[K]) + reg;
-    const T inv = dk > T(0) ? T(1) / dk : T(0);
+    const T inv = dk > T(0) ? pivot_inv(dk) : T(0);
     const T s = lane > K ? G[K] * inv : T(0);
     sfor<K + 1, 12>([&](auto i) {
       constexpr int I = decltype(i)::value;
@@ -129,6 +152,25 @@ __device__ __forceinline__ void trsv_upper_t(const T (&Lc)[12], const T rs, cons
     });
     z[K] = s * bc<K>(rs);
   });
+}
+
+// Kc = -L^-T y by column sweeps: for K = 11..0: z_K = y_K / L_KK, then
+// y_I -= L_KI z_K for I < K (L_KI = lane I's column, row K).  y is kept.
+template <typename T>
+__device__ __forceinline__ void trsv_upper_t_neg_axpy(const T (&Lc)[12], const T rs,
+                                                      const T (&y)[12], T (&Kc)[12]) {
+  T w[12];
+  sfor<0, 12>([&](auto i) { w[decltype(i)::value] = y[decltype(i)::value]; });
+  sfor_down<0, 12>([&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    w[K] = w[K] * bc<K>(rs);
+    const T nz = -w[K];
+    sfor<0, K>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      w[I] = fmadd(bc<I>(Lc[K]), nz, w[I]);
+    });
+  });
+  sfor<0, 12>([&](auto i) { Kc[decltype(i)::value] = -w[decltype(i)::value]; });
 }
 
 template <typename T>
@@ -200,6 +242,9 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
   trsv_lower(o.Lc, o.rs, o.H);
   SRBD_PHASE_FENCE();
   launder(o.Lc);
+#if SRBD_TRSV_AXPY
+  trsv_upper_t_neg_axpy(o.Lc, o.rs, o.H, o.Kc);
+#else
   {
     T z[12];
     trsv_upper_t(o.Lc, o.rs, o.H, z);
@@ -208,6 +253,7 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
       o.Kc[I] = -z[I];
     });
   }
+#endif
   SRBD_PHASE_FENCE();
   if constexpr (MidAt == 2) {
     mid();
