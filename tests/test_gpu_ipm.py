@@ -222,3 +222,19 @@ def test_cone_without_c_equals_zero_c(pkg):
     np.testing.assert_array_equal(a["iter"], b["iter"])
     for key in ("x", "u", "pi", "stat"):
         np.testing.assert_allclose(a[key], b[key], rtol=1e-12, atol=1e-12 * np.abs(b[key]).max())
+
+
+@pytest.mark.parametrize("dims", [(12, 12, 64, 1, 301), (6, 4, 40, 3, 302), (12, 12, 0, 1, 303)])
+def test_extreme_sizes_vs_oracle(pkg, oracle, dims):
+    """Edges of the supported range: ng = 64 (the maximum, 6 chunks of 12 rows), N = 1
+    (a single stage plus the terminal one), a padded nx/nu with 4 chunks."""
+    nx, nu, ng, N, seed = dims
+    qp, x0 = helpers.random_constrained(8, N, nx, nu, ng, seed, pkg.OcpQpBatch)
+    st = dict(iter_max=60, mode="Balance")
+    out = pkg.capi.solve(qp, x0, st)
+    ref = oracle.solve(qp, st, x0=x0)
+    ok = (out["status"] == 0) & (ref["status"] == 0)
+    assert ok.sum() >= qp.batch - 1, (out["status"], ref["status"])
+    for i in np.nonzero(ok)[0]:
+        for key in ("x", "u"):
+            assert helpers.is_approx(out[key][i], ref[key][i], 1e-6), (key, i)
