@@ -131,7 +131,10 @@ typedef struct srbd_qp_settings {
   int pred_corr;
   int ric_alg;      /* accepted; both values run the classical recursion   */
   int split_step;
-  int compute_residuals; /* 1: fill res/obj also for unconstrained QPs     */
+  int compute_residuals; /* unconstrained QPs (nc = 0): 1 (default) = res/obj, when
+                          * given, hold the solution's KKT residual norms and
+                          * objective (HPIPM's comp_res_exit; one extra pass over
+                          * the QP data); 0 = they are zero-filled              */
 } srbd_qp_settings;
 
 typedef struct srbd_qp_data_f64 {

@@ -81,6 +81,9 @@ size_t ws_doubles_unconstr(int N);
 
 template <typename T>
 hipError_t launch_riccati_unconstr(const ProblemArgsT<T>& a, hipStream_t stream);
+// KKT residual norms / objective of an unconstrained solution into a.res / a.obj
+template <typename T>
+hipError_t launch_unconstr_residuals(const ProblemArgsT<T>& a, hipStream_t stream);
 
 // nx < 12 or nu < 12: embed the problem in 12 x 12 stages (pad.hip).  pad_elems
 // is the pad buffer size (elements of T); pad_problem fills it from `a` and

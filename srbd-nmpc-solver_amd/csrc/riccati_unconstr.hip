@@ -47,5 +47,13 @@ template <>
 hipError_t launch_riccati_unconstr<float>(const ProblemArgsT<float>& a, hipStream_t stream) {
   return ric_f32::launch(a, stream);
 }
+template <>
+hipError_t launch_unconstr_residuals<double>(const ProblemArgsT<double>& a, hipStream_t stream) {
+  return ric_f64::launch_residuals(a, stream);
+}
+template <>
+hipError_t launch_unconstr_residuals<float>(const ProblemArgsT<float>& a, hipStream_t stream) {
+  return ric_f32::launch_residuals(a, stream);
+}
 
 }  // namespace srbd

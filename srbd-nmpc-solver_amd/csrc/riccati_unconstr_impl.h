@@ -325,6 +325,111 @@ __global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<r
 }
 
 
+// KKT residuals and objective of an unconstrained solution: HPIPM's
+// d_ocp_qp_res_compute (hpipm_d_ocp_qp_res.h:57-67) for nc = 0, as the oracle's
+// compute_residuals states it (oracle/ocp_qp_oracle.c):
+//   res_stat = max( |R u + S x + r + B'pi_{k+1}| (k < N), |Q x + S'u + q + A'pi_{k+1} - pi_k| (k >= 1) )
+//   res_eq   = max |A x + B u + b - x_{k+1}|,   res_ineq = res_comp = 0,
+//   obj      = sum_k u'(R u / 2 + r) + x'(Q x / 2 + q) (k >= 1) + u'S x.
+// Run only when the caller asks for res / obj.  One 32-lane group per QP, lane l
+// takes stages l, l + 32, ...; any dims (padded problems are checked unpadded).
+constexpr int kResGroup = 32;
+__global__ void __launch_bounds__(256) unconstr_residuals_kernel(ProblemArgsT<real> a) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int qp = gid / kResGroup, lane = gid % kResGroup;
+  if (qp >= a.batch) return;
+  const int N = a.N, nx = a.nx, nu = a.nu;
+  const bool smaj = a.layout == 1;
+  auto at = [&](const real* base, int nstage, size_t blk, int k) -> const real* {
+    return smaj ? base + ((size_t)k * a.batch + qp) * blk : base + ((size_t)qp * nstage + k) * blk;
+  };
+  const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu, nuu = (size_t)nu * nu;
+  const real* x = a.x + (size_t)qp * (N + 1) * nx;
+  const real* u = a.u + (size_t)qp * N * nu;
+  const real* pi = a.pi + (size_t)qp * (N + 1) * nx;
+  auto upd = [](real& m, real v) {
+    v = v < real(0) ? -v : v;
+    if (v > m || v != v) m = v;  // NaN propagates
+  };
+  real mg = real(0), mb = real(0), ob = real(0);
+  for (int k = lane; k <= N; k += kResGroup) {
+    const real* xk = x + (size_t)k * nx;
+    const real* Q = at(a.Q, N + 1, nxx, k);
+    const real* q = at(a.q, N + 1, nx, k);
+    real Sx[12];
+    for (int i = 0; i < 12; ++i) Sx[i] = real(0);
+    if (k < N) {
+      const real* uk = u + (size_t)k * nu;
+      const real* xn = x + (size_t)(k + 1) * nx;
+      const real* pn = pi + (size_t)(k + 1) * nx;
+      const real* A = at(a.A, N, nxx, k);
+      const real* B = at(a.B, N, nxu, k);
+      const real* b = at(a.b, N, nx, k);
+      const real* S = at(a.S, N, nxu, k);
+      const real* R = at(a.R, N, nuu, k);
+      const real* r = at(a.r, N, nu, k);
+      for (int i = 0; i < nu; ++i) {  // column-major blocks: M[i][j] = M[j * rows + i]
+        real ru = real(0), sx = real(0), bp = real(0);
+        for (int j = 0; j < nu; ++j) ru += R[(size_t)j * nu + i] * uk[j];
+        for (int j = 0; j < nx; ++j) sx += S[(size_t)j * nu + i] * xk[j];
+        for (int j = 0; j < nx; ++j) bp += B[(size_t)i * nx + j] * pn[j];
+        Sx[i] = sx;
+        upd(mg, ru + sx + r[i] + bp);
+        ob += uk[i] * (real(0.5) * ru + r[i]) + (k == 0 ? uk[i] * sx : real(0));
+      }
+      for (int i = 0; i < nx; ++i) {
+        real v = b[i] - xn[i];
+        for (int j = 0; j < nx; ++j) v += A[(size_t)j * nx + i] * xk[j];
+        for (int j = 0; j < nu; ++j) v += B[(size_t)j * nx + i] * uk[j];
+        upd(mb, v);
+      }
+    }
+    if (k > 0) {
+      const real* uk = u + (size_t)k * nu;
+      const real* pn = pi + (size_t)(k + 1) * nx;
+      const real* A = k < N ? at(a.A, N, nxx, k) : nullptr;
+      const real* S = k < N ? at(a.S, N, nxu, k) : nullptr;
+      for (int i = 0; i < nx; ++i) {
+        real qx = real(0), g = q[i] - pi[(size_t)k * nx + i];
+        for (int j = 0; j < nx; ++j) qx += Q[(size_t)j * nx + i] * xk[j];
+        g += qx;
+        if (k < N) {
+          for (int j = 0; j < nu; ++j) g += S[(size_t)i * nu + j] * uk[j];
+          for (int j = 0; j < nx; ++j) g += A[(size_t)i * nx + j] * pn[j];
+        }
+        upd(mg, g);
+        ob += xk[i] * (real(0.5) * qx + q[i]);
+      }
+      if (k < N)
+        for (int i = 0; i < nu; ++i) ob += uk[i] * Sx[i];
+    }
+  }
+  for (int m = kResGroup / 2; m >= 1; m >>= 1) {
+    const real og = __shfl_xor(mg, m, kResGroup), obb = __shfl_xor(mb, m, kResGroup);
+    if (og > mg || og != og) mg = og;
+    if (obb > mb || obb != obb) mb = obb;
+    ob += __shfl_xor(ob, m, kResGroup);
+  }
+  if (lane == 0) {
+    if (a.res) {
+      a.res[(size_t)qp * 4 + 0] = mg;
+      a.res[(size_t)qp * 4 + 1] = mb;
+      a.res[(size_t)qp * 4 + 2] = real(0);
+      a.res[(size_t)qp * 4 + 3] = real(0);
+    }
+    if (a.obj) a.obj[qp] = ob;
+    if (a.status && (mg != mg || mb != mb)) a.status[qp] = 3;  // NaNDetected
+  }
+}
+
+hipError_t launch_residuals(const ProblemArgsT<real>& a, hipStream_t stream) {
+  if (a.batch <= 0) return hipSuccess;
+  const long long n = (long long)a.batch * kResGroup;
+  hipLaunchKernelGGL(unconstr_residuals_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     stream, a);
+  return hipGetLastError();
+}
+
 hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {
   if (a.batch <= 0) return hipSuccess;
   const int threads = 256;

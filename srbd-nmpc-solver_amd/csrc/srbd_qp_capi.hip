@@ -95,7 +95,7 @@ void srbd_qp_default_settings(srbd_qp_settings* s) {
   s->pred_corr = 1;
   s->ric_alg = 1;
   s->split_step = 0;
-  s->compute_residuals = 0;
+  s->compute_residuals = 1;  // HPIPM's comp_res_exit
 }
 
 int srbd_qp_check_settings(const srbd_qp_settings* s) {
@@ -284,11 +284,15 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   } else {
     e = srbd::launch_riccati_unconstr(run, strm);
     if (e == hipSuccess && padded) e = srbd::unpad_solution<T>(a, run, strm);
+    // residual norms / objective of the solution when asked for (HPIPM computes them
+    // for nc = 0 too; an extra pass over the QP data, so only on request)
     if (e == hipSuccess && (s->res || s->obj)) {
-      // an unconstrained solve reports zero residual norms / objective unless
-      // computed (compute_residuals is not implemented for nc == 0 yet)
-      if (s->res) e = hipMemsetAsync(s->res, 0, sizeof(T) * 4 * (size_t)batch, strm);
-      if (e == hipSuccess && s->obj) e = hipMemsetAsync(s->obj, 0, sizeof(T) * (size_t)batch, strm);
+      if (st->compute_residuals) {
+        e = srbd::launch_unconstr_residuals<T>(a, strm);
+      } else {
+        if (s->res) e = hipMemsetAsync(s->res, 0, sizeof(T) * 4 * (size_t)batch, strm);
+        if (e == hipSuccess && s->obj) e = hipMemsetAsync(s->obj, 0, sizeof(T) * (size_t)batch, strm);
+      }
     }
   }
   hipSetDevice(prev);

@@ -134,3 +134,62 @@ def test_stage_major_layout_identical(pkg):
     h.synchronize()
     for k in ("x", "u", "pi"):
         np.testing.assert_array_equal(st[k].cpu().numpy(), ref[k])
+
+
+@pytest.mark.parametrize("case", ["srbd", "random", "padded", "stage_major", "fp32"])
+def test_unconstrained_residuals_and_objective(pkg, oracle, case):
+    """nc = 0: res (max |res_stat|, |res_eq|, 0, 0) and obj of the Riccati solution
+    (HPIPM's comp_res_exit; d_ocp_qp_res_compute) against the oracle's
+    compute_residuals on the same solution; compute_residuals = 0 zero-fills."""
+    import torch
+    N = 20
+    if case in ("srbd", "stage_major", "fp32"):
+        qp, x0 = pkg.srbd_model.generate_batch(24, N=N, seed=606, constraints="none")
+    else:
+        nx, nu = (12, 12) if case == "random" else (7, 5)
+        qp, x0 = helpers.random_unconstrained(24, N, nx, nu, 607, pkg.OcpQpBatch)
+        # well-posed horizon (see test_full_12x12_fast_path: with spectral radius ~2,
+        # pi = P x + p cancels catastrophically over 20 stages in any fp64 order)
+        rho = np.max(np.abs(np.linalg.eigvals(qp.A)), axis=-1)
+        qp.A = qp.A / rho[..., None, None]
+    ref = oracle.solve(qp, dict(iter_max=30), x0=x0)
+    if case == "fp32":
+        out = pkg.capi.solve(qp, x0, dict(iter_max=30), dtype=np.float32)
+        # fp32 solution: residuals at fp32 rounding of the terms, objective to fp32
+        assert np.all(out["res"][:, 2:] == 0)
+        assert np.all(out["res"][:, :2] < 1e-2), out["res"].max(0)
+        np.testing.assert_allclose(out["obj"], ref["obj"], rtol=1e-4, atol=1e-3)
+        return
+    if case == "stage_major":
+        N, B = qp.N, qp.batch
+        h = pkg.capi.Handle(N, 12, 12, 0, False, False, capacity=B, layout=1)
+        p = qp.packed()
+        p["x0"] = np.ascontiguousarray(x0)
+        dev = {}
+        for k, v in p.items():
+            if v is None:
+                continue
+            t = torch.from_numpy(v).cuda()
+            dev[k] = t.transpose(0, 1).contiguous() if k != "x0" else t
+        f64 = dict(dtype=torch.float64, device="cuda")
+        sol = {"x": torch.zeros(B, N + 1, 12, **f64), "u": torch.zeros(B, N, 12, **f64),
+               "pi": torch.zeros(B, N + 1, 12, **f64), "res": torch.zeros(B, 4, **f64),
+               "obj": torch.zeros(B, **f64)}
+        data = pkg.capi.Data(**{k: (dev[k].data_ptr() if k in dev else None) for k in pkg.capi.DATA_FIELDS})
+        S = pkg.capi.Solution(**{k: (sol[k].data_ptr() if k in sol else None) for k in pkg.capi.SOL_FIELDS})
+        h.solve_device(B, pkg.capi.settings_struct(dict(iter_max=30)), data, S)
+        h.synchronize()
+        out = {k: v.cpu().numpy() for k, v in sol.items()}
+    else:
+        out = pkg.capi.solve(qp, x0, dict(iter_max=30))
+    assert np.all(out["res"][:, 2:] == 0)
+    scale = max(1.0, float(np.abs(ref["obj"]).max()))
+    np.testing.assert_allclose(out["obj"], ref["obj"], rtol=1e-10, atol=1e-12 * scale)
+    # both are rounding-level numbers of the same size (the two solutions differ at ~1e-15):
+    # bounded by the magnitudes of the terms (the random data's unstable A makes x, pi large)
+    mag = np.array([max(np.abs(out[k][i]).max() for k in ("x", "u", "pi")) for i in range(qp.batch)])
+    for j in (0, 1):
+        assert np.all(out["res"][:, j] <= 1e-12 * mag), (j, out["res"][:, j] / mag)
+        assert np.all(ref["res"][:, j] <= 1e-12 * mag), (j, ref["res"][:, j] / mag)
+    zero = pkg.capi.solve(qp, x0, dict(iter_max=30, compute_residuals=0))
+    assert np.all(zero["res"] == 0) and np.all(zero["obj"] == 0)
