@@ -1377,7 +1377,16 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
   // at the top of every later launch.  iter_max + 1 factorization sweeps at
   // most: the last one always decides (converged or MaxIterReached).
   hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhInit>), grid, block, 0, stream, a);
-#if SRBD_IPM_FUSE
+#if SRBD_IPM_FUSE == 3
+  // (diagnostic schedule) RB and F1 as launches of their own, B2 -> F2 fused
+  for (int it = 0;; ++it) {
+    hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB>), grid, block, 0, stream, a);
+    if (it >= a.iter_max) break;
+    hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF1>), grid, block, 0, stream, a);
+    if (a.pred_corr)
+      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhB2, kPhF2>), grid, block, 0, stream, a);
+  }
+#elif SRBD_IPM_FUSE
   for (int it = 0;; ++it) {
     if (it >= a.iter_max) {
       hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB>), grid, block, 0, stream, a);
