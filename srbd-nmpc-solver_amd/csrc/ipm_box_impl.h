@@ -6,6 +6,12 @@
 #ifndef SRBD_IPM_FUSE
 #define SRBD_IPM_FUSE 1
 #endif
+#ifndef SRBD_FWD_PREFETCH
+#define SRBD_FWD_PREFETCH 0
+#endif
+#ifndef SRBD_FWD_PREFETCH_F2
+#define SRBD_FWD_PREFETCH_F2 0
+#endif
 #ifndef SRBD_RB_ACC_LDS
 #define SRBD_RB_ACC_LDS 1
 #endif
@@ -1215,6 +1221,22 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       ap = real(1e30);
       ad = real(1e30);
       real dxk = real(0.0);  // dx_0 = 0 (x0 fixed)
+      // The rows of K and Acl (and k, bcl) of stage k+1 are requested while stage k
+      // computes: they do not depend on dx, so each stage pays one latency less
+      // (F1 shares RB's register budget; F2 only with SRBD_FWD_PREFETCH_F2).
+      constexpr bool kPf = SRBD_FWD_PREFETCH && (!corr || SRBD_FWD_PREFETCH_F2);
+      real Kn[12], An[12], kn = real(0.0), bn = real(0.0);
+      auto load_rows = [&](int k, real (&Kr)[12], real (&Ar)[12], real& kv, real& bv) {
+        const real* rk = c.st(k) + par * kRecSize;
+        sfor<0, 12>([&](auto j) {
+          constexpr int J = decltype(j)::value;
+          Kr[J] = rk[kRecK + J * 12 + li];
+          Ar[J] = rk[kRecAcl + J * 12 + li];
+        });
+        kv = rk[kRecKv + li];
+        bv = rk[kRecBcl + li];
+      };
+      if (kPf && N > 0) load_rows(0, Kn, An, kn, bn);
       for (int k = 0; k <= N; ++k) {
         real* stk = c.st(k);
         const real* rec = stk + par * kRecSize;
@@ -1228,13 +1250,18 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         real du = real(0.0), dxn = real(0.0);
         if (k < N) {
           real Kr[12], Ar[12];
-          sfor<0, 12>([&](auto j) {
-            constexpr int J = decltype(j)::value;
-            Kr[J] = rec[kRecK + J * 12 + li];
-            Ar[J] = rec[kRecAcl + J * 12 + li];
-          });
-          du = rec[kRecKv + li];
-          dxn = rec[kRecBcl + li];
+          if constexpr (kPf) {
+            sfor<0, 12>([&](auto j) {
+              constexpr int J = decltype(j)::value;
+              Kr[J] = Kn[J];
+              Ar[J] = An[J];
+            });
+            du = kn;
+            dxn = bn;
+            if (k + 1 < N) load_rows(k + 1, Kn, An, kn, bn);
+          } else {
+            load_rows(k, Kr, Ar, du, dxn);
+          }
           dot_bcast2(Kr, Ar, dxk, du, dxn);
         }
         if (!uel || k == N) du = real(0.0);
