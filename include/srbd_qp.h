@@ -21,6 +21,11 @@
  *                        hpipm_s_ocp_qp_ipm.h:238).
  *   srbd_qp_destroy      ~OcpQpIpmSolver (d_ocp_qp_*_wrapper frees).
  *   srbd_qp_status_string  hpipm::to_string(HpipmStatus) (:19-33).
+ * The steps either side of the solve in the reference's SQP iteration, batched:
+ *   srbd_qp_srbd_linearize_f64   NMPCSolver::prepareQpStructures (NMPC_solver.cpp:276-314)
+ *   srbd_qp_srbd_linesearch_f64  NMPCSolver::linearSearch (NMPC_solver.cpp:149-274)
+ *   srbd_qp_srbd_nmpc_f64        the SQP loop of NMPCSolver::controlLoop
+ *                                (NMPC_solver.cpp:362-372) around all three.
  *
  * ------------------------------------------------------------------------
  * Problem (per QP, stages k = 0..N), identical to hpipm::OcpQp
