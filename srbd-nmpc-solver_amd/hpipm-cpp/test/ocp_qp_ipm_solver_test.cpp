@@ -194,6 +194,13 @@ TEST(unconstrained, true) {
   EXPECT_EQ(status, hpipm::HpipmStatus::Success);
   EXPECT_EQ(solver.getSolverStatistics().iter, 0);
   EXPECT_TRUE(sol[0].x.isApprox(p.x0));
+  // nc = 0 still reports the solution's KKT residuals (HPIPM's comp_res_exit):
+  // rounding-level stationarity and dynamics, no inequality terms
+  {
+    const auto& st = solver.getSolverStatistics();
+    EXPECT_TRUE(st.max_res_stat < 1e-8 && st.max_res_eq < 1e-8);
+    EXPECT_TRUE(st.max_res_ineq == 0.0 && st.max_res_comp == 0.0);
+  }
   // textbook Riccati recursion (reference test :60-90), s = -p
   std::vector<MatrixXd> P(N + 1), K(N);
   std::vector<VectorXd> s(N + 1), k(N);
