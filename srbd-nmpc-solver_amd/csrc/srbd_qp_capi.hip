@@ -285,8 +285,9 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
     e = srbd::launch_riccati_unconstr(run, strm);
     if (e == hipSuccess && padded) e = srbd::unpad_solution<T>(a, run, strm);
     // residual norms / objective of the solution when asked for (HPIPM computes them
-    // for nc = 0 too; an extra pass over the QP data, so only on request)
-    if (e == hipSuccess && (s->res || s->obj)) {
+    // for nc = 0 too; an extra pass over the QP data, so only on request); the stat
+    // table's row 0 gets them as well
+    if (e == hipSuccess && (s->res || s->obj || s->stat)) {
       if (st->compute_residuals) {
         e = srbd::launch_unconstr_residuals<T>(a, strm);
       } else {

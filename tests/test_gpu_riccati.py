@@ -181,7 +181,12 @@ def test_unconstrained_residuals_and_objective(pkg, oracle, case):
         h.synchronize()
         out = {k: v.cpu().numpy() for k, v in sol.items()}
     else:
-        out = pkg.capi.solve(qp, x0, dict(iter_max=30))
+        out = pkg.capi.solve(qp, x0, dict(iter_max=30), stats=True)
+        # iteration 0's row of the stat table holds the same numbers (cols 6, 7, 10)
+        np.testing.assert_array_equal(out["stat"][:, 0, 6], out["res"][:, 0])
+        np.testing.assert_array_equal(out["stat"][:, 0, 7], out["res"][:, 1])
+        np.testing.assert_array_equal(out["stat"][:, 0, 10], out["obj"])
+        assert np.all(out["stat"][:, 1:] == 0)
     assert np.all(out["res"][:, 2:] == 0)
     scale = max(1.0, float(np.abs(ref["obj"]).max()))
     np.testing.assert_allclose(out["obj"], ref["obj"], rtol=1e-10, atol=1e-12 * scale)
