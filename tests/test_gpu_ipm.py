@@ -238,3 +238,29 @@ def test_extreme_sizes_vs_oracle(pkg, oracle, dims):
     for i in np.nonzero(ok)[0]:
         for key in ("x", "u"):
             assert helpers.is_approx(out[key][i], ref[key][i], 1e-6), (key, i)
+
+
+@pytest.mark.parametrize("constraints", ["none", "box_u"])
+def test_nan_input_isolated(pkg, constraints):
+    """A QP with a NaN in its data ends with NaNDetected (HPIPM's NAN_SOL, status 3);
+    the other QPs of the batch are unaffected (bit-identical to a batch without it)."""
+    qp, x0 = pkg.srbd_model.generate_batch(20, N=10, seed=515, constraints=constraints)
+    st = dict(iter_max=30, tol_stat=1e-8, tol_eq=1e-8, tol_ineq=1e-8, tol_comp=1e-8)
+    clean = pkg.capi.solve(qp, x0, st)
+    bad = 7
+    qp.q[bad, 3, 2] = np.nan
+    out = pkg.capi.solve(qp, x0, st)
+    assert out["status"][bad] == 3, out["status"]
+    others = np.arange(qp.batch) != bad
+    assert np.all(out["status"][others] == clean["status"][others])
+    for k in ("x", "u", "pi"):
+        assert np.array_equal(out[k][others], clean[k][others]), k
+
+
+def test_batch_over_capacity_is_rejected(pkg):
+    """srbd_qp_solve_* refuse a batch larger than the handle's capacity (ECAPACITY)
+    instead of writing past its workspace."""
+    qp, x0 = pkg.srbd_model.generate_batch(8, N=5, seed=3, constraints="none")
+    h = pkg.capi.Handle(5, 12, 12, 0, False, False, capacity=4)
+    with pytest.raises(pkg.capi.SrbdQpError, match="exceeds capacity"):
+        pkg.capi.solve(qp, x0, None, handle=h)
