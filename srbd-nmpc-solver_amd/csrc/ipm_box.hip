@@ -48,7 +48,8 @@ namespace srbd {
 
 size_t ws_doubles_ipm(int N, int ng) {
   const int nch = (ng + kMaxDim - 1) / kMaxDim;
-  return ipm_f64::kQsSize + (size_t)(N + 1) * ((size_t)kIpmStage + (size_t)nch * kGenChunk);
+  return ipm_f64::kQsSize +
+         (size_t)(N + 1) * ((size_t)kIpmStage + (size_t)nch * kGenChunk + (nch ? kGenVec : 0));
 }
 
 template <>

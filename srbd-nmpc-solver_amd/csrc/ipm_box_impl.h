@@ -12,6 +12,11 @@
 #ifndef SRBD_FWD_PREFETCH_F2
 #define SRBD_FWD_PREFETCH_F2 0
 #endif
+// 1: C-free general rows (GEN == 1): B2 takes the corrector's D'gamma as
+// D'gamma_pred + sigma mu D'e (RB) + D'z (F1) instead of re-reading D and the rows' state
+#ifndef SRBD_B2_GENVEC
+#define SRBD_B2_GENVEC 1
+#endif
 #ifndef SRBD_RB_ACC_LDS
 #define SRBD_RB_ACC_LDS 1
 #endif
@@ -108,6 +113,13 @@ struct Side {
   real ml, mu;   // 1 if the lower / upper bound is active, else 0
 };
 
+// The RB sweep's per-group LDS blocks (A, B, S: 3 x 144 reals per QP group).  One
+// function, so one allocation per kernel: the fused RB -> F1 kernel's F1 reuses them.
+__device__ __forceinline__ real* group_lds_blocks() {
+  __shared__ real blocks[(256 / kGroup) * 3 * 144];
+  return blocks + (threadIdx.x / kGroup) * 3 * 144;
+}
+
 template <bool FULL, int GEN>
 struct Ctx {
   int N, nx, nu, lane, qp;
@@ -176,6 +188,8 @@ struct Ctx {
   }
   // state of constraint chunk ch at stage k: bars [48], steps [48], row values [12]
   __device__ real* gs(int k, int ch) const { return st(k) + kIpmStage + ch * kGenChunk; }
+  // per-stage general-row vectors (kGenVec) after the chunks
+  __device__ real* gv(int k) const { return st(k) + kIpmStage + nch * kGenChunk; }
   // row i of chunk ch (element-owned): lg <= v <= ug
   __device__ Side side_g(int k, int ch, int i) const {
     Side s{real(0.0), real(0.0), real(0.0), real(0.0)};
@@ -438,7 +452,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   c.qp = qp;
   c.ng = a.ng;
   c.nch = (a.ng + kMaxDim - 1) / kMaxDim;
-  c.stride = (size_t)kIpmStage + (size_t)c.nch * kGenChunk;
+  c.stride = (size_t)kIpmStage + (size_t)c.nch * kGenChunk + (c.nch ? kGenVec : 0);
   c.ws_qp = a.ws_qp;
   c.bA = a.A; c.bB = a.B; c.bb = a.b; c.bQ = a.Q; c.bS = a.S; c.bR = a.R; c.bq = a.q; c.br = a.r;
   c.bx0 = a.x0;
@@ -769,8 +783,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     // or transposed) and a row-owned copy through LDS where they are not (A x, B u,
     // S x); S stays in LDS until the factorization's second phase asks for it.
     // LDS per QP group: A, B, S columns (3 x 144 reals).
-    __shared__ real rb_lds[(256 / kGroup) * 3 * 144];
-    real* const ldsA = rb_lds + (threadIdx.x / kGroup) * 3 * 144;
+    real* const ldsA = group_lds_blocks();
     real* const ldsB = ldsA + 144;
     real* const ldsS = ldsA + 288;
     // The sweep's six accumulators are live across the whole factorization, where the
@@ -834,6 +847,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       // lam_l) / D'(..), predictor Gamma / gamma, gradient adds C'gamma / D'gamma and
       // (GEN == 1) the Hessian add D'Gamma D, accumulated for the factorization
       real gra = real(0.0), gqa = real(0.0);  // D'gamma, C'gamma (lane j)
+      real gea = real(0.0);                   // D'e, e = d gamma / d(sigma mu) (GEN == 1)
       real RG[12];                            // D'Gamma D, column j (GEN == 1)
       sfor<0, 12>([&](auto i) { RG[decltype(i)::value] = real(0.0); });
       if constexpr (GEN) {
@@ -889,6 +903,15 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           }
           rgu = dot_bcast(Dc, dl, rgu);
           gra = dot_bcast(Dc, gg, gra);
+          if constexpr (GEN == 1 && SRBD_B2_GENVEC) {
+            // gamma is affine in sigma mu: d gamma / d(sigma mu) = mu_row / t_u - ml / t_l
+            real e = real(0.0);
+            if (lane < kMaxDim) {
+              if (sg.ml != real(0.0)) e -= real(1.0) / bg.tl;
+              if (sg.mu != real(0.0)) e += real(1.0) / bg.tu;
+            }
+            gea = dot_bcast(Dc, e, gea);
+          }
           if constexpr (GEN == 1) {
             real Gb[12], Y[12];
             gather12(G, Gb);
@@ -934,6 +957,13 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       if (lane < kMaxDim) {
         gamma_of(su, bu, uk, real(0.0), real(0.0), real(0.0), Gu, gu);
         gamma_of(sx, bx, xk, real(0.0), real(0.0), real(0.0), Gx, gx);
+      }
+      if constexpr (GEN == 1 && SRBD_B2_GENVEC) {
+        if (lane < kMaxDim) {
+          real* v = c.gv(k);
+          v[lane] = gra;
+          v[12 + lane] = gea;
+        }
       }
       gu += gra;
       gx += gqa;
@@ -1135,7 +1165,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             gamma_of(sx, c.bar(stN, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, G, g);
           }
           pnext = lane < kMaxDim && xel ? stN[kStRes + 12 + lane] + g : real(0.0);
-          if constexpr (GEN) {
+          if constexpr (GEN == 2 || (GEN == 1 && !SRBD_B2_GENVEC)) {
+            // (C = NULL: the terminal stage has no general-row gradient, D_N is absent)
             real ra, qa;
             g_grad(N, true, sigma_mu, ra, qa);
             if (lane < kMaxDim && xel) pnext += qa;
@@ -1158,7 +1189,13 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           }
           real rt = lane < kMaxDim && uel ? stk[kStRes + lane] + gu : real(0.0);
           real qt = lane < kMaxDim && xel ? stk[kStRes + 12 + lane] + gx : real(0.0);
-          if constexpr (GEN) {
+          if constexpr (GEN == 1 && SRBD_B2_GENVEC) {
+            // D'gamma_corr = D'gamma_pred + sigma mu D'e + D'z (gamma is affine in both)
+            if (lane < kMaxDim && uel) {
+              const real* v = c.gv(k);
+              rt += v[lane] + v[24 + lane] + sigma_mu * v[12 + lane];
+            }
+          } else if constexpr (GEN) {
             real ra, qa;
             g_grad(k, true, sigma_mu, ra, qa);
             if (lane < kMaxDim && uel) rt += ra;
@@ -1214,6 +1251,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   }
   if constexpr (PH == kPhF1 || PH == kPhF2) {
     constexpr bool corr = PH == kPhF2;
+    // F1 with C-free general rows: D'z goes through the group's first LDS block
+    real* const f1_lds_grp = group_lds_blocks();
     real ap = real(1e30), ad = real(1e30);
     real s1 = real(0.0), s2 = real(0.0);  // predictor sums lam dt + t dlam, dlam dt (element-owned)
     bool bad = false;  // a non-finite component in the final step (fp32 breakdown)
@@ -1271,9 +1310,16 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         }
         if constexpr (GEN) {
           // general rows: dv = C dx + D du, dt / dlam, step ratios
+          // (GEN == 1, F1: z_i = ml dlam_l dt_l / t_l - mu dlam_u dt_u / t_u and D'z, the
+          // predictor-product part of the corrector's D'gamma, for B2)
+          constexpr bool kZ = GEN == 1 && SRBD_B2_GENVEC && !corr;
+          real gza = real(0.0);
           for (int ch = 0; ch < c.nch; ++ch) {
             real* g = c.gs(k, ch);
-            const real dv = c.g_row_dot_b(k, ch, lane, dxk, du);
+            real Cr[12], Dr[12];
+            c.g_row(k, ch, lane, Cr, Dr);
+            const real dv = dot_bcast(Dr, du, GEN == 2 ? dot_bcast(Cr, dxk, real(0.0)) : real(0.0));
+            real z = real(0.0);
             if (lane < kMaxDim) {
               const Side sg = c.side_g(k, ch, lane);
               const Bar bg = load_gbar(g, lane);
@@ -1289,7 +1335,25 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
               ratio(sg, bg, d, ap, ad);
               if (!corr) aff_sums(sg, bg, d, s1, s2);
               store_gstep(g, lane, d);
+              if constexpr (kZ) {
+                if (sg.ml != real(0.0)) z += d.dll * d.dtl / bg.tl;
+                if (sg.mu != real(0.0)) z -= d.dlu * d.dtu / bg.tu;
+              }
             }
+            if constexpr (kZ) {
+              // (D'z)_j = sum_i D[i][j] z_i: row i's products through this group's LDS
+              // block, summed down column j by lane j
+              real Y[12], M[12];
+              sfor<0, 12>([&](auto j) { Y[decltype(j)::value] = Dr[decltype(j)::value] * z; });
+              lds_put_col(f1_lds_grp, lane, Y);
+              lds_wave_fence();
+              lds_get_row(f1_lds_grp, li, M);
+              sfor<0, 12>([&](auto i) { gza += M[decltype(i)::value]; });
+              lds_wave_fence();
+            }
+          }
+          if constexpr (kZ) {
+            if (lane < kMaxDim) c.gv(k)[24 + lane] = gza;
           }
         }
         if (lane < kMaxDim) {

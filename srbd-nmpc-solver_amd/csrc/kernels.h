@@ -71,6 +71,10 @@ static_assert(kIpmStage % 2 == 0, "16-byte aligned stages");
 // kIpmStage: bars lam_l / lam_u / t_l / t_u [4][12], steps [4][12], row values
 // C x + D u [12], 4 pad
 constexpr int kGenChunk = 112;
+// general rows, per stage after the chunks: the corrector's u-gradient D'gamma in
+// parts (C = NULL kernels): D'gamma_pred [12] (RB), D'e [12] with e = d gamma / d(sigma mu)
+// (RB), D'z [12] with z the predictor-product term of gamma_corr (F1)
+constexpr int kGenVec = 36;
 
 size_t ws_doubles_ipm(int N, int ng);  // elements per QP (either precision)
 template <typename T>
