@@ -52,6 +52,8 @@ WORKLOADS = {
                      "f32"),
 }
 DEFAULT_WORKLOAD = "unconstr_n20"
+# settings.f64_rescue of the cone_n40_f32_f64_rescue line (fp32 iterations before the fp64 re-solve)
+RESCUE_CAP = 12
 
 
 def log(*a):
@@ -145,6 +147,9 @@ def main():
                     help="skip the IPM workloads (configs 3 and 5) measured beside the default line")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip the on-device SQP-iteration measurement (linearise + solve + line search)")
+    ap.add_argument("--f64-rescue", type=int, default=0,
+                    help="fp32 workloads: settings.f64_rescue = n (the fp32 pass runs at most n "
+                         "iterations, the QPs it leaves unsolved are solved again in fp64)")
     args = ap.parse_args()
 
     import torch
@@ -189,6 +194,7 @@ def main():
     sol = SolT(**{k: (sol_t[k].data_ptr() if k in sol_t else None) for k in capi.SOL_FIELDS})
     # solver settings of the reference caller (NMPC_solver.cpp:70-82)
     settings = capi.settings_struct(F32_SETTINGS if dtype == "f32" else NMPC_SETTINGS)
+    settings.f64_rescue = int(args.f64_rescue)
     stream_ptr = h.stream()
     ext = torch.cuda.ExternalStream(stream_ptr, device=device)
 
@@ -268,6 +274,8 @@ def main():
         torch.cuda.empty_cache()
         secondary = {w: secondary_workload(pkg, capi, w, device, args.seed)
                      for w in ("box_u_n20", "cone_n40_f32")}
+        secondary["cone_n40_f32_f64_rescue"] = secondary_workload(pkg, capi, "cone_n40_f32", device,
+                                                                  args.seed, rescue=RESCUE_CAP)
         secondary["nmpc_step_config1"] = nmpc_config1(pkg, capi, device, args.seed,
                                                       with_cpu=not args.no_cpu_baseline)
 
@@ -316,10 +324,12 @@ def main():
         dist.destroy_process_group()
 
 
-def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1):
+def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=0):
     """One IPM workload (its own handle and synthetic shard) timed the same way as
     the main line: kernel time from HIP events on the handle's stream, wall time
-    around `steps` solves.  Reported beside `value`, never as it."""
+    around `steps` solves.  Reported beside `value`, never as it.  rescue = n > 0 runs
+    an fp32 workload with settings.f64_rescue = n (the fp32 pass capped at n
+    iterations, the QPs it leaves unsolved solved again in fp64)."""
     import torch
     N, constraints, batch, desc = WORKLOADS[name][:4]
     dtype = WORKLOADS[name][4] if len(WORKLOADS[name]) > 4 else "f64"
@@ -337,6 +347,7 @@ def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1):
     data = DataT(**{k: (None if dt.get(k) is None else dt[k].data_ptr()) for k in capi.DATA_FIELDS})
     sol = SolT(**{k: (sol_t[k].data_ptr() if k in sol_t else None) for k in capi.SOL_FIELDS})
     settings = capi.settings_struct(F32_SETTINGS if dtype == "f32" else NMPC_SETTINGS)
+    settings.f64_rescue = int(rescue)  # 0: off
     ext = torch.cuda.ExternalStream(h.stream(), device=device)
     for _ in range(warmup):
         h.solve_device(batch, settings, data, sol)
@@ -357,7 +368,10 @@ def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1):
     bytes_qp = alg_bytes_per_qp(N, constraints=constraints, elem=elem)
     it = float(iters.mean())
     traffic = pmc_traffic(name, batch)
-    out = {"description": desc, "dtype": dtype, "batch": batch, "N": N, "steps": steps,
+    if rescue:
+        desc += (f"; settings.f64_rescue = {rescue}: the fp32 pass runs at most {rescue} iterations, "
+                 "the QPs it leaves unsolved are solved again in fp64 (their iter is the fp64 solve's)")
+    out = {"description": desc, "dtype": dtype + ("+f64 rescue" if rescue else ""), "batch": batch, "N": N, "steps": steps,
            "value": batch * steps / t_wall, "unit": "QP solves/s", "kernel_ms": kernel_ms,
            "success_rate": float((status == 0).mean()), "iters_mean": it,
            "iters_max": int(iters.max()),

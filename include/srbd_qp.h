@@ -76,7 +76,7 @@
 extern "C" {
 #endif
 
-#define SRBD_QP_ABI_VERSION 7
+#define SRBD_QP_ABI_VERSION 8
 #define SRBD_QP_MAX_NX 12
 #define SRBD_QP_MAX_NU 12
 #define SRBD_QP_MAX_NG 64
@@ -140,6 +140,15 @@ typedef struct srbd_qp_settings {
                           * given, hold the solution's KKT residual norms and
                           * objective (HPIPM's comp_res_exit; one extra pass over
                           * the QP data); 0 = they are zero-filled              */
+  int f64_rescue;   /* fp32 solves with constraints only (ignored otherwise):
+                     * 0 (default) = HPIPM's s_ocp_qp_ipm behaviour; n > 0 =
+                     * the fp32 pass runs min(n, iter_max) iterations, then
+                     * every QP it left with status != Success is solved again,
+                     * cold, by the fp64 kernels (iter_max as given) on its data
+                     * widened to fp64, and its outputs (x, u, pi, P, p, K, k,
+                     * status, iter, res, obj, stat) are the fp64 solve's,
+                     * narrowed.  The call then waits for the fp32 pass (it
+                     * counts the QPs to re-solve on the host).             */
 } srbd_qp_settings;
 
 typedef struct srbd_qp_data_f64 {

@@ -1111,7 +1111,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     const real musum_all = gsum(lane < kMaxDim ? musum : real(0.0));
     const real mu = musum_all * nc_inv;
     real* const stat_row = a.stat && lane == 0
-                           ? a.stat + ((size_t)qp * (a.iter_max + 2) + iter) * kStatCols
+                           ? a.stat + ((size_t)qp * a.stat_rows + iter) * kStatCols
                            : nullptr;
     if (stat_row) {
       stat_row[5] = mu;
@@ -1391,7 +1391,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         dxk = dxn;
       }
     real* const next = a.stat && lane == 0
-                             ? a.stat + ((size_t)qp * (a.iter_max + 2) + iter + 1) * kStatCols
+                             ? a.stat + ((size_t)qp * a.stat_rows + iter + 1) * kStatCols
                              : nullptr;  // HPIPM stores step kk in row kk+1
     if (!corr) {
       // alpha_aff, mu_aff, sigma: sum (lam + a dlam)(t + a dt) = S0 + a S1 + a^2 S2

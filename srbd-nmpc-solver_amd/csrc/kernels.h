@@ -42,6 +42,7 @@ struct ProblemArgsT {
   T reg;
   // IPM settings (hpipm-cpp OcpQpIpmSolverSettings semantics)
   int iter_max, pred_corr, split_step, warm_start;
+  int stat_rows;  // rows per QP of `stat` (the caller's iter_max + 2)
   T alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp;
 };
 using ProblemArgs = ProblemArgsT<double>;
@@ -114,5 +115,14 @@ hipError_t launch_nmpc_after(int batch, int it, const int* conv, int* done, int*
 hipError_t launch_srbd_linearize(const srbd_model_params& p, int batch, int N, int mode,
                                  const double* xs, const double* us,
                                  const srbd_qp_data_f64& out, hipStream_t stream);
+
+// rescue.hip (srbd_qp_settings.f64_rescue): list the QPs with status != 0 in batch
+// order, widen / narrow QP-major rows of `elems` values between fp32 and fp64
+hipError_t launch_select_unsolved(const int* status, int batch, int* idx, int* count, hipStream_t s);
+hipError_t launch_gather_widen(const float* src, double* dst, const int* idx, int rows, size_t elems,
+                               hipStream_t s);
+hipError_t launch_scatter_narrow(const double* src, float* dst, const int* idx, int rows, size_t elems,
+                                 hipStream_t s);
+hipError_t launch_scatter_int(const int* src, int* dst, const int* idx, int rows, hipStream_t s);
 
 }  // namespace srbd

@@ -419,7 +419,7 @@ __global__ void __launch_bounds__(256) unconstr_residuals_kernel(ProblemArgsT<re
     }
     if (a.obj) a.obj[qp] = ob;
     if (a.stat) {  // row 0 (iteration 0): mu = 0, res_stat, res_eq, res_ineq, res_comp, obj
-      real* row = a.stat + (size_t)qp * (a.iter_max + 2) * kStatCols;
+      real* row = a.stat + (size_t)qp * a.stat_rows * kStatCols;
       row[6] = mg;
       row[7] = mb;
       row[10] = ob;

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace {
@@ -48,6 +49,12 @@ struct srbd_qp_handle_s {
   void* nmpc = nullptr;
   size_t nmpc_bytes = 0;
   int* nmpc_active_host = nullptr;  // pinned
+  // settings.f64_rescue: unsolved-QP list + status (capacity ints each, then the count),
+  // and the compact fp64 batch, allocated on first use
+  int* resc_idx = nullptr;
+  int* resc_count_host = nullptr;  // pinned
+  void* resc = nullptr;
+  size_t resc_bytes = 0;
 };
 
 extern "C" {
@@ -96,6 +103,7 @@ void srbd_qp_default_settings(srbd_qp_settings* s) {
   s->ric_alg = 1;
   s->split_step = 0;
   s->compute_residuals = 1;  // HPIPM's comp_res_exit
+  s->f64_rescue = 0;
 }
 
 int srbd_qp_check_settings(const srbd_qp_settings* s) {
@@ -180,6 +188,9 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   if (h->pad) hipFree(h->pad);
   if (h->nmpc) hipFree(h->nmpc);
   if (h->nmpc_active_host) hipHostFree(h->nmpc_active_host);
+  if (h->resc_idx) hipFree(h->resc_idx);
+  if (h->resc) hipFree(h->resc);
+  if (h->resc_count_host) hipHostFree(h->resc_count_host);
   if (h->stream) hipStreamDestroy(h->stream);
   hipSetDevice(prev);
   delete h;
@@ -220,6 +231,10 @@ static int validate_call(srbd_qp_handle h, int batch, const srbd_qp_settings* st
   return SRBD_QP_OK;
 }
 
+static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                             const srbd_qp_data_f32* d, const srbd_qp_solution_f32* s,
+                             const int* status, hipStream_t strm, int* rc);
+
 template <typename T, typename DataT, typename SolT>
 static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, const DataT* d,
                       const SolT* s, void* stream) {
@@ -230,6 +245,19 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   int prev = 0;
   hipGetDevice(&prev);
   hipSetDevice(h->device);
+  // fp32 with f64_rescue: the status the fp32 pass leaves decides what is solved again
+  const bool rescue = std::is_same_v<T, float> && st->f64_rescue && constrained(h->dims);
+  if (rescue && !h->resc_idx) {
+    hipError_t ea = hipMalloc(reinterpret_cast<void**>(&h->resc_idx),
+                              sizeof(int) * (2 * (size_t)h->capacity + 1));
+    if (ea == hipSuccess) ea = hipHostMalloc(reinterpret_cast<void**>(&h->resc_count_host), sizeof(int));
+    if (ea != hipSuccess) {
+      hipSetDevice(prev);
+      return fail(SRBD_QP_ENOMEM, std::string("rescue buffers: ") + hipGetErrorString(ea));
+    }
+  }
+  int* status = s->status;
+  if (rescue && !status) status = h->resc_idx + h->capacity;
   srbd::ProblemArgsT<T> a{};
   a.batch = batch;
   a.N = h->dims.N;
@@ -244,12 +272,15 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   a.C = d->C; a.D = d->D; a.lg = d->lg; a.ug = d->ug; a.lg_mask = d->lg_mask; a.ug_mask = d->ug_mask;
   a.x = s->x; a.u = s->u; a.pi = s->pi;
   a.P = s->P; a.p = s->p; a.K = s->K; a.k = s->k;
-  a.status = s->status; a.iter = s->iter; a.res = s->res; a.obj = s->obj;
+  a.status = status; a.iter = s->iter; a.res = s->res; a.obj = s->obj;
   a.stat = s->stat;
   a.ws = reinterpret_cast<T*>(h->ws);
   a.ws_qp = h->ws_qp;
   a.reg = st->reg_prim;
   a.iter_max = st->iter_max;
+  a.stat_rows = st->iter_max + 2;
+  // f64_rescue = n: the fp32 pass stops after n iterations at most, the rest is fp64's
+  if (rescue && st->f64_rescue < a.iter_max) a.iter_max = st->f64_rescue;
   a.pred_corr = st->pred_corr;
   a.split_step = st->split_step;
   a.warm_start = st->warm_start;
@@ -281,6 +312,14 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   } else if (constrained(h->dims)) {
     e = srbd::launch_ipm_box(run, strm);
     if (e == hipSuccess && padded) e = srbd::unpad_solution<T>(a, run, strm);
+    if constexpr (std::is_same_v<T, float>) {
+      if (e == hipSuccess && rescue) {
+        hipSetDevice(prev);
+        e = rescue_f32(h, batch, st, d, s, status, strm, &rc);
+        if (rc) return rc;
+        hipSetDevice(h->device);
+      }
+    }
   } else {
     e = srbd::launch_riccati_unconstr(run, strm);
     if (e == hipSuccess && padded) e = srbd::unpad_solution<T>(a, run, strm);
@@ -299,6 +338,95 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   hipSetDevice(prev);
   if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
   return SRBD_QP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// settings.f64_rescue: the QPs an fp32 pass left unsolved, solved again in fp64
+// ---------------------------------------------------------------------------
+static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                             const srbd_qp_data_f32* d, const srbd_qp_solution_f32* s,
+                             const int* status, hipStream_t strm, int* rc) {
+  *rc = SRBD_QP_OK;
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipSetDevice(h->device);
+  int* idx = h->resc_idx;
+  int* count = h->resc_idx + 2 * (size_t)h->capacity;
+  hipError_t e = srbd::launch_select_unsolved(status, batch, idx, count, strm);
+  if (e == hipSuccess) e = hipMemcpyAsync(h->resc_count_host, count, sizeof(int), hipMemcpyDeviceToHost, strm);
+  if (e == hipSuccess) e = hipStreamSynchronize(strm);
+  const int R = e == hipSuccess ? *h->resc_count_host : 0;
+  if (e != hipSuccess || R == 0) {
+    hipSetDevice(prev);
+    return e;
+  }
+  const srbd_qp_dims& m = h->dims;
+  const size_t N = (size_t)m.N, nx = (size_t)m.nx, nu = (size_t)m.nu, ng = (size_t)m.ng;
+  const size_t stat_e = srbd::kStatCols * (size_t)(st->iter_max + 2);
+  // (fp32 source, values per QP) of every input the caller passed, then every output
+  struct In { const float* src; size_t e; const double** dst; };
+  struct Out { float* dst; size_t e; double** src; };
+  srbd_qp_data_f64 d64{};
+  srbd_qp_solution_f64 s64{};
+  const In ins[] = {
+      {d->A, N * nx * nx, &d64.A}, {d->B, N * nx * nu, &d64.B}, {d->b, N * nx, &d64.b},
+      {d->Q, (N + 1) * nx * nx, &d64.Q}, {d->S, N * nu * nx, &d64.S}, {d->R, N * nu * nu, &d64.R},
+      {d->q, (N + 1) * nx, &d64.q}, {d->r, N * nu, &d64.r}, {d->x0, nx, &d64.x0},
+      {d->lbu, N * nu, &d64.lbu}, {d->ubu, N * nu, &d64.ubu}, {d->lbu_mask, N * nu, &d64.lbu_mask},
+      {d->ubu_mask, N * nu, &d64.ubu_mask}, {d->lbx, (N + 1) * nx, &d64.lbx},
+      {d->ubx, (N + 1) * nx, &d64.ubx}, {d->lbx_mask, (N + 1) * nx, &d64.lbx_mask},
+      {d->ubx_mask, (N + 1) * nx, &d64.ubx_mask}, {d->C, (N + 1) * ng * nx, &d64.C},
+      {d->D, N * ng * nu, &d64.D}, {d->lg, (N + 1) * ng, &d64.lg}, {d->ug, (N + 1) * ng, &d64.ug},
+      {d->lg_mask, (N + 1) * ng, &d64.lg_mask}, {d->ug_mask, (N + 1) * ng, &d64.ug_mask}};
+  const Out outs[] = {
+      {s->x, (N + 1) * nx, &s64.x}, {s->u, N * nu, &s64.u}, {s->pi, (N + 1) * nx, &s64.pi},
+      {s->P, (N + 1) * nx * nx, &s64.P}, {s->p, (N + 1) * nx, &s64.p}, {s->K, N * nu * nx, &s64.K},
+      {s->k, N * nu, &s64.k}, {s->res, 4, &s64.res}, {s->obj, 1, &s64.obj}, {s->stat, stat_e, &s64.stat}};
+  size_t per_qp = 0;  // doubles
+  for (const In& f : ins) per_qp += f.src ? f.e : 0;
+  for (const Out& f : outs) per_qp += f.dst ? f.e : 0;
+  const size_t need = sizeof(double) * per_qp * (size_t)R + 2 * sizeof(int) * (size_t)R + 256;
+  if (need > h->resc_bytes) {
+    if (h->resc) hipFree(h->resc);
+    h->resc = nullptr;
+    h->resc_bytes = 0;
+    e = hipMalloc(&h->resc, need);
+    if (e != hipSuccess) {
+      hipSetDevice(prev);
+      *rc = fail(SRBD_QP_ENOMEM, std::string("rescue batch: ") + hipGetErrorString(e));
+      return e;
+    }
+    h->resc_bytes = need;
+  }
+  double* cur = reinterpret_cast<double*>(h->resc);
+  for (const In& f : ins) {
+    if (!f.src || e != hipSuccess) continue;
+    e = srbd::launch_gather_widen(f.src, cur, idx, R, f.e, strm);
+    *f.dst = cur;
+    cur += f.e * (size_t)R;
+  }
+  for (const Out& f : outs) {
+    if (!f.dst) continue;
+    *f.src = cur;
+    cur += f.e * (size_t)R;
+  }
+  s64.status = reinterpret_cast<int*>(cur);
+  s64.iter = s64.status + R;
+  hipSetDevice(prev);
+  if (e != hipSuccess) return e;
+  // cold start (the caller's x / u now hold the fp32 pass's answer)
+  srbd_qp_settings st64 = *st;
+  st64.warm_start = 0;
+  st64.f64_rescue = 0;
+  *rc = solve_impl<double>(h, R, &st64, &d64, &s64, strm);
+  if (*rc) return hipSuccess;
+  hipSetDevice(h->device);
+  for (const Out& f : outs)
+    if (f.dst && e == hipSuccess) e = srbd::launch_scatter_narrow(*f.src, f.dst, idx, R, f.e, strm);
+  if (e == hipSuccess && s->status) e = srbd::launch_scatter_int(s64.status, s->status, idx, R, strm);
+  if (e == hipSuccess && s->iter) e = srbd::launch_scatter_int(s64.iter, s->iter, idx, R, strm);
+  hipSetDevice(prev);
+  return e;
 }
 
 // ---------------------------------------------------------------------------

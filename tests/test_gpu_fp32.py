@@ -78,3 +78,86 @@ def test_friction_cone_n40_fp32(pkg):
     ru = [np.linalg.norm(o32["u"][i] - o64["u"][i]) / np.linalg.norm(o64["u"][i])
           for i in np.nonzero(ok)[0]]
     assert np.median(ru) <= 3e-2 and np.max(ru) <= 2e-1, (np.median(ru), np.max(ru))
+
+
+def _rounded_to_f32(qp):
+    """The same batch with every array rounded to fp32 (what the fp32 path reads)."""
+    import dataclasses
+    kw = {}
+    for f in dataclasses.fields(qp):
+        v = getattr(qp, f.name)
+        kw[f.name] = v.astype(np.float32).astype(np.float64) if isinstance(v, np.ndarray) else v
+    return type(qp)(**kw)
+
+
+@pytest.mark.parametrize("cap,stats", [(30, False), (30, True), (12, False)])
+def test_f64_rescue_cone_n40(pkg, cap, stats):
+    """settings.f64_rescue = cap: the fp32 pass runs at most `cap` iterations, and the
+    QPs it leaves unsolved are solved again in fp64 on their data widened from fp32.
+    Every QP ends with status Success; the QPs fp32 solved keep their fp32 outputs
+    bit for bit (an fp32 solve with iter_max = cap); the rescued ones carry exactly
+    the fp64 solve of the fp32-rounded data (narrowed), iter and stat included
+    (per-QP arithmetic does not depend on the QP's place in a batch)."""
+    qp, x0 = pkg.srbd_model.generate_batch(512, N=40, seed=1005, constraints="cone")
+    st = dict(F32, tol_stat=3e-2)
+    plain = pkg.capi.solve(qp, x0, dict(st, iter_max=cap), dtype=np.float32, riccati=True,
+                           stats=stats)
+    resc = pkg.capi.solve(qp, x0, dict(st, f64_rescue=cap), dtype=np.float32, riccati=True,
+                          stats=stats)
+    o64 = pkg.capi.solve(_rounded_to_f32(qp), x0.astype(np.float32).astype(np.float64), st,
+                         riccati=True, stats=stats)
+    bad = plain["status"] != 0
+    assert bad.any(), "seed 1005 at N = 40 has fp32 failures (DESIGN.md 4.5)"
+    assert np.all(o64["status"] == 0)
+    assert np.all(resc["status"] == 0), np.bincount(resc["status"])
+    keys = ["x", "u", "pi", "P", "p", "K", "k", "iter", "res", "obj"] + (["stat"] if stats else [])
+    for key in keys:
+        assert np.array_equal(resc[key][~bad], plain[key][~bad]), key
+        want = o64[key][bad]
+        want = want if key == "iter" else want.astype(np.float32)
+        assert np.array_equal(resc[key][bad], want), key
+
+
+def test_f64_rescue_noop_without_failures(pkg):
+    """Nothing unsolved (box-u, fp32 converges everywhere at these settings): f64_rescue
+    changes no output bit."""
+    qp, x0 = pkg.srbd_model.generate_batch(64, N=20, seed=92, constraints="box_u")
+    st = dict(F32, tol_stat=3e-2)
+    a = pkg.capi.solve(qp, x0, st, dtype=np.float32)
+    b = pkg.capi.solve(qp, x0, dict(st, f64_rescue=30), dtype=np.float32)
+    assert np.all(a["status"] == 0)
+    for key in a:
+        assert np.array_equal(a[key], b[key]), key
+
+
+def test_f64_rescue_without_status_output_and_host_path(pkg):
+    """The rescue keeps its own status list when the caller passes no status buffer,
+    and the host-buffer entry point rescues the same QPs: x / u agree bit for bit."""
+    import torch
+    qp, x0 = pkg.srbd_model.generate_batch(256, N=40, seed=1005, constraints="cone")
+    st = dict(F32, tol_stat=3e-2, f64_rescue=12)
+    ref = pkg.capi.solve(qp, x0, st, dtype=np.float32)
+    h = pkg.capi.Handle(qp.N, qp.nx, qp.nu, qp.ng, qp.has_box_u, qp.has_box_x, capacity=qp.batch)
+    try:
+        s = pkg.capi.settings_struct(st)
+        dt, out, data, sol = pkg.capi.device_buffers(qp, x0, "cuda:0", dtype=np.float32)
+        sol.status = None
+        sol.iter = None
+        h.solve_device(qp.batch, s, data, sol)
+        h.synchronize()
+        torch.cuda.synchronize()
+        for key in ("x", "u", "pi"):
+            assert np.array_equal(out[key].cpu().numpy(), ref[key]), key
+        capi = pkg.capi
+        p = {k: (None if v is None else np.ascontiguousarray(v, dtype=np.float32))
+             for k, v in qp.packed().items()}
+        p["x0"] = np.ascontiguousarray(x0, dtype=np.float32)
+        hx = {k: np.zeros_like(ref[k]) for k in ("x", "u", "pi", "status")}
+        hdata = capi.Data32(**{k: (None if p.get(k) is None else p[k].ctypes.data)
+                               for k in capi.DATA_FIELDS})
+        hsol = capi.Solution32(**{k: v.ctypes.data for k, v in hx.items()})
+        h.solve_host(qp.batch, s, hdata, hsol)
+        for key in ("x", "u", "pi", "status"):
+            assert np.array_equal(hx[key], ref[key]), key
+    finally:
+        h.close()
