@@ -1441,8 +1441,14 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 }
 
 
+// fp64: 2 workgroups per CU (<= 256 VGPRs); fp32 boxes / C-free rows: 3 (<= 168 VGPRs, 3 waves
+// per SIMD -- the fp32 RB sweep sits just under that cliff and a free allocator crosses it:
+// cone 175 -> 194 ms); fp32 rows with C need 216 and stay at 2
+template <int GEN>
+constexpr int kIpmMinBlocks = sizeof(real) == 4 && GEN < 2 ? 3 : 2;
+
 template <bool FULL, int GEN, int PH>
-__global__ void __launch_bounds__(256, FULL ? 2 : 1) ipm_phase_kernel(ProblemArgsT<real> a) {
+__global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase_kernel(ProblemArgsT<real> a) {
   ipm_phase<FULL, GEN, PH>(a);
 }
 
@@ -1452,7 +1458,7 @@ __global__ void __launch_bounds__(256, FULL ? 2 : 1) ipm_phase_kernel(ProblemArg
 // The second phase re-reads the per-QP state the first one wrote (same wave:
 // visible after the workgroup-scope fence).
 template <bool FULL, int GEN, int PH1, int PH2>
-__global__ void __launch_bounds__(256, FULL ? 2 : 1) ipm_phase2_kernel(ProblemArgsT<real> a) {
+__global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase2_kernel(ProblemArgsT<real> a) {
   ipm_phase<FULL, GEN, PH1>(a);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   ipm_phase<FULL, GEN, PH2>(a);
