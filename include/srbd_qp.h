@@ -143,12 +143,14 @@ typedef struct srbd_qp_settings {
   int f64_rescue;   /* fp32 solves with constraints only (ignored otherwise):
                      * 0 (default) = HPIPM's s_ocp_qp_ipm behaviour; n > 0 =
                      * the fp32 pass runs min(n, iter_max) iterations, then
-                     * every QP it left with status != Success is solved again,
-                     * cold, by the fp64 kernels (iter_max as given) on its data
-                     * widened to fp64, and its outputs (x, u, pi, P, p, K, k,
-                     * status, iter, res, obj, stat) are the fp64 solve's,
-                     * narrowed.  The call then waits for the fp32 pass (it
-                     * counts the QPs to re-solve on the host).             */
+                     * every QP it left with status != Success continues in
+                     * fp64 (iter_max as given) on its data widened to fp64,
+                     * starting from the fp32 iterate (x, u, pi, lam, t; cold
+                     * when nx or nu < 12 or the iterate is not finite), and
+                     * its outputs (x, u, pi, P, p, K, k, status, iter, res,
+                     * obj, stat) are the fp64 solve's, narrowed.  The call
+                     * then waits for the fp32 pass (it counts the QPs to
+                     * re-solve on the host).                               */
 } srbd_qp_settings;
 
 typedef struct srbd_qp_data_f64 {

@@ -52,6 +52,33 @@ size_t ws_doubles_ipm(int N, int ng) {
          (size_t)(N + 1) * ((size_t)kIpmStage + (size_t)nch * kGenChunk + (nch ? kGenVec : 0));
 }
 
+namespace {
+__global__ void gather_warm_bars_kernel(const float* __restrict__ ws32, size_t ws_qp, int N,
+                                        size_t stride, int nch, const int* __restrict__ idx, int rows,
+                                        double* __restrict__ dst) {
+  const size_t W = 96 + (size_t)nch * 48, per_qp = (size_t)(N + 1) * W;
+  const size_t total = (size_t)rows * per_qp;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = t / per_qp, rem = t - r * per_qp, k = rem / W, j = rem - k * W;
+    const size_t off = j < 96 ? kStLam + j : kIpmStage + ((j - 96) / 48) * kGenChunk + (j - 96) % 48;
+    dst[t] = (double)ws32[(size_t)idx[r] * ws_qp + ipm_f32::kQsSize + k * stride + off];
+  }
+}
+}  // namespace
+
+hipError_t launch_gather_warm_bars(const float* ws32, size_t ws_qp, int N, int ng, const int* idx,
+                                   int rows, double* dst, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  const int nch = (ng + kMaxDim - 1) / kMaxDim;
+  const size_t stride = (size_t)kIpmStage + (size_t)nch * kGenChunk + (nch ? kGenVec : 0);
+  const size_t total = (size_t)rows * (N + 1) * (96 + (size_t)nch * 48);
+  const size_t blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(gather_warm_bars_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256),
+                     0, s, ws32, ws_qp, N, stride, nch, idx, rows, dst);
+  return hipGetLastError();
+}
+
 template <>
 hipError_t launch_ipm_box<double>(const ProblemArgsT<double>& a, hipStream_t stream) {
   return ipm_f64::launch(a, stream);

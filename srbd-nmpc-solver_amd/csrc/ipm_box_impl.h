@@ -520,7 +520,82 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   if constexpr (PH == kPhInit) {
   // =================== init (var_init_scheme 0, relative form) ===================
   real ncl = real(0.0);
-  for (int k = 0; k <= N; ++k) {
+  // warm_start 2: continue from a whole iterate -- x, u, pi from the solution buffers, the
+  // barrier state from a.warm_bars (HPIPM's warm_start = 2 level; used by the fp64
+  // continuation of srbd_qp_settings.f64_rescue).  A non-finite value or a t <= 0 anywhere
+  // in the QP falls back to the cold start.
+  const size_t warm_w = 96 + (size_t)c.nch * 48;
+  const real* wb = a.warm_start == 2 && a.warm_bars
+                       ? a.warm_bars + (size_t)c.oq() * (size_t)(N + 1) * warm_w
+                       : nullptr;
+  bool cont = false;
+  if (wb) {
+    int bad = 0;
+    auto chk = [&](real v, bool is_t) { bad |= !__builtin_isfinite(v) || (is_t && !(v > real(0.0))); };
+    for (int k = 0; k <= N && lane < kMaxDim; ++k) {
+      const real* w = wb + (size_t)k * warm_w;
+      for (int j = 0; j < 8; ++j) chk(w[j * 12 + lane], (j & 3) >= 2);
+      for (int ch = 0; ch < c.nch; ++ch)
+        for (int j = 0; j < 4; ++j) chk(w[96 + ch * 48 + j * 12 + lane], j >= 2);
+      if (k < N && uel) chk(c.u()[(size_t)k * nu + lane], false);
+      if (k > 0 && xel) {
+        chk(c.x()[(size_t)k * nx + lane], false);
+        chk(c.pi()[(size_t)k * nx + lane], false);
+      }
+    }
+    cont = gsum(real(bad)) == real(0.0);
+  }
+  if (cont) {
+    for (int k = 0; k <= N; ++k) {
+      real* stk = c.st(k);
+      const real* w = wb + (size_t)k * warm_w;
+      if (lane < kMaxDim)
+        for (int j = 0; j < 8; ++j) stk[kStLam + j * 12 + lane] = w[j * 12 + lane];
+      const real ui = (k < N && uel) ? c.u()[(size_t)k * nu + li] : real(0.0);
+      real xi;
+      if (k == 0) {
+        xi = xel ? c.x0()[li] : real(0.0);
+        if (xel) {
+          c.x()[lane] = xi;
+          c.pi()[lane] = real(0.0);
+        }
+      } else {
+        xi = xel ? c.x()[(size_t)k * nx + li] : real(0.0);
+      }
+      if (k < N) {
+        const Side s = c.side_u(k, lane);
+        ncl += s.ml + s.mu;
+      }
+      {
+        const Side s = c.side_x(k, lane);
+        ncl += s.ml + s.mu;
+      }
+      if constexpr (GEN) {
+        real bxi[12], bui[12];
+        gather12(xi, bxi);
+        gather12(ui, bui);
+        for (int ch = 0; ch < c.nch; ++ch) {
+          const real v = c.g_row_dot(k, ch, lane, bxi, bui);
+          const Side s = c.side_g(k, ch, lane);
+          ncl += s.ml + s.mu;
+          if (lane < kMaxDim) {
+            real* g = c.gs(k, ch);
+            for (int j = 0; j < 4; ++j) g[j * 12 + lane] = w[96 + ch * 48 + j * 12 + lane];
+            store_gstep(g, lane, BarStep{0, 0, 0, 0});
+            g[kGenVal + lane] = v;
+          }
+        }
+      }
+      if (lane < kMaxDim) {
+        stk[kStStep + lane] = real(0.0);
+        stk[kStStep + 12 + lane] = real(0.0);
+        stk[kStStep + 24 + lane] = real(0.0);
+        store_bstep(stk, 0, lane, BarStep{0, 0, 0, 0});
+        store_bstep(stk, 1, lane, BarStep{0, 0, 0, 0});
+      }
+    }
+  }
+  for (int k = 0; k <= N && !cont; ++k) {
     real* stk = c.st(k);
     real ui = real(0.0), xi = real(0.0);  // initial u_k, x_k (element-owned)
     // u_k

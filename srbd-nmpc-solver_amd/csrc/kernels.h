@@ -43,6 +43,9 @@ struct ProblemArgsT {
   // IPM settings (hpipm-cpp OcpQpIpmSolverSettings semantics)
   int iter_max, pred_corr, split_step, warm_start;
   int stat_rows;  // rows per QP of `stat` (the caller's iter_max + 2)
+  // warm_start 2 only (internal: the fp64 continuation of srbd_qp_settings.f64_rescue):
+  // per QP and stage the barrier state [kStLam block 96][nch chunks x 48], see ipm_box.hip
+  const T* warm_bars;
   T alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp;
 };
 using ProblemArgs = ProblemArgsT<double>;
@@ -124,5 +127,9 @@ hipError_t launch_gather_widen(const float* src, double* dst, const int* idx, in
 hipError_t launch_scatter_narrow(const double* src, float* dst, const int* idx, int rows, size_t elems,
                                  hipStream_t s);
 hipError_t launch_scatter_int(const int* src, int* dst, const int* idx, int rows, hipStream_t s);
+// ipm_box.hip: the barrier state of the fp32 IPM workspace rows idx[0..rows), widened into the
+// warm_bars layout of ProblemArgsT (rows x (N+1) x (96 + nch*48) doubles)
+hipError_t launch_gather_warm_bars(const float* ws32, size_t ws_qp, int N, int ng, const int* idx,
+                                   int rows, double* dst, hipStream_t s);
 
 }  // namespace srbd

@@ -235,9 +235,10 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
                              const srbd_qp_data_f32* d, const srbd_qp_solution_f32* s,
                              const int* status, hipStream_t strm, int* rc);
 
+// warm_bars: warm_start 2 only (the fp64 continuation of rescue_f32), see ProblemArgsT
 template <typename T, typename DataT, typename SolT>
 static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, const DataT* d,
-                      const SolT* s, void* stream) {
+                      const SolT* s, void* stream, const T* warm_bars = nullptr) {
   int rc = validate_call(h, batch, st, d, s);
   if (rc) return rc;
   if (batch == 0) return SRBD_QP_OK;
@@ -279,6 +280,7 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   a.reg = st->reg_prim;
   a.iter_max = st->iter_max;
   a.stat_rows = st->iter_max + 2;
+  a.warm_bars = warm_bars;
   // f64_rescue = n: the fp32 pass stops after n iterations at most, the rest is fp64's
   if (rescue && st->f64_rescue < a.iter_max) a.iter_max = st->f64_rescue;
   a.pred_corr = st->pred_corr;
@@ -382,7 +384,11 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
       {s->x, (N + 1) * nx, &s64.x}, {s->u, N * nu, &s64.u}, {s->pi, (N + 1) * nx, &s64.pi},
       {s->P, (N + 1) * nx * nx, &s64.P}, {s->p, (N + 1) * nx, &s64.p}, {s->K, N * nu * nx, &s64.K},
       {s->k, N * nu, &s64.k}, {s->res, 4, &s64.res}, {s->obj, 1, &s64.obj}, {s->stat, stat_e, &s64.stat}};
-  size_t per_qp = 0;  // doubles
+  // fp64 continuation from the fp32 iterate (x, u, pi and the barrier state: HPIPM's
+  // warm_start = 2) on 12 x 12 stages; a padded problem is re-solved cold
+  const bool cont = m.nx == 12 && m.nu == 12;
+  const size_t warm_e = cont ? (N + 1) * (96 + (size_t)((m.ng + 11) / 12) * 48) : 0;
+  size_t per_qp = warm_e;  // doubles
   for (const In& f : ins) per_qp += f.src ? f.e : 0;
   for (const Out& f : outs) per_qp += f.dst ? f.e : 0;
   const size_t need = sizeof(double) * per_qp * (size_t)R + 2 * sizeof(int) * (size_t)R + 256;
@@ -410,15 +416,26 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
     *f.src = cur;
     cur += f.e * (size_t)R;
   }
+  double* warm = cur;
+  cur += warm_e * (size_t)R;
   s64.status = reinterpret_cast<int*>(cur);
   s64.iter = s64.status + R;
+  if (cont && e == hipSuccess) {
+    // the iterate the fp32 pass ended on: x, u, pi (caller's buffers), barrier state (its
+    // workspace, read before the fp64 solve reuses that memory)
+    e = srbd::launch_gather_widen(s->x, s64.x, idx, R, (N + 1) * nx, strm);
+    if (e == hipSuccess) e = srbd::launch_gather_widen(s->u, s64.u, idx, R, N * nu, strm);
+    if (e == hipSuccess) e = srbd::launch_gather_widen(s->pi, s64.pi, idx, R, (N + 1) * nx, strm);
+    if (e == hipSuccess)
+      e = srbd::launch_gather_warm_bars(reinterpret_cast<const float*>(h->ws), h->ws_qp, m.N, m.ng, idx,
+                                        R, warm, strm);
+  }
   hipSetDevice(prev);
   if (e != hipSuccess) return e;
-  // cold start (the caller's x / u now hold the fp32 pass's answer)
   srbd_qp_settings st64 = *st;
-  st64.warm_start = 0;
+  st64.warm_start = cont ? 2 : 0;
   st64.f64_rescue = 0;
-  *rc = solve_impl<double>(h, R, &st64, &d64, &s64, strm);
+  *rc = solve_impl<double>(h, R, &st64, &d64, &s64, strm, cont ? warm : nullptr);
   if (*rc) return hipSuccess;
   hipSetDevice(h->device);
   for (const Out& f : outs)

@@ -93,19 +93,19 @@ def _rounded_to_f32(qp):
 @pytest.mark.parametrize("cap,stats", [(30, False), (30, True), (12, False)])
 def test_f64_rescue_cone_n40(pkg, cap, stats):
     """settings.f64_rescue = cap: the fp32 pass runs at most `cap` iterations, and the
-    QPs it leaves unsolved are solved again in fp64 on their data widened from fp32.
-    Every QP ends with status Success; the QPs fp32 solved keep their fp32 outputs
-    bit for bit (an fp32 solve with iter_max = cap); the rescued ones carry exactly
-    the fp64 solve of the fp32-rounded data (narrowed), iter and stat included
-    (per-QP arithmetic does not depend on the QP's place in a batch)."""
+    QPs it leaves unsolved continue in fp64 from the iterate it ended on (x, u, pi and
+    the barrier state: HPIPM's warm_start = 2).  Every QP ends with status Success
+    within the tolerances; the QPs fp32 solved keep their fp32 outputs bit for bit (an
+    fp32 solve with iter_max = cap); the rescued ones land at the fp64 KKT point to the
+    accuracy the stationarity tolerance allows (the bound of test_friction_cone_n40_fp32)
+    in a few fp64 iterations."""
     qp, x0 = pkg.srbd_model.generate_batch(512, N=40, seed=1005, constraints="cone")
     st = dict(F32, tol_stat=3e-2)
     plain = pkg.capi.solve(qp, x0, dict(st, iter_max=cap), dtype=np.float32, riccati=True,
                            stats=stats)
     resc = pkg.capi.solve(qp, x0, dict(st, f64_rescue=cap), dtype=np.float32, riccati=True,
                           stats=stats)
-    o64 = pkg.capi.solve(_rounded_to_f32(qp), x0.astype(np.float32).astype(np.float64), st,
-                         riccati=True, stats=stats)
+    o64 = pkg.capi.solve(qp, x0, NMPC)
     bad = plain["status"] != 0
     assert bad.any(), "seed 1005 at N = 40 has fp32 failures (DESIGN.md 4.5)"
     assert np.all(o64["status"] == 0)
@@ -113,6 +113,31 @@ def test_f64_rescue_cone_n40(pkg, cap, stats):
     keys = ["x", "u", "pi", "P", "p", "K", "k", "iter", "res", "obj"] + (["stat"] if stats else [])
     for key in keys:
         assert np.array_equal(resc[key][~bad], plain[key][~bad]), key
+    assert np.all(resc["res"][bad][:, 0] <= st["tol_stat"])
+    assert np.all(resc["res"][bad][:, 1:] <= 1e-3)
+    ru = [np.linalg.norm(resc["u"][i] - o64["u"][i]) / np.linalg.norm(o64["u"][i])
+          for i in np.nonzero(bad)[0]]
+    assert np.median(ru) <= 3e-2 and np.max(ru) <= 2e-1, (np.median(ru), np.max(ru))
+    # the continuation starts near the solution: far fewer iterations than a cold fp64 solve
+    assert resc["iter"][bad].mean() < 0.6 * o64["iter"][bad].mean(), (
+        resc["iter"][bad].mean(), o64["iter"][bad].mean())
+
+
+def test_f64_rescue_padded_is_a_cold_fp64_solve(pkg):
+    """nx, nu < 12 (the 12 x 12 embedding): the rescue re-solves cold, so a rescued QP's
+    outputs are exactly the fp64 solve of its fp32-rounded data, narrowed (per-QP
+    arithmetic does not depend on the QP's place in a batch).  fp32 cannot reach tol
+    1e-8, so every QP is rescued."""
+    qp, x0 = helpers.random_constrained(64, 8, 8, 4, 6, 31, pkg.OcpQpBatch)
+    st = dict(iter_max=30, tol_stat=1e-8, tol_eq=1e-8, tol_ineq=1e-8, tol_comp=1e-8)
+    plain = pkg.capi.solve(qp, x0, st, dtype=np.float32)
+    resc = pkg.capi.solve(qp, x0, dict(st, f64_rescue=30), dtype=np.float32, riccati=True)
+    o64 = pkg.capi.solve(_rounded_to_f32(qp), x0.astype(np.float32).astype(np.float64), st,
+                         riccati=True)
+    bad = plain["status"] != 0
+    assert bad.mean() > 0.5
+    assert np.all(o64["status"] == 0) and np.all(resc["status"] == 0)
+    for key in ["x", "u", "pi", "P", "p", "K", "k", "iter", "res", "obj"]:
         want = o64[key][bad]
         want = want if key == "iter" else want.astype(np.float32)
         assert np.array_equal(resc[key][bad], want), key
