@@ -54,6 +54,8 @@ WORKLOADS = {
 DEFAULT_WORKLOAD = "unconstr_n20"
 # settings.f64_rescue of the cone_n40_f32_f64_rescue line (fp32 iterations before the fp64 re-solve)
 RESCUE_CAP = 12
+# settings.f32_iters of the box_u_n20_mixed line (fp32 iterations before fp64 takes over)
+MIXED_F32_ITERS = 6
 
 
 def log(*a):
@@ -274,6 +276,8 @@ def main():
         torch.cuda.empty_cache()
         secondary = {w: secondary_workload(pkg, capi, w, device, args.seed)
                      for w in ("box_u_n20", "cone_n40_f32")}
+        secondary["box_u_n20_mixed"] = secondary_workload(pkg, capi, "box_u_n20", device, args.seed,
+                                                          f32_iters=MIXED_F32_ITERS)
         secondary["cone_n40_f32_f64_rescue"] = secondary_workload(pkg, capi, "cone_n40_f32", device,
                                                                   args.seed, rescue=RESCUE_CAP)
         secondary["nmpc_step_config1"] = nmpc_config1(pkg, capi, device, args.seed,
@@ -324,12 +328,15 @@ def main():
         dist.destroy_process_group()
 
 
-def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=0):
+def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=0, f32_iters=0):
     """One IPM workload (its own handle and synthetic shard) timed the same way as
     the main line: kernel time from HIP events on the handle's stream, wall time
     around `steps` solves.  Reported beside `value`, never as it.  rescue = n > 0 runs
     an fp32 workload with settings.f64_rescue = n (the fp32 pass capped at n
-    iterations, the QPs it leaves unsolved solved again in fp64)."""
+    iterations, the QPs it leaves unsolved solved again in fp64).  f32_iters = n > 0
+    runs an fp64 workload as the mixed-precision IPM (settings.f32_iters: n fp32
+    iterations, then fp64 to the fp64 tolerances) and reports its distance to the
+    plain fp64 solve of the same shard."""
     import torch
     N, constraints, batch, desc = WORKLOADS[name][:4]
     dtype = WORKLOADS[name][4] if len(WORKLOADS[name]) > 4 else "f64"
@@ -348,6 +355,7 @@ def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=
     sol = SolT(**{k: (sol_t[k].data_ptr() if k in sol_t else None) for k in capi.SOL_FIELDS})
     settings = capi.settings_struct(F32_SETTINGS if dtype == "f32" else NMPC_SETTINGS)
     settings.f64_rescue = int(rescue)  # 0: off
+    settings.f32_iters = int(f32_iters)  # 0: off
     ext = torch.cuda.ExternalStream(h.stream(), device=device)
     for _ in range(warmup):
         h.solve_device(batch, settings, data, sol)
@@ -368,10 +376,30 @@ def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=
     bytes_qp = alg_bytes_per_qp(N, constraints=constraints, elem=elem)
     it = float(iters.mean())
     traffic = pmc_traffic(name, batch)
+    mixed = None
+    if f32_iters:
+        desc += (f"; settings.f32_iters = {f32_iters}: the first {f32_iters} IPM iterations in fp32 "
+                 "on a narrowed copy of the data, then fp64 from that iterate to the fp64 tolerances "
+                 "(iter counts the fp64 iterations)")
+        u_mix, x_mix = sol_t["u"].clone(), sol_t["x"].clone()
+        settings.f32_iters = 0
+        h.solve_device(batch, settings, data, sol)
+        h.synchronize()
+        # per-QP max-norm distance relative to the fp64 solution's max norm; both solves stop
+        # at the NMPC tolerance (1e-4), so the worst QPs differ by a tolerance-level step
+        rel = lambda a, b: ((a - b).abs().amax(dim=(1, 2)) / b.abs().amax(dim=(1, 2)))
+        du, dx = rel(u_mix, sol_t["u"]), rel(x_mix, sol_t["x"])
+        mixed = {"u_rel_diff_vs_fp64": {"max": float(du.max()), "median": float(du.median()),
+                                        "p99": float(du.quantile(0.99))},
+                 "x_rel_diff_vs_fp64": {"max": float(dx.max()), "median": float(dx.median()),
+                                        "p99": float(dx.quantile(0.99))},
+                 "fp64_success_rate": float((sol_t["status"] == 0).float().mean())}
     if rescue:
         desc += (f"; settings.f64_rescue = {rescue}: the fp32 pass runs at most {rescue} iterations, "
                  "the QPs it leaves unsolved are solved again in fp64 (their iter is the fp64 solve's)")
-    out = {"description": desc, "dtype": dtype + ("+f64 rescue" if rescue else ""), "batch": batch, "N": N, "steps": steps,
+    dtype_s = dtype + ("+f64 rescue" if rescue else "") + (f" (first {f32_iters} iterations f32)"
+                                                          if f32_iters else "")
+    out = {"description": desc, "dtype": dtype_s, "batch": batch, "N": N, "steps": steps,
            "value": batch * steps / t_wall, "unit": "QP solves/s", "kernel_ms": kernel_ms,
            "success_rate": float((status == 0).mean()), "iters_mean": it,
            "iters_max": int(iters.max()),
@@ -380,6 +408,11 @@ def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=
            "hbm_alg_bytes_per_iter_frac": bytes_qp * it * batch / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
            "hbm_traffic_per_solve": traffic,
            "hbm_actual_tbs": None if traffic is None else traffic / (kernel_ms * 1e-3) / 1e12}
+    if mixed is not None:
+        out["mixed_precision"] = mixed
+        # iterations of two precisions; the PMC traffic on file is the fp64 solve's
+        out["hbm_alg_bytes_per_iter_frac"] = None
+        out["hbm_traffic_per_solve"] = out["hbm_actual_tbs"] = None
     log(f"[secondary] {name}: kernel {kernel_ms:.2f} ms, {out['value']:.4g} QP/s, "
         f"success {out['success_rate']:.3f}, iters {it:.2f}")
     del h

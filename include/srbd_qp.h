@@ -151,6 +151,14 @@ typedef struct srbd_qp_settings {
                      * obj, stat) are the fp64 solve's, narrowed.  The call
                      * then waits for the fp32 pass (it counts the QPs to
                      * re-solve on the host).                               */
+  int f32_iters;    /* fp64 solves with constraints on 12 x 12 stages only
+                     * (ignored otherwise): 0 (default) = fp64 throughout;
+                     * n > 0 = a mixed-precision IPM: the data is narrowed
+                     * once to fp32, the first min(n, iter_max) iterations run
+                     * in fp32 (half the bytes per sweep), and the fp64 IPM
+                     * continues from that iterate (x, u, pi, lam, t) on the
+                     * caller's fp64 data to the fp64 tolerances; iter and stat
+                     * count the fp64 iterations.                           */
 } srbd_qp_settings;
 
 typedef struct srbd_qp_data_f64 {

@@ -62,7 +62,8 @@ __global__ void gather_warm_bars_kernel(const float* __restrict__ ws32, size_t w
        t += (size_t)gridDim.x * blockDim.x) {
     const size_t r = t / per_qp, rem = t - r * per_qp, k = rem / W, j = rem - k * W;
     const size_t off = j < 96 ? kStLam + j : kIpmStage + ((j - 96) / 48) * kGenChunk + (j - 96) % 48;
-    dst[t] = (double)ws32[(size_t)idx[r] * ws_qp + ipm_f32::kQsSize + k * stride + off];
+    const size_t q = idx ? (size_t)idx[r] : r;
+    dst[t] = (double)ws32[q * ws_qp + ipm_f32::kQsSize + k * stride + off];
   }
 }
 }  // namespace

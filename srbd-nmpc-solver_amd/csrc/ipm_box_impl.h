@@ -534,7 +534,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     auto chk = [&](real v, bool is_t) { bad |= !__builtin_isfinite(v) || (is_t && !(v > real(0.0))); };
     for (int k = 0; k <= N && lane < kMaxDim; ++k) {
       const real* w = wb + (size_t)k * warm_w;
-      for (int j = 0; j < 8; ++j) chk(w[j * 12 + lane], (j & 3) >= 2);
+      for (int j = k < N ? 0 : 4; j < 8; ++j) chk(w[j * 12 + lane], (j & 3) >= 2);  // (no u_N)
       for (int ch = 0; ch < c.nch; ++ch)
         for (int j = 0; j < 4; ++j) chk(w[96 + ch * 48 + j * 12 + lane], j >= 2);
       if (k < N && uel) chk(c.u()[(size_t)k * nu + lane], false);
@@ -549,8 +549,14 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     for (int k = 0; k <= N; ++k) {
       real* stk = c.st(k);
       const real* w = wb + (size_t)k * warm_w;
-      if (lane < kMaxDim)
-        for (int j = 0; j < 8; ++j) stk[kStLam + j * 12 + lane] = w[j * 12 + lane];
+      if (lane < kMaxDim) {
+        for (int j = 4; j < 8; ++j) stk[kStLam + j * 12 + lane] = w[j * 12 + lane];
+        if (k < N) {
+          for (int j = 0; j < 4; ++j) stk[kStLam + j * 12 + lane] = w[j * 12 + lane];
+        } else {
+          store_bar(stk, 0, lane, Bar{real(0.0), real(0.0), real(1.0), real(1.0)});
+        }
+      }
       const real ui = (k < N && uel) ? c.u()[(size_t)k * nu + li] : real(0.0);
       real xi;
       if (k == 0) {
@@ -1204,7 +1210,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       if (isnan_) {
         status = 3;
       } else if (res_stat <= a.tol_stat && res_eq <= a.tol_eq && res_ineq <= a.tol_ineq &&
-                 res_comp <= a.tol_comp) {
+                 res_comp <= a.tol_comp && (iter > 0 || a.warm_start != 2)) {
+        // (a continued iterate -- warm_start 2, an fp32 pass's -- takes one fp64 step first)
         status = 0;
       } else if (iter >= a.iter_max) {
         status = 1;

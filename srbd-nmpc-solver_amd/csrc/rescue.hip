@@ -1,4 +1,6 @@
-// rescue.hip -- the data movement of srbd_qp_settings.f64_rescue: after an fp32
+// rescue.hip -- the data movement of the mixed-precision paths.
+//
+// srbd_qp_settings.f64_rescue: after an fp32
 // solve, the QPs it left unsolved (status != Success) are listed in batch order,
 // their fp32 data widened into a compact fp64 batch, solved by the fp64 kernels,
 // and the fp64 solutions narrowed back into the caller's fp32 outputs.
@@ -8,6 +10,9 @@
 // fp32 factorization of R + D'Gamma D breaks down on the friction-cone QPs whose
 // active rows reach Gamma ~ 1e8-1e10.  All of it is
 // HBM-bound copy work over a few percent of the batch.
+//
+// srbd_qp_settings.f32_iters (fp64 solves): the fp64 data narrowed once to fp32 for
+// the first IPM iterations, the fp32 iterate widened back for the fp64 ones.
 #include "kernels.h"
 
 #include <hip/hip_runtime.h>
@@ -76,6 +81,16 @@ __global__ void scatter_int_kernel(const int* __restrict__ src, int* __restrict_
   if (t < rows) dst[idx[t]] = src[t];
 }
 
+__global__ void narrow_kernel(const double* __restrict__ src, float* __restrict__ dst, size_t n) {
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (size_t)gridDim.x * blockDim.x)
+    dst[t] = (float)src[t];
+}
+
+__global__ void widen_kernel(const float* __restrict__ src, double* __restrict__ dst, size_t n) {
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (size_t)gridDim.x * blockDim.x)
+    dst[t] = (double)src[t];
+}
+
 dim3 copy_grid(size_t total) {
   const size_t blocks = (total + 255) / 256;
   return dim3((unsigned)(blocks < 8192 ? (blocks ? blocks : 1) : 8192));
@@ -101,6 +116,18 @@ hipError_t launch_scatter_narrow(const double* src, float* dst, const int* idx, 
   if (!rows || !elems) return hipSuccess;
   hipLaunchKernelGGL(scatter_narrow_kernel, copy_grid((size_t)rows * elems), dim3(256), 0, s, src, dst,
                      idx, rows, elems);
+  return hipGetLastError();
+}
+
+hipError_t launch_narrow(const double* src, float* dst, size_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(narrow_kernel, copy_grid(n), dim3(256), 0, s, src, dst, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_widen(const float* src, double* dst, size_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(widen_kernel, copy_grid(n), dim3(256), 0, s, src, dst, n);
   return hipGetLastError();
 }
 

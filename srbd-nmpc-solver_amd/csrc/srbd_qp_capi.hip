@@ -55,6 +55,9 @@ struct srbd_qp_handle_s {
   int* resc_count_host = nullptr;  // pinned
   void* resc = nullptr;
   size_t resc_bytes = 0;
+  // settings.f32_iters: fp32 copy of the data, fp32 iterate, barrier state (first use)
+  void* mixed = nullptr;
+  size_t mixed_bytes = 0;
 };
 
 extern "C" {
@@ -104,6 +107,7 @@ void srbd_qp_default_settings(srbd_qp_settings* s) {
   s->split_step = 0;
   s->compute_residuals = 1;  // HPIPM's comp_res_exit
   s->f64_rescue = 0;
+  s->f32_iters = 0;
 }
 
 int srbd_qp_check_settings(const srbd_qp_settings* s) {
@@ -190,6 +194,7 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   if (h->nmpc_active_host) hipHostFree(h->nmpc_active_host);
   if (h->resc_idx) hipFree(h->resc_idx);
   if (h->resc) hipFree(h->resc);
+  if (h->mixed) hipFree(h->mixed);
   if (h->resc_count_host) hipHostFree(h->resc_count_host);
   if (h->stream) hipStreamDestroy(h->stream);
   hipSetDevice(prev);
@@ -234,6 +239,8 @@ static int validate_call(srbd_qp_handle h, int batch, const srbd_qp_settings* st
 static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                              const srbd_qp_data_f32* d, const srbd_qp_solution_f32* s,
                              const int* status, hipStream_t strm, int* rc);
+static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                     const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s, hipStream_t strm);
 
 // warm_bars: warm_start 2 only (the fp64 continuation of rescue_f32), see ProblemArgsT
 template <typename T, typename DataT, typename SolT>
@@ -243,6 +250,11 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   if (rc) return rc;
   if (batch == 0) return SRBD_QP_OK;
   hipStream_t strm = stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;
+  if constexpr (std::is_same_v<T, double>) {
+    if (st->f32_iters > 0 && st->iter_max > 0 && constrained(h->dims) && h->dims.nx == 12 &&
+        h->dims.nu == 12)
+      return mixed_f64(h, batch, st, d, s, strm);
+  }
   int prev = 0;
   hipGetDevice(&prev);
   hipSetDevice(h->device);
@@ -394,6 +406,7 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
   const size_t need = sizeof(double) * per_qp * (size_t)R + 2 * sizeof(int) * (size_t)R + 256;
   if (need > h->resc_bytes) {
     if (h->resc) hipFree(h->resc);
+  if (h->mixed) hipFree(h->mixed);
     h->resc = nullptr;
     h->resc_bytes = 0;
     e = hipMalloc(&h->resc, need);
@@ -444,6 +457,89 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
   if (e == hipSuccess && s->iter) e = srbd::launch_scatter_int(s64.iter, s->iter, idx, R, strm);
   hipSetDevice(prev);
   return e;
+}
+
+// ---------------------------------------------------------------------------
+// settings.f32_iters: mixed-precision IPM (fp32 iterations, then fp64 to the end)
+// ---------------------------------------------------------------------------
+static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                     const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s, hipStream_t strm) {
+  const srbd_qp_dims& m = h->dims;
+  const size_t B = (size_t)batch, N = (size_t)m.N, nx = (size_t)m.nx, nu = (size_t)m.nu,
+               ng = (size_t)m.ng;
+  srbd_qp_data_f32 d32{};
+  struct F { const double* src; size_t e; const float** dst; };
+  const F ins[] = {
+      {d->A, N * nx * nx, &d32.A}, {d->B, N * nx * nu, &d32.B}, {d->b, N * nx, &d32.b},
+      {d->Q, (N + 1) * nx * nx, &d32.Q}, {d->S, N * nu * nx, &d32.S}, {d->R, N * nu * nu, &d32.R},
+      {d->q, (N + 1) * nx, &d32.q}, {d->r, N * nu, &d32.r}, {d->x0, nx, &d32.x0},
+      {d->lbu, N * nu, &d32.lbu}, {d->ubu, N * nu, &d32.ubu}, {d->lbu_mask, N * nu, &d32.lbu_mask},
+      {d->ubu_mask, N * nu, &d32.ubu_mask}, {d->lbx, (N + 1) * nx, &d32.lbx},
+      {d->ubx, (N + 1) * nx, &d32.ubx}, {d->lbx_mask, (N + 1) * nx, &d32.lbx_mask},
+      {d->ubx_mask, (N + 1) * nx, &d32.ubx_mask}, {d->C, (N + 1) * ng * nx, &d32.C},
+      {d->D, N * ng * nu, &d32.D}, {d->lg, (N + 1) * ng, &d32.lg}, {d->ug, (N + 1) * ng, &d32.ug},
+      {d->lg_mask, (N + 1) * ng, &d32.lg_mask}, {d->ug_mask, (N + 1) * ng, &d32.ug_mask}};
+  const size_t ex = (N + 1) * nx, eu = N * nu;
+  const size_t warm_e = (N + 1) * (96 + (size_t)((m.ng + 11) / 12) * 48);
+  size_t floats = 2 * ex + eu;  // per QP: x, u, pi
+  for (const F& f : ins) floats += f.src ? f.e : 0;
+  const size_t need = B * (floats * sizeof(float) + warm_e * sizeof(double)) + 512;
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipSetDevice(h->device);
+  hipError_t e = hipSuccess;
+  if (need > h->mixed_bytes) {
+    if (h->mixed) hipFree(h->mixed);
+    h->mixed = nullptr;
+    h->mixed_bytes = 0;
+    e = hipMalloc(&h->mixed, need);
+    if (e != hipSuccess) {
+      hipSetDevice(prev);
+      return fail(SRBD_QP_ENOMEM, std::string("mixed-precision buffers: ") + hipGetErrorString(e));
+    }
+    h->mixed_bytes = need;
+  }
+  double* warm = reinterpret_cast<double*>(h->mixed);
+  float* cur = reinterpret_cast<float*>(warm + B * warm_e);
+  for (const F& f : ins) {
+    if (!f.src || e != hipSuccess) continue;
+    e = srbd::launch_narrow(f.src, cur, f.e * B, strm);
+    *f.dst = cur;
+    cur += f.e * B;
+  }
+  srbd_qp_solution_f32 s32{};
+  s32.x = cur;
+  s32.u = cur + ex * B;
+  s32.pi = cur + (ex + eu) * B;
+  if (e == hipSuccess && st->warm_start) {
+    e = srbd::launch_narrow(s->x, s32.x, ex * B, strm);
+    if (e == hipSuccess) e = srbd::launch_narrow(s->u, s32.u, eu * B, strm);
+  }
+  hipSetDevice(prev);
+  if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("mixed precision: ") + hipGetErrorString(e));
+  // fp32 iterations: tolerances out of reach, so every QP runs them all (a QP that stops
+  // early on NaN / min step continues cold in fp64: its iterate fails the finiteness test
+  // or is simply where it stopped)
+  srbd_qp_settings st32 = *st;
+  st32.iter_max = st->f32_iters < st->iter_max ? st->f32_iters : st->iter_max;
+  st32.tol_stat = st32.tol_eq = st32.tol_ineq = st32.tol_comp = 1e-30;
+  st32.f64_rescue = 0;
+  st32.f32_iters = 0;
+  int rc = solve_impl<float>(h, batch, &st32, &d32, &s32, strm);
+  if (rc) return rc;
+  hipSetDevice(h->device);
+  e = srbd::launch_widen(s32.x, s->x, ex * B, strm);
+  if (e == hipSuccess) e = srbd::launch_widen(s32.u, s->u, eu * B, strm);
+  if (e == hipSuccess) e = srbd::launch_widen(s32.pi, s->pi, ex * B, strm);
+  if (e == hipSuccess)
+    e = srbd::launch_gather_warm_bars(reinterpret_cast<const float*>(h->ws), h->ws_qp, m.N, m.ng, nullptr,
+                                      batch, warm, strm);
+  hipSetDevice(prev);
+  if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("mixed precision: ") + hipGetErrorString(e));
+  srbd_qp_settings st64 = *st;
+  st64.warm_start = 2;
+  st64.f32_iters = 0;
+  return solve_impl<double>(h, batch, &st64, d, s, strm, warm);
 }
 
 // ---------------------------------------------------------------------------

@@ -1,0 +1,85 @@
+"""settings.f32_iters: the mixed-precision IPM for fp64 solves.  The first n IPM
+iterations run in fp32 on a narrowed copy of the data (half the bytes per sweep);
+the fp64 IPM then continues from that iterate (x, u, pi and every lam / t: HPIPM's
+warm_start = 2 level) on the caller's fp64 data to the fp64 tolerances.  The bar is
+the fp64 path's own: the oracle at the tolerances of test_gpu_ipm.py (1e-7 on x / u
+at tol 1e-8), and the fp64 solution at the NMPC settings."""
+import numpy as np
+import pytest
+
+import helpers
+
+pytestmark = pytest.mark.gpu
+
+NMPC = dict(iter_max=30, tol_stat=1e-4, tol_eq=1e-4, tol_ineq=1e-4, tol_comp=1e-4, split_step=1)
+
+
+def test_mixed_box_u_nmpc_settings(pkg):
+    """Config 3's problem at the reference caller's settings (NMPC_solver.cpp:70-82):
+    the continuation picks up where fp32 stopped (fp64 iterations = the fp64 solve's
+    minus n) and lands on the fp64 solution well inside the tolerance."""
+    qp, x0 = pkg.srbd_model.generate_batch(256, N=20, seed=5, constraints="box_u")
+    o64 = pkg.capi.solve(qp, x0, NMPC, stats=True)
+    mix = pkg.capi.solve(qp, x0, dict(NMPC, f32_iters=6), stats=True, riccati=True)
+    assert np.all(o64["status"] == 0) and np.all(mix["status"] == 0)
+    assert np.all(mix["res"] <= 1e-4)
+    assert np.all(mix["iter"] <= o64["iter"] - 6 + 1), (mix["iter"], o64["iter"])
+    for key in ("x", "u"):
+        d = np.abs(mix[key] - o64[key]).reshape(qp.batch, -1).max(1)
+        scale = np.abs(o64[key]).reshape(qp.batch, -1).max(1)
+        assert np.all(d <= 1e-5 * scale), (key, (d / scale).max())
+    # the stat table is the fp64 continuation's: row 0 is the fp32 iterate's residuals
+    # in fp64, mu no longer mu0
+    assert np.all(mix["stat"][:, 0, 5] < 1.0)
+
+
+@pytest.mark.parametrize("case", ["box_u", "cone", "general_with_c"])
+def test_mixed_vs_oracle_tight(pkg, oracle, case):
+    """tol 1e-8 (hpipm-cpp's defaults): the fp64 continuation reaches the oracle's
+    solution like the fp64 path does -- fp32 only supplies the starting point."""
+    if case == "general_with_c":
+        qp, x0 = helpers.random_constrained(20, 12, 12, 12, 14, 211, pkg.OcpQpBatch)
+        st = dict(iter_max=50, mode="Balance")
+    else:
+        qp, x0 = pkg.srbd_model.generate_batch(24, N=20, seed=12, constraints=case)
+        st = dict(iter_max=40)
+    ref = oracle.solve(qp, st, x0=x0)
+    out = pkg.capi.solve(qp, x0, dict(st, f32_iters=5))
+    plain = pkg.capi.solve(qp, x0, st)
+    assert np.all(ref["status"] == 0), ref["status"]
+    ok = plain["status"] == 0
+    assert np.all(out["status"][ok] == 0), (out["status"], out["res"])
+    for i in np.nonzero(ok)[0]:
+        for key in ("x", "u"):
+            assert helpers.is_approx(out[key][i], ref[key][i], 1e-7), (key, i)
+        assert helpers.is_approx(out["pi"][i, 1:], ref["pi"][i, 1:], 1e-6), ("pi", i)
+
+
+def test_mixed_ignored_when_padded_or_unconstrained(pkg):
+    """nx or nu < 12 (the 12 x 12 embedding) and nc = 0: f32_iters changes no bit."""
+    qp, x0 = helpers.random_constrained(16, 8, 5, 3, 4, 7, pkg.OcpQpBatch)
+    a = pkg.capi.solve(qp, x0, dict(iter_max=40))
+    b = pkg.capi.solve(qp, x0, dict(iter_max=40, f32_iters=5))
+    for key in a:
+        assert np.array_equal(a[key], b[key]), key
+    qp, x0 = pkg.srbd_model.generate_batch(16, N=10, seed=3, constraints="none")
+    a = pkg.capi.solve(qp, x0)
+    b = pkg.capi.solve(qp, x0, dict(f32_iters=5))
+    for key in a:
+        assert np.array_equal(a[key], b[key]), key
+
+
+def test_mixed_iter_max_bounds_the_fp32_pass(pkg):
+    """f32_iters >= iter_max: the fp32 pass runs iter_max iterations and the fp64
+    continuation still has its own iter_max; warm-started calls narrow the caller's
+    x / u for the fp32 pass."""
+    qp, x0 = pkg.srbd_model.generate_batch(32, N=20, seed=9, constraints="box_u")
+    o64 = pkg.capi.solve(qp, x0, NMPC)
+    mix = pkg.capi.solve(qp, x0, dict(NMPC, iter_max=8, f32_iters=50))
+    assert np.all(mix["status"] == 0), mix["status"]
+    warm = pkg.capi.solve(qp, x0, dict(NMPC, warm_start=1, f32_iters=4),
+                          x_init=o64["x"], u_init=o64["u"])
+    assert np.all(warm["status"] == 0), warm["status"]
+    assert np.all(warm["res"] <= 1e-4)
+    # (a different tol-1e-4 KKT point than the cold solve's: the warm start re-centres
+    # lam = mu0 / t, and the SRBD R has 1e-4 curvature directions, so no closeness bound)
