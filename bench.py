@@ -152,6 +152,9 @@ def main():
     ap.add_argument("--f64-rescue", type=int, default=0,
                     help="fp32 workloads: settings.f64_rescue = n (the fp32 pass runs at most n "
                          "iterations, the QPs it leaves unsolved are solved again in fp64)")
+    ap.add_argument("--f32-iters", type=int, default=0,
+                    help="fp64 IPM workloads: settings.f32_iters = n (mixed precision: the first n "
+                         "IPM iterations in fp32, then fp64 to the fp64 tolerances)")
     args = ap.parse_args()
 
     import torch
@@ -197,6 +200,7 @@ def main():
     # solver settings of the reference caller (NMPC_solver.cpp:70-82)
     settings = capi.settings_struct(F32_SETTINGS if dtype == "f32" else NMPC_SETTINGS)
     settings.f64_rescue = int(args.f64_rescue)
+    settings.f32_iters = int(args.f32_iters)
     stream_ptr = h.stream()
     ext = torch.cuda.ExternalStream(stream_ptr, device=device)
 
@@ -295,7 +299,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": dtype,
+        "dtype": dtype + (f" (first {args.f32_iters} IPM iterations f32)"
+                          if args.f32_iters and dtype == "f64" and constraints != "none" else "")
+                 + (f" + f64 rescue after {args.f64_rescue} it" if args.f64_rescue and dtype == "f32" else ""),
         "data": f"synthetic SRBD linearisations (seed {args.seed} + global QP index; every QP of "
                 f"the batch distinct, linearised on the device), generated per rank",
         "config": {"workload": args.workload, "description": desc, "batch_per_gpu": batch,
