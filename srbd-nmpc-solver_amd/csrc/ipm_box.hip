@@ -66,7 +66,83 @@ __global__ void gather_warm_bars_kernel(const float* __restrict__ ws32, size_t w
     dst[t] = (double)ws32[q * ws_qp + ipm_f32::kQsSize + k * stride + off];
   }
 }
+// f32_iters: one thread per (QP, stage, value); exp = ((c + 2) & 3) * 12 maps a bar component
+// (ll, lu, tl, tu) to its step (dll at 24, dlu at 36, dtl at 0, dtu at 12)
+__global__ void gather_warm_apply_kernel(const float* __restrict__ ws32, size_t ws_qp, int N,
+                                         size_t stride, int nch, int batch, double* __restrict__ dst) {
+  const size_t W = 96 + (size_t)nch * 48, per_qp = (size_t)(N + 1) * W;
+  const size_t total = (size_t)batch * per_qp;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const size_t q = t / per_qp, rem = t - q * per_qp, k = rem / W, j = rem - k * W;
+    const float* qs = ws32 + q * ws_qp;
+    const float* st = qs + ipm_f32::kQsSize + k * stride;
+    const bool pending = qs[ipm_f32::kQsStatus] < 0.0f;
+    const size_t f = j < 96 ? j / 48 : 0, c = ((j < 96 ? j : j - 96) % 48) / 12, i = j % 12;
+    const float* bar = j < 96 ? st + kStLam + j
+                              : st + kIpmStage + ((j - 96) / 48) * kGenChunk + (j - 96) % 48;
+    const float* stp = j < 96 ? st + kStDlt + f * 48 + ((c + 2) & 3) * 12 + i
+                              : st + kIpmStage + ((j - 96) / 48) * kGenChunk + 48 + ((c + 2) & 3) * 12 + i;
+    const float a = pending ? qs[c < 2 ? ipm_f32::kQsAlphaD : ipm_f32::kQsAlphaP] : 0.0f;
+    double v = (double)*bar;
+    if (a != 0.0f) v += (double)a * (double)*stp;
+    dst[t] = v;
+  }
+}
+
+__global__ void gather_warm_iterate_kernel(const float* __restrict__ ws32, size_t ws_qp, int N,
+                                           size_t stride, int batch, const float* __restrict__ x32,
+                                           const float* __restrict__ u32, const float* __restrict__ pi32,
+                                           double* __restrict__ x, double* __restrict__ u,
+                                           double* __restrict__ pi) {
+  const size_t ex = (size_t)(N + 1) * 12, eu = (size_t)N * 12, per_qp = 2 * ex + eu;
+  const size_t total = (size_t)batch * per_qp;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const size_t q = t / per_qp, rem = t - q * per_qp;
+    const float* qs = ws32 + q * ws_qp;
+    const bool pending = qs[ipm_f32::kQsStatus] < 0.0f;
+    const float ap = pending ? qs[ipm_f32::kQsAlphaP] : 0.0f, ad = pending ? qs[ipm_f32::kQsAlphaD] : 0.0f;
+    if (rem < ex) {  // x (x_0 is never stepped)
+      const size_t k = rem / 12, i = rem % 12;
+      double v = (double)x32[q * ex + rem];
+      if (k > 0 && ap != 0.0f)
+        v += (double)ap * (double)qs[ipm_f32::kQsSize + k * stride + kStStep + 12 + i];
+      x[q * ex + rem] = v;
+    } else if (rem < ex + eu) {
+      const size_t e = rem - ex, k = e / 12, i = e % 12;
+      double v = (double)u32[q * eu + e];
+      if (ap != 0.0f) v += (double)ap * (double)qs[ipm_f32::kQsSize + k * stride + kStStep + i];
+      u[q * eu + e] = v;
+    } else {
+      const size_t e = rem - ex - eu, k = e / 12, i = e % 12;
+      double v = (double)pi32[q * ex + e];
+      if (k > 0 && ad != 0.0f)
+        v += (double)ad * (double)qs[ipm_f32::kQsSize + k * stride + kStStep + 24 + i];
+      pi[q * ex + e] = v;
+    }
+  }
+}
 }  // namespace
+
+hipError_t launch_gather_warm_apply(const float* ws32, size_t ws_qp, int N, int ng, int batch,
+                                    const float* x32, const float* u32, const float* pi32, double* x,
+                                    double* u, double* pi, double* bars, hipStream_t s) {
+  if (batch <= 0) return hipSuccess;
+  const int nch = (ng + kMaxDim - 1) / kMaxDim;
+  const size_t stride = (size_t)kIpmStage + (size_t)nch * kGenChunk + (nch ? kGenVec : 0);
+  auto grid = [](size_t total) {
+    const size_t blocks = (total + 255) / 256;
+    return dim3((unsigned)(blocks < 8192 ? blocks : 8192));
+  };
+  const size_t tb = (size_t)batch * (N + 1) * (96 + (size_t)nch * 48);
+  hipLaunchKernelGGL(gather_warm_apply_kernel, grid(tb), dim3(256), 0, s, ws32, ws_qp, N, stride, nch,
+                     batch, bars);
+  const size_t ti = (size_t)batch * ((size_t)(N + 1) * 24 + (size_t)N * 12);
+  hipLaunchKernelGGL(gather_warm_iterate_kernel, grid(ti), dim3(256), 0, s, ws32, ws_qp, N, stride, batch,
+                     x32, u32, pi32, x, u, pi);
+  return hipGetLastError();
+}
 
 hipError_t launch_gather_warm_bars(const float* ws32, size_t ws_qp, int N, int ng, const int* idx,
                                    int rows, double* dst, hipStream_t s) {

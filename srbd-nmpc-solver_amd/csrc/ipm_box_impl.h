@@ -1568,7 +1568,8 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
 #elif SRBD_IPM_FUSE
   for (int it = 0;; ++it) {
     if (it >= a.iter_max) {
-      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB>), grid, block, 0, stream, a);
+      if (!a.skip_last_rb)
+        hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB>), grid, block, 0, stream, a);
       break;
     }
     hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1>), grid, block, 0, stream, a);

@@ -46,6 +46,9 @@ struct ProblemArgsT {
   // warm_start 2 only (internal: the fp64 continuation of srbd_qp_settings.f64_rescue):
   // per QP and stage the barrier state [kStLam block 96][nch chunks x 48], see ipm_box.hip
   const T* warm_bars;
+  // internal (srbd_qp_settings.f32_iters): end the IPM launch loop after the last corrector
+  // step without the sweep that would apply it; the step is handed to the fp64 continuation
+  int skip_last_rb;
   T alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp;
 };
 using ProblemArgs = ProblemArgsT<double>;
@@ -131,6 +134,12 @@ hipError_t launch_narrow(const double* src, float* dst, size_t n, hipStream_t s)
 hipError_t launch_widen(const float* src, double* dst, size_t n, hipStream_t s);
 // ipm_box.hip: the barrier state of the fp32 IPM workspace rows idx[0..rows) (idx NULL: rows
 // 0..rows), widened into the warm_bars layout of ProblemArgsT (rows x (N+1) x (96 + nch*48))
+// ipm_box.hip (f32_iters): the fp32 pass's whole iterate, widened, with the step it computed
+// last applied (QPs still running, fp32 status < 0): x, u, pi into the fp64 outputs, the barrier
+// state into the warm_bars layout
+hipError_t launch_gather_warm_apply(const float* ws32, size_t ws_qp, int N, int ng, int batch,
+                                    const float* x32, const float* u32, const float* pi32, double* x,
+                                    double* u, double* pi, double* bars, hipStream_t s);
 hipError_t launch_gather_warm_bars(const float* ws32, size_t ws_qp, int N, int ng, const int* idx,
                                    int rows, double* dst, hipStream_t s);
 

@@ -245,7 +245,8 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
 // warm_bars: warm_start 2 only (the fp64 continuation of rescue_f32), see ProblemArgsT
 template <typename T, typename DataT, typename SolT>
 static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, const DataT* d,
-                      const SolT* s, void* stream, const T* warm_bars = nullptr) {
+                      const SolT* s, void* stream, const T* warm_bars = nullptr,
+                      int skip_last_rb = 0) {
   int rc = validate_call(h, batch, st, d, s);
   if (rc) return rc;
   if (batch == 0) return SRBD_QP_OK;
@@ -293,6 +294,7 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   a.iter_max = st->iter_max;
   a.stat_rows = st->iter_max + 2;
   a.warm_bars = warm_bars;
+  a.skip_last_rb = skip_last_rb;
   // f64_rescue = n: the fp32 pass stops after n iterations at most, the rest is fp64's
   if (rescue && st->f64_rescue < a.iter_max) a.iter_max = st->f64_rescue;
   a.pred_corr = st->pred_corr;
@@ -525,15 +527,12 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   st32.tol_stat = st32.tol_eq = st32.tol_ineq = st32.tol_comp = 1e-30;
   st32.f64_rescue = 0;
   st32.f32_iters = 0;
-  int rc = solve_impl<float>(h, batch, &st32, &d32, &s32, strm);
+  // (the loop ends after the last corrector step; its application rides on the widening)
+  int rc = solve_impl<float>(h, batch, &st32, &d32, &s32, strm, nullptr, 1);
   if (rc) return rc;
   hipSetDevice(h->device);
-  e = srbd::launch_widen(s32.x, s->x, ex * B, strm);
-  if (e == hipSuccess) e = srbd::launch_widen(s32.u, s->u, eu * B, strm);
-  if (e == hipSuccess) e = srbd::launch_widen(s32.pi, s->pi, ex * B, strm);
-  if (e == hipSuccess)
-    e = srbd::launch_gather_warm_bars(reinterpret_cast<const float*>(h->ws), h->ws_qp, m.N, m.ng, nullptr,
-                                      batch, warm, strm);
+  e = srbd::launch_gather_warm_apply(reinterpret_cast<const float*>(h->ws), h->ws_qp, m.N, m.ng, batch,
+                                     s32.x, s32.u, s32.pi, s->x, s->u, s->pi, warm, strm);
   hipSetDevice(prev);
   if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("mixed precision: ") + hipGetErrorString(e));
   srbd_qp_settings st64 = *st;
