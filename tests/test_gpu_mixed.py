@@ -83,3 +83,23 @@ def test_mixed_iter_max_bounds_the_fp32_pass(pkg):
     assert np.all(warm["res"] <= 1e-4)
     # (a different tol-1e-4 KKT point than the cold solve's: the warm start re-centres
     # lam = mu0 / t, and the SRBD R has 1e-4 curvature directions, so no closeness bound)
+
+
+def test_mixed_host_entry_point_matches_device(pkg):
+    """srbd_qp_solve_host_f64 runs the same mixed path: bit-identical to the device call."""
+    capi = pkg.capi
+    qp, x0 = pkg.srbd_model.generate_batch(64, N=20, seed=17, constraints="box_u")
+    st = dict(NMPC, f32_iters=6)
+    dev = capi.solve(qp, x0, st)
+    p = {k: (None if v is None else np.ascontiguousarray(v)) for k, v in qp.packed().items()}
+    p["x0"] = np.ascontiguousarray(x0)
+    out = {k: np.zeros_like(dev[k]) for k in ("x", "u", "pi", "status", "iter")}
+    data = capi.Data(**{k: (None if p.get(k) is None else p[k].ctypes.data) for k in capi.DATA_FIELDS})
+    sol = capi.Solution(**{k: v.ctypes.data for k, v in out.items()})
+    h = capi.Handle(qp.N, qp.nx, qp.nu, 0, True, False, capacity=qp.batch)
+    try:
+        h.solve_host(qp.batch, capi.settings_struct(st), data, sol)
+    finally:
+        h.close()
+    for key in out:
+        assert np.array_equal(out[key], dev[key]), key
