@@ -90,16 +90,18 @@ def _rounded_to_f32(qp):
     return type(qp)(**kw)
 
 
-@pytest.mark.parametrize("cap,stats", [(30, False), (30, True), (12, False)])
-def test_f64_rescue_cone_n40(pkg, cap, stats):
+@pytest.mark.parametrize("cap,stats,batch", [(30, False, 512), (30, True, 512), (12, False, 512),
+                                             (12, False, 2500)])
+def test_f64_rescue_cone_n40(pkg, cap, stats, batch):
     """settings.f64_rescue = cap: the fp32 pass runs at most `cap` iterations, and the
     QPs it leaves unsolved continue in fp64 from the iterate it ended on (x, u, pi and
     the barrier state: HPIPM's warm_start = 2).  Every QP ends with status Success
     within the tolerances; the QPs fp32 solved keep their fp32 outputs bit for bit (an
     fp32 solve with iter_max = cap); the rescued ones land at the fp64 KKT point to the
     accuracy the stationarity tolerance allows (the bound of test_friction_cone_n40_fp32)
-    in a few fp64 iterations."""
-    qp, x0 = pkg.srbd_model.generate_batch(512, N=40, seed=1005, constraints="cone")
+    in a few fp64 iterations.  batch 2500: the unsolved-QP list spans three ragged
+    1024-QP tiles of the selection kernel."""
+    qp, x0 = pkg.srbd_model.generate_batch(batch, N=40, seed=1005, constraints="cone")
     st = dict(F32, tol_stat=3e-2)
     plain = pkg.capi.solve(qp, x0, dict(st, iter_max=cap), dtype=np.float32, riccati=True,
                            stats=stats)
