@@ -50,12 +50,16 @@ WORKLOADS = {
     "cone_n40_f32": (40, "cone", 65536,
                      "BASELINE config 5: batch 65536, N=40, friction-cone rows (ng=24), fp32 IPM",
                      "f32"),
+    "cone_n40_f64": (40, "cone", 65536,
+                     "config 5's problem solved in fp64 (batch 65536, N=40, friction-cone rows)"),
 }
 DEFAULT_WORKLOAD = "unconstr_n20"
 # settings.f64_rescue of the cone_n40_f32_f64_rescue line (fp32 iterations before the fp64 re-solve)
 RESCUE_CAP = 12
 # settings.f32_iters of the box_u_n20_mixed line (fp32 iterations before fp64 takes over)
 MIXED_F32_ITERS = 6
+# ... and of the cone_n40_f64_mixed line (config 5's problem solved to fp64 tolerances)
+MIXED_F32_ITERS_CONE = 9
 
 
 def log(*a):
@@ -282,6 +286,8 @@ def main():
                      for w in ("box_u_n20", "cone_n40_f32")}
         secondary["box_u_n20_mixed"] = secondary_workload(pkg, capi, "box_u_n20", device, args.seed,
                                                           f32_iters=MIXED_F32_ITERS)
+        secondary["cone_n40_f64_mixed"] = secondary_workload(pkg, capi, "cone_n40_f64", device, args.seed,
+                                                             f32_iters=MIXED_F32_ITERS_CONE)
         secondary["cone_n40_f32_f64_rescue"] = secondary_workload(pkg, capi, "cone_n40_f32", device,
                                                                   args.seed, rescue=RESCUE_CAP)
         secondary["nmpc_step_config1"] = nmpc_config1(pkg, capi, device, args.seed,

@@ -158,7 +158,10 @@ typedef struct srbd_qp_settings {
                      * in fp32 (half the bytes per sweep), and the fp64 IPM
                      * continues from that iterate (x, u, pi, lam, t) on the
                      * caller's fp64 data to the fp64 tolerances; iter and stat
-                     * count the fp64 iterations.                           */
+                     * count the fp64 iterations.  A QP the continuation leaves
+                     * unsolved is solved again cold in fp64 (its outputs are
+                     * then the fp64 path's); the call waits once to count
+                     * them.                                                */
 } srbd_qp_settings;
 
 typedef struct srbd_qp_data_f64 {

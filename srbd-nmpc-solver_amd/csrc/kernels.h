@@ -130,6 +130,10 @@ hipError_t launch_gather_widen(const float* src, double* dst, const int* idx, in
 hipError_t launch_scatter_narrow(const double* src, float* dst, const int* idx, int rows, size_t elems,
                                  hipStream_t s);
 hipError_t launch_scatter_int(const int* src, int* dst, const int* idx, int rows, hipStream_t s);
+hipError_t launch_gather_rows(const double* src, double* dst, const int* idx, int rows, size_t elems,
+                              hipStream_t s);
+hipError_t launch_scatter_rows(const double* src, double* dst, const int* idx, int rows, size_t elems,
+                               hipStream_t s);
 hipError_t launch_narrow(const double* src, float* dst, size_t n, hipStream_t s);
 hipError_t launch_widen(const float* src, double* dst, size_t n, hipStream_t s);
 // ipm_box.hip: the barrier state of the fp32 IPM workspace rows idx[0..rows) (idx NULL: rows

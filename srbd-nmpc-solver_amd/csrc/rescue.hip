@@ -81,6 +81,26 @@ __global__ void scatter_int_kernel(const int* __restrict__ src, int* __restrict_
   if (t < rows) dst[idx[t]] = src[t];
 }
 
+__global__ void gather_rows_kernel(const double* __restrict__ src, double* __restrict__ dst,
+                                   const int* __restrict__ idx, int rows, size_t elems) {
+  const size_t total = (size_t)rows * elems;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = t / elems, j = t - r * elems;
+    dst[t] = src[(size_t)idx[r] * elems + j];
+  }
+}
+
+__global__ void scatter_rows_kernel(const double* __restrict__ src, double* __restrict__ dst,
+                                    const int* __restrict__ idx, int rows, size_t elems) {
+  const size_t total = (size_t)rows * elems;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = t / elems, j = t - r * elems;
+    dst[(size_t)idx[r] * elems + j] = src[t];
+  }
+}
+
 __global__ void narrow_kernel(const double* __restrict__ src, float* __restrict__ dst, size_t n) {
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (size_t)gridDim.x * blockDim.x)
     dst[t] = (float)src[t];
@@ -116,6 +136,22 @@ hipError_t launch_scatter_narrow(const double* src, float* dst, const int* idx, 
   if (!rows || !elems) return hipSuccess;
   hipLaunchKernelGGL(scatter_narrow_kernel, copy_grid((size_t)rows * elems), dim3(256), 0, s, src, dst,
                      idx, rows, elems);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const double* src, double* dst, const int* idx, int rows, size_t elems,
+                              hipStream_t s) {
+  if (!rows || !elems) return hipSuccess;
+  hipLaunchKernelGGL(gather_rows_kernel, copy_grid((size_t)rows * elems), dim3(256), 0, s, src, dst, idx,
+                     rows, elems);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_rows(const double* src, double* dst, const int* idx, int rows, size_t elems,
+                               hipStream_t s) {
+  if (!rows || !elems) return hipSuccess;
+  hipLaunchKernelGGL(scatter_rows_kernel, copy_grid((size_t)rows * elems), dim3(256), 0, s, src, dst, idx,
+                     rows, elems);
   return hipGetLastError();
 }
 

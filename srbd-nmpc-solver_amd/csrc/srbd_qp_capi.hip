@@ -464,6 +464,91 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
 // ---------------------------------------------------------------------------
 // settings.f32_iters: mixed-precision IPM (fp32 iterations, then fp64 to the end)
 // ---------------------------------------------------------------------------
+// f32_iters: a QP the continuation leaves unsolved (status != Success) is solved again, cold,
+// in fp64 -- the mixed path never ends a QP worse than the fp64 path would
+static int fallback_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                        const srbd_qp_data_f64* d, const srbd_qp_solution_f64* sc,
+                        const srbd_qp_solution_f64* s, hipStream_t strm) {
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipSetDevice(h->device);
+  int* idx = h->resc_idx;
+  int* count = h->resc_idx + 2 * (size_t)h->capacity;
+  hipError_t e = srbd::launch_select_unsolved(sc->status, batch, idx, count, strm);
+  if (e == hipSuccess) e = hipMemcpyAsync(h->resc_count_host, count, sizeof(int), hipMemcpyDeviceToHost, strm);
+  if (e == hipSuccess) e = hipStreamSynchronize(strm);
+  const int R = e == hipSuccess ? *h->resc_count_host : 0;
+  if (e != hipSuccess || R == 0) {
+    hipSetDevice(prev);
+    return e == hipSuccess ? SRBD_QP_OK : fail(SRBD_QP_EDEVICE, std::string("fallback: ") + hipGetErrorString(e));
+  }
+  const srbd_qp_dims& m = h->dims;
+  const size_t N = (size_t)m.N, nx = (size_t)m.nx, nu = (size_t)m.nu, ng = (size_t)m.ng;
+  struct In { const double* src; size_t e; const double** dst; };
+  struct Out { double* dst; size_t e; double** src; };
+  srbd_qp_data_f64 d2{};
+  srbd_qp_solution_f64 s2{};
+  const In ins[] = {
+      {d->A, N * nx * nx, &d2.A}, {d->B, N * nx * nu, &d2.B}, {d->b, N * nx, &d2.b},
+      {d->Q, (N + 1) * nx * nx, &d2.Q}, {d->S, N * nu * nx, &d2.S}, {d->R, N * nu * nu, &d2.R},
+      {d->q, (N + 1) * nx, &d2.q}, {d->r, N * nu, &d2.r}, {d->x0, nx, &d2.x0},
+      {d->lbu, N * nu, &d2.lbu}, {d->ubu, N * nu, &d2.ubu}, {d->lbu_mask, N * nu, &d2.lbu_mask},
+      {d->ubu_mask, N * nu, &d2.ubu_mask}, {d->lbx, (N + 1) * nx, &d2.lbx},
+      {d->ubx, (N + 1) * nx, &d2.ubx}, {d->lbx_mask, (N + 1) * nx, &d2.lbx_mask},
+      {d->ubx_mask, (N + 1) * nx, &d2.ubx_mask}, {d->C, (N + 1) * ng * nx, &d2.C},
+      {d->D, N * ng * nu, &d2.D}, {d->lg, (N + 1) * ng, &d2.lg}, {d->ug, (N + 1) * ng, &d2.ug},
+      {d->lg_mask, (N + 1) * ng, &d2.lg_mask}, {d->ug_mask, (N + 1) * ng, &d2.ug_mask}};
+  const Out outs[] = {
+      {s->x, (N + 1) * nx, &s2.x}, {s->u, N * nu, &s2.u}, {s->pi, (N + 1) * nx, &s2.pi},
+      {s->P, (N + 1) * nx * nx, &s2.P}, {s->p, (N + 1) * nx, &s2.p}, {s->K, N * nu * nx, &s2.K},
+      {s->k, N * nu, &s2.k}, {s->res, 4, &s2.res}, {s->obj, 1, &s2.obj},
+      {s->stat, srbd::kStatCols * (size_t)(st->iter_max + 2), &s2.stat}};
+  size_t per_qp = 0;
+  for (const In& f : ins) per_qp += f.src ? f.e : 0;
+  for (const Out& f : outs) per_qp += f.dst ? f.e : 0;
+  const size_t need = sizeof(double) * per_qp * (size_t)R + 2 * sizeof(int) * (size_t)R + 256;
+  if (need > h->resc_bytes) {
+    if (h->resc) hipFree(h->resc);
+    h->resc = nullptr;
+    h->resc_bytes = 0;
+    e = hipMalloc(&h->resc, need);
+    if (e != hipSuccess) {
+      hipSetDevice(prev);
+      return fail(SRBD_QP_ENOMEM, std::string("fallback batch: ") + hipGetErrorString(e));
+    }
+    h->resc_bytes = need;
+  }
+  double* cur = reinterpret_cast<double*>(h->resc);
+  for (const In& f : ins) {
+    if (!f.src || e != hipSuccess) continue;
+    e = srbd::launch_gather_rows(f.src, cur, idx, R, f.e, strm);
+    *f.dst = cur;
+    cur += f.e * (size_t)R;
+  }
+  for (const Out& f : outs) {
+    if (!f.dst) continue;
+    *f.src = cur;
+    cur += f.e * (size_t)R;
+  }
+  s2.status = reinterpret_cast<int*>(cur);
+  s2.iter = s2.status + R;
+  hipSetDevice(prev);
+  if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("fallback: ") + hipGetErrorString(e));
+  srbd_qp_settings st2 = *st;
+  st2.warm_start = 0;
+  st2.f32_iters = 0;
+  int rc = solve_impl<double>(h, R, &st2, &d2, &s2, strm);
+  if (rc) return rc;
+  hipSetDevice(h->device);
+  for (const Out& f : outs)
+    if (f.dst && e == hipSuccess) e = srbd::launch_scatter_rows(*f.src, f.dst, idx, R, f.e, strm);
+  if (e == hipSuccess) e = srbd::launch_scatter_int(s2.status, sc->status, idx, R, strm);
+  if (e == hipSuccess && s->iter) e = srbd::launch_scatter_int(s2.iter, s->iter, idx, R, strm);
+  hipSetDevice(prev);
+  if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("fallback: ") + hipGetErrorString(e));
+  return SRBD_QP_OK;
+}
+
 static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                      const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s, hipStream_t strm) {
   const srbd_qp_dims& m = h->dims;
@@ -538,7 +623,18 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   srbd_qp_settings st64 = *st;
   st64.warm_start = 2;
   st64.f32_iters = 0;
-  return solve_impl<double>(h, batch, &st64, d, s, strm, warm);
+  if (!h->resc_idx) {
+    hipSetDevice(h->device);
+    e = hipMalloc(reinterpret_cast<void**>(&h->resc_idx), sizeof(int) * (2 * (size_t)h->capacity + 1));
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&h->resc_count_host), sizeof(int));
+    hipSetDevice(prev);
+    if (e != hipSuccess) return fail(SRBD_QP_ENOMEM, std::string("fallback buffers: ") + hipGetErrorString(e));
+  }
+  srbd_qp_solution_f64 sc = *s;
+  if (!sc.status) sc.status = h->resc_idx + h->capacity;
+  rc = solve_impl<double>(h, batch, &st64, d, &sc, strm, warm);
+  if (rc) return rc;
+  return fallback_f64(h, batch, st, d, &sc, s, strm);
 }
 
 // ---------------------------------------------------------------------------

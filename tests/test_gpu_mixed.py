@@ -103,3 +103,18 @@ def test_mixed_host_entry_point_matches_device(pkg):
         h.close()
     for key in out:
         assert np.array_equal(out[key], dev[key]), key
+
+
+def test_mixed_fallback_is_the_fp64_solve(pkg):
+    """A QP the fp64 continuation leaves unsolved is solved again cold in fp64, so it ends
+    exactly as the fp64 path ends it.  iter_max = 3 leaves most QPs unsolved either way:
+    every QP the mixed call reports unsolved carries the plain fp64 outputs bit for bit."""
+    qp, x0 = pkg.srbd_model.generate_batch(300, N=20, seed=23, constraints="box_u")
+    st = dict(NMPC, iter_max=3)
+    plain = pkg.capi.solve(qp, x0, st, stats=True)
+    mix = pkg.capi.solve(qp, x0, dict(st, f32_iters=3), stats=True)
+    bad = mix["status"] != 0
+    assert bad.sum() > 100, np.bincount(mix["status"])
+    for key in ("x", "u", "pi", "status", "iter", "res", "obj", "stat"):
+        assert np.array_equal(mix[key][bad], plain[key][bad]), key
+    assert np.all(plain["status"][~bad] != 0) or np.all(mix["res"][~bad] <= 1e-4)
