@@ -35,6 +35,21 @@ def test_abi_version_and_strings(pkg):
     assert pkg.capi.status_string(17) == "HpipmStatus::UnknownFailure"
 
 
+def test_settings_struct_layout_matches_the_header(pkg):
+    """The ctypes mirror of srbd_qp_settings ends where the C struct's last field ends:
+    srbd_qp_default_settings writes every field, so on a sentinel-filled buffer it
+    touches exactly the bytes up to the last field's end (trailing padding untouched),
+    and each extension field reads back its documented default."""
+    capi = pkg.capi
+    buf = (C.c_ubyte * 256)(*([0xAB] * 256))
+    capi.lib().srbd_qp_default_settings(C.cast(buf, C.POINTER(capi.Settings)))
+    last = capi.Settings._fields_[-1][0]
+    end = getattr(capi.Settings, last).offset + C.sizeof(C.c_int)
+    assert all(b == 0xAB for b in bytes(buf)[end:]), "C struct is larger than the ctypes mirror"
+    s = capi.Settings.from_buffer(buf)
+    assert (s.compute_residuals, s.f64_rescue, s.f32_iters) == (1, 0, 0)
+
+
 def test_default_settings_match_hpipm_cpp(pkg):
     s = pkg.capi.settings_struct()
     # hpipm-cpp/include/hpipm-cpp/ocp_qp_ipm_solver_settings.hpp:26-86
