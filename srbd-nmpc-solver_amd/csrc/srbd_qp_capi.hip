@@ -122,6 +122,9 @@ int srbd_qp_check_settings(const srbd_qp_settings* s) {
   if (s->tol_ineq <= 0.0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.tol_ineq must be positive");
   if (s->tol_comp <= 0.0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.tol_comp must be positive");
   if (s->reg_prim < 0.0) return fail(SRBD_QP_ESETTINGS, "OcpQpIpmSolverSettings.reg_prim must be non-negative");
+  // extensions (srbd_qp.h)
+  if (s->f64_rescue < 0) return fail(SRBD_QP_ESETTINGS, "srbd_qp_settings.f64_rescue must be non-negative");
+  if (s->f32_iters < 0) return fail(SRBD_QP_ESETTINGS, "srbd_qp_settings.f32_iters must be non-negative");
   return SRBD_QP_OK;
 }
 

@@ -22,6 +22,10 @@ struct OcpQpIpmSolverSettings {
   int pred_corr = 1;
   int ric_alg = 1;
   int split_step = 0;
+  // Extension (not in the reference; the default keeps its behaviour): the first
+  // f32_iters IPM iterations of a constrained solve run in fp32, then fp64 continues
+  // from that iterate to the tolerances above (srbd_qp_settings.f32_iters).
+  int f32_iters = 0;
 
   // throws std::runtime_error on an invalid setting
   void checkSettings() const;

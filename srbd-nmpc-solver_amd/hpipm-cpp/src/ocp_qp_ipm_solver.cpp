@@ -134,6 +134,7 @@ struct OcpQpIpmSolver::Impl {
     s.pred_corr = settings.pred_corr;
     s.ric_alg = settings.ric_alg;
     s.split_step = settings.split_step;
+    s.f32_iters = settings.f32_iters;
     return s;
   }
 

@@ -50,6 +50,14 @@ def test_settings_struct_layout_matches_the_header(pkg):
     assert (s.compute_residuals, s.f64_rescue, s.f32_iters) == (1, 0, 0)
 
 
+def test_extension_settings_are_validated(pkg):
+    capi = pkg.capi
+    for key in ("f64_rescue", "f32_iters"):
+        s = capi.settings_struct({key: -1})
+        assert capi.lib().srbd_qp_check_settings(C.byref(s)) == -6  # SRBD_QP_ESETTINGS
+        assert key in capi.lib().srbd_qp_last_error().decode()
+
+
 def test_default_settings_match_hpipm_cpp(pkg):
     s = pkg.capi.settings_struct()
     # hpipm-cpp/include/hpipm-cpp/ocp_qp_ipm_solver_settings.hpp:26-86
