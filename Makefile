@@ -16,10 +16,11 @@ HPIPM_SRCS := $(wildcard $(HPIPM_DIR)/src/*.cpp)
 HPIPM_HDRS := $(wildcard $(HPIPM_DIR)/include/hpipm-cpp/*.hpp) include/srbd_qp.h
 HPIPM_LIB := $(PKG)/libhpipm-cpp.so
 HPIPM_TEST := build/hpipm_cpp_test
+HPIPM_BENCH := build/call_pattern_bench
 CXXFLAGS ?= -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
 HPIPM_INC := -Iinclude -I$(HPIPM_DIR)/include
 
-all: $(LIB) $(HPIPM_LIB) $(HPIPM_TEST) oracle
+all: $(LIB) $(HPIPM_LIB) $(HPIPM_TEST) $(HPIPM_BENCH) oracle
 
 # hpipm-cpp interface (host C++ over the C-ABI); rpath $ORIGIN finds libsrbd_qp.so
 $(OBJDIR)/hpipm/%.o: $(HPIPM_DIR)/src/%.cpp $(HPIPM_HDRS)
@@ -30,6 +31,12 @@ $(HPIPM_LIB): $(patsubst $(HPIPM_DIR)/src/%.cpp,$(OBJDIR)/hpipm/%.o,$(HPIPM_SRCS
 	$(CXX) -shared -o $@ $(filter %.o,$^) -L$(PKG) -lsrbd_qp -Wl,-rpath,'$$ORIGIN'
 
 $(HPIPM_TEST): $(HPIPM_DIR)/test/ocp_qp_ipm_solver_test.cpp $(HPIPM_DIR)/test/test_util.hpp $(HPIPM_LIB)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) $(HPIPM_INC) -o $@ $< -L$(PKG) -lhpipm-cpp -lsrbd_qp \
+	  -Wl,-rpath,'$$ORIGIN/../$(PKG)'
+
+# the reference caller's construct-solve-destruct pattern through hpipm-cpp (bench.py)
+$(HPIPM_BENCH): $(HPIPM_DIR)/bench/call_pattern_bench.cpp $(HPIPM_LIB)
 	@mkdir -p build
 	$(CXX) $(CXXFLAGS) $(HPIPM_INC) -o $@ $< -L$(PKG) -lhpipm-cpp -lsrbd_qp \
 	  -Wl,-rpath,'$$ORIGIN/../$(PKG)'

@@ -132,6 +132,31 @@ def device_shard(pkg, h, N, constraints, batch, rank, seed, device, np_dtype=np.
     return dt, xs, us, x0
 
 
+def shard_buffers(capi, dt, batch, N, dtype, device):
+    """Zeroed solution tensors (x, u, pi, status, iter) for one rank's shard and the
+    C-ABI structs pointing at the shard's device data / solution."""
+    import torch
+    f = dict(dtype=torch.float32 if dtype == "f32" else torch.float64, device=device)
+    sol_t = {"x": torch.zeros(batch, N + 1, 12, **f), "u": torch.zeros(batch, N, 12, **f),
+             "pi": torch.zeros(batch, N + 1, 12, **f),
+             "status": torch.zeros(batch, dtype=torch.int32, device=device),
+             "iter": torch.zeros(batch, dtype=torch.int32, device=device)}
+    DataT, SolT = (capi.Data32, capi.Solution32) if dtype == "f32" else (capi.Data, capi.Solution)
+    data = DataT(**{k: (None if dt.get(k) is None else dt[k].data_ptr()) for k in capi.DATA_FIELDS})
+    sol = SolT(**{k: (sol_t[k].data_ptr() if k in sol_t else None) for k in capi.SOL_FIELDS})
+    return sol_t, data, sol
+
+
+def gather_solutions(pkg, sol_t, world, rank, cpu_staged=False):
+    """The config-4 gather: every rank's (x, u, pi) to rank 0 in one message per rank
+    (RCCL over xGMI; cpu_staged=True stages through host memory for a gloo group).
+    Returns the list of payloads on rank 0, None elsewhere."""
+    payload = pkg.dist.solution_payload(sol_t["x"], sol_t["u"], sol_t["pi"])
+    if cpu_staged:
+        payload = payload.cpu()
+    return pkg.dist.gather_to_root(payload, world, rank)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -139,6 +164,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default=DEFAULT_WORKLOAD, choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="QPs per rank (default: workload's)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="QPs over all ranks, split evenly (strong scaling; BASELINE config 4 is "
+                         "--gpus 8 --global-batch 262144)")
     ap.add_argument("--cpu-pool", type=int, default=4096, help="QPs in the cpu_baseline sample")
     ap.add_argument("--seed", type=int, default=1003)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline budget")
@@ -180,6 +208,10 @@ def main():
     dtype = wl[4] if len(wl) > 4 else "f64"
     np_dtype = np.float32 if dtype == "f32" else np.float64
     batch = args.batch or default_batch
+    if args.global_batch:
+        if args.global_batch % world:
+            raise SystemExit(f"--global-batch {args.global_batch} is not divisible by {world} ranks")
+        batch = args.global_batch // world
     log(f"[rank {rank}] workload={args.workload} batch/rank={batch} N={N} world={world}")
     t0 = time.perf_counter()
     stage_major = args.layout == "stage"
@@ -193,14 +225,7 @@ def main():
     log(f"[rank {rank}] {batch} distinct QPs generated (linearised on device) in "
         f"{time.perf_counter() - t0:.1f}s")
 
-    f64 = dict(dtype=torch.float32 if dtype == "f32" else torch.float64, device=device)
-    sol_t = {"x": torch.zeros(batch, N + 1, 12, **f64), "u": torch.zeros(batch, N, 12, **f64),
-             "pi": torch.zeros(batch, N + 1, 12, **f64),
-             "status": torch.zeros(batch, dtype=torch.int32, device=device),
-             "iter": torch.zeros(batch, dtype=torch.int32, device=device)}
-    DataT, SolT = (capi.Data32, capi.Solution32) if dtype == "f32" else (capi.Data, capi.Solution)
-    data = DataT(**{k: (None if dt.get(k) is None else dt[k].data_ptr()) for k in capi.DATA_FIELDS})
-    sol = SolT(**{k: (sol_t[k].data_ptr() if k in sol_t else None) for k in capi.SOL_FIELDS})
+    sol_t, data, sol = shard_buffers(capi, dt, batch, N, dtype, device)
     # solver settings of the reference caller (NMPC_solver.cpp:70-82)
     settings = capi.settings_struct(F32_SETTINGS if dtype == "f32" else NMPC_SETTINGS)
     settings.f64_rescue = int(args.f64_rescue)
@@ -244,16 +269,20 @@ def main():
     if not args.no_host_path and not stage_major and rank == 0:
         host = host_path(capi, h, dt, batch, N, settings, dtype)
 
+    # ---- the reference's construct-solve-destroy call pattern, batch 1 (secondary) ----
+    pattern = None
+    if not args.no_host_path and rank == 0 and world == 1 and args.workload == DEFAULT_WORKLOAD:
+        pattern = call_pattern(pkg, args.seed)
+
     # ---- solution gather to rank 0 over RCCL (BASELINE config 4) ----
     gather_ms = None
     if distributed and not args.no_gather:
-        payload = pkg.dist.solution_payload(sol_t["x"], sol_t["u"], sol_t["pi"])
         dist.barrier()
         torch.cuda.synchronize()
         tg = time.perf_counter()
         reps = 5
         for _ in range(reps):
-            pkg.dist.gather_to_root(payload, world, rank)
+            gather_solutions(pkg, sol_t, world, rank)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) / reps * 1e3
 
@@ -303,7 +332,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_batch else "weak",
         "vs_baseline": None,
         "dtype": dtype + (f" (first {args.f32_iters} IPM iterations f32)"
                           if args.f32_iters and dtype == "f64" and constraints != "none" else "")
@@ -331,6 +360,8 @@ def main():
         line["sqp_pipeline"] = pipeline
     if host is not None:
         line["host_buffers"] = host
+    if pattern is not None:
+        line["reference_call_pattern"] = pattern
     if gather_ms is not None:
         line["gather"] = {"ms": gather_ms, "bytes_per_rank": batch * (2 * (N + 1) * 12 + N * 12) * 8,
                           "value_with_gather": total_qps / (t_max / args.steps + gather_ms * 1e-3)}
@@ -524,6 +555,49 @@ def host_path(capi, h, dt, batch, N, settings, dtype, max_batch=16384, reps=2):
             "latency_batch1_ms": float(np.median(lat[1:])) * 1e3}
 
 
+def call_pattern(pkg, seed, N=20, reps=20, oracle_reps=400):
+    """The reference caller's own pattern (NMPC_solver.cpp:316-330, 362-372): per SQP
+    iteration a fresh hpipm::OcpQpIpmSolver is constructed, solves ONE SRBD QP from
+    host Eigen-layout buffers and is destroyed, 15 times per NMPC step.  Timed by the
+    compiled C++ program build/call_pattern_bench through libhpipm-cpp.so (handles come
+    from the shim's pool, the host staging is pinned), beside the C oracle solving the
+    same QP on one host core."""
+    import subprocess
+    import tempfile
+    exe = REPO / "build" / "call_pattern_bench"
+    if not exe.exists():
+        return {"error": f"{exe} not built"}
+    qp, x0 = pkg.srbd_model.generate_batch(1, N=N, seed=seed)
+    p = qp.packed()
+    vals = [np.array([float(N)])]
+    for k in range(N):
+        for name in ("A", "B", "b", "Q", "S", "R", "q", "r"):
+            vals.append(p[name][0].reshape(N + (1 if name in ("Q", "q") else 0), -1)[k])
+    vals += [p["Q"][0].reshape(N + 1, -1)[N], p["q"][0].reshape(N + 1, -1)[N], x0[0]]
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.concatenate(vals).astype("<f8").tobytes())
+        path = f.name
+    try:
+        r = subprocess.run([str(exe), path, str(reps)], capture_output=True, text=True, timeout=300)
+    finally:
+        os.unlink(path)
+    if r.returncode != 0:
+        return {"error": (r.stdout + r.stderr)[-2000:]}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle  # test infrastructure: CPU baseline leg only
+    oracle.solve_batch_threaded(qp, NMPC_SETTINGS, x0, 1)
+    ts = []
+    for _ in range(oracle_reps):
+        _, d = oracle.solve_batch_threaded(qp, NMPC_SETTINGS, x0, 1)
+        ts.append(d)
+    out["what"] = ("NMPC_solver.cpp:316-330 call pattern through hpipm-cpp: construct OcpQpIpmSolver, "
+                   "solve one SRBD QP (N=20) from host buffers, destroy; 15 per NMPC step")
+    out["oracle_1_core_us"] = {"median": float(np.median(ts)) * 1e6, "min": float(np.min(ts)) * 1e6,
+                               "kind": "port", "cores": 1}
+    return out
+
+
 def sqp_pipeline(pkg, h, N, constraints, batch, xs, us, x0, device, settings, iters=3):
     """One SQP iteration of NMPCSolver::controlLoop (NMPC_solver.cpp:362-372) for the
     whole batch on the device: srbd_qp_srbd_linearize_f64 -> solve ->
@@ -575,25 +649,25 @@ def sqp_pipeline(pkg, h, N, constraints, batch, xs, us, x0, device, settings, it
 
 def roofline(constraints, achieved_gbs, traffic, kernel_ms, bytes_qp, flops_qp, batch, iters,
              dtype="f64"):
-    """Unconstrained: one streaming sweep, HBM-bound.  IPM: every
-    iteration re-sweeps the QP, so the binding roof is FP64 compute on the
-    algorithmic flops x iterations actually taken (IPM rows)."""
+    """HBM roofline of the solve.  Unconstrained: one streaming sweep,
+    achieved = algorithmic bytes per launch / kernel time.  IPM: the QP data does not
+    fit on-chip, so every iteration re-streams it; achieved = algorithmic bytes x
+    iterations taken / kernel time, against the same 8 TB/s peak (no MFMA is used:
+    the 12 x 12 blocks run on the FP vector pipe)."""
     if constraints == "none":
         return {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                 "kernel": "riccati_unconstr_kernel<true>", "kernel_avg_ms": kernel_ms,
                 "alg_bytes_per_qp": bytes_qp}
-    # per IPM iteration: factorization sweep + corrector sweep + residuals (~1.4 sweeps)
-    it = float(np.mean(iters))
-    flops = flops_qp * 1.4 * max(it, 1.0) * batch
-    tf = flops / (kernel_ms * 1e-3) / 1e12
+    it = max(float(np.mean(iters)), 1.0)
+    gbs = achieved_gbs * it
     peak = FP32_PEAK_TFS if dtype == "f32" else FP64_PEAK_TFS
-    return {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s",
-            "frac": tf / peak, "traffic": traffic,
-            "kernel": "ipm_phase_kernel<*> (init, RB, F1, B2, F2, out per iteration)",
-            "kernel_avg_ms": kernel_ms, "alg_flops_per_qp_iter": flops_qp * 1.4,
-            "mean_iters": it, "note": "no MFMA: 12x12 blocks run on the FP vector pipe (MFMA f64 = VALU rate)",
-            "hbm_frac_of_alg_bytes": achieved_gbs / HBM_PEAK_GBS}
+    tf = flops_qp * 1.4 * it * batch / (kernel_ms * 1e-3) / 1e12
+    return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": "ipm_phase_kernel<*> (init, RB+F1, B2+F2, out; whole solve)",
+            "kernel_avg_ms": kernel_ms, "alg_bytes_per_qp_iter": bytes_qp, "mean_iters": it,
+            "fp_vector_frac": tf / peak}
 
 
 def settings_dict(s):

@@ -531,12 +531,20 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   bool cont = false;
   if (wb) {
     int bad = 0;
-    auto chk = [&](real v, bool is_t) { bad |= !__builtin_isfinite(v) || (is_t && !(v > real(0.0))); };
+    // every t > 0; every lam >= 0, and > 0 on an active side (a multiplier that
+    // underflowed to 0 there would pin the fraction-to-boundary step at 0)
+    auto chk = [&](real v, bool pos) { bad |= !__builtin_isfinite(v) || (pos ? !(v > real(0.0)) : v < real(0.0)); };
+    auto chk_bar = [&](const real* p, const Side& s) {
+      chk(p[0], s.ml != real(0.0));
+      chk(p[12], s.mu != real(0.0));
+      chk(p[24], true);
+      chk(p[36], true);
+    };
     for (int k = 0; k <= N && lane < kMaxDim; ++k) {
       const real* w = wb + (size_t)k * warm_w;
-      for (int j = k < N ? 0 : 4; j < 8; ++j) chk(w[j * 12 + lane], (j & 3) >= 2);  // (no u_N)
-      for (int ch = 0; ch < c.nch; ++ch)
-        for (int j = 0; j < 4; ++j) chk(w[96 + ch * 48 + j * 12 + lane], j >= 2);
+      if (k < N) chk_bar(w + lane, c.side_u(k, lane));  // (no u_N)
+      chk_bar(w + 48 + lane, c.side_x(k, lane));
+      for (int ch = 0; ch < c.nch; ++ch) chk_bar(w + 96 + ch * 48 + lane, c.side_g(k, ch, lane));
       if (k < N && uel) chk(c.u()[(size_t)k * nu + lane], false);
       if (k > 0 && xel) {
         chk(c.x()[(size_t)k * nx + lane], false);

@@ -42,6 +42,10 @@ struct srbd_qp_handle_s {
   // host-solve staging (device)
   double* stage = nullptr;
   size_t stage_bytes = 0;
+  // small host solves (batch 1: the reference's call pattern): pinned mirror of the
+  // staging buffer, so inputs go over in one copy and the outputs come back in one
+  void* pinned = nullptr;
+  size_t pinned_bytes = 0;
   // nx < 12 or nu < 12: the 12 x 12 embedding (pad.hip), allocated on first use
   void* pad = nullptr;
   size_t pad_bytes = 0;
@@ -192,6 +196,7 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->ws) hipFree(h->ws);
   if (h->stage) hipFree(h->stage);
+  if (h->pinned) hipHostFree(h->pinned);
   if (h->pad) hipFree(h->pad);
   if (h->nmpc) hipFree(h->nmpc);
   if (h->nmpc_active_host) hipHostFree(h->nmpc_active_host);
@@ -411,7 +416,6 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
   const size_t need = sizeof(double) * per_qp * (size_t)R + 2 * sizeof(int) * (size_t)R + 256;
   if (need > h->resc_bytes) {
     if (h->resc) hipFree(h->resc);
-  if (h->mixed) hipFree(h->mixed);
     h->resc = nullptr;
     h->resc_bytes = 0;
     e = hipMalloc(&h->resc, need);
@@ -644,6 +648,8 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
 // host-buffer convenience path
 // ---------------------------------------------------------------------------
 namespace {
+// host solves whose staged bytes fit this go through the handle's pinned buffer
+constexpr size_t kPinnedMaxBytes = size_t(8) << 20;
 struct Field {
   const void* host;
   size_t bytes;
@@ -710,19 +716,48 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
   hipError_t e = hipSuccess;
   if (off > h->stage_bytes) {
     if (h->stage) hipFree(h->stage);
+  if (h->pinned) hipHostFree(h->pinned);
     h->stage = nullptr;
     h->stage_bytes = 0;
     e = hipMalloc(reinterpret_cast<void**>(&h->stage), off);
     if (e == hipSuccess) h->stage_bytes = off;
   }
   char* base = reinterpret_cast<char*>(h->stage);
-  for (size_t i = 0; e == hipSuccess && i < in.size(); ++i)
+  // Small problems go through a pinned mirror of the staging buffer: the fields are
+  // packed with memcpy and cross PCIe in one DMA each way (per-field pageable copies
+  // cost ~10 us of driver latency apiece).  Large ones copy field by field: the
+  // pageable path streams at PCIe rate with no extra host pass over the data.
+  const size_t in_end = outs.empty() ? off : outs.front().off;
+  const bool small = off <= kPinnedMaxBytes;
+  char* pin = nullptr;
+  if (e == hipSuccess && small) {
+    if (off > h->pinned_bytes) {
+      if (h->pinned) hipHostFree(h->pinned);
+      h->pinned = nullptr;
+      h->pinned_bytes = 0;
+      e = hipHostMalloc(&h->pinned, off);
+      if (e == hipSuccess) h->pinned_bytes = off;
+    }
+    pin = reinterpret_cast<char*>(h->pinned);
+  }
+  if (e == hipSuccess && small) {
+    for (const Field& f : in) std::memcpy(pin + f.off, f.host, f.bytes);
+    e = hipMemcpyAsync(base, pin, in_end, hipMemcpyHostToDevice, h->stream);
+  }
+  for (size_t i = 0; !small && e == hipSuccess && i < in.size(); ++i)
     e = hipMemcpyAsync(base + in[i].off, in[i].host, in[i].bytes, hipMemcpyHostToDevice, h->stream);
   // warm start: x/u outputs are inputs too
   if (e == hipSuccess && st->warm_start) {
-    e = hipMemcpyAsync(base + ox, s->x, B * (N + 1) * nx * D, hipMemcpyHostToDevice, h->stream);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(base + ou, s->u, B * N * nu * D, hipMemcpyHostToDevice, h->stream);
+    const size_t bx = B * (N + 1) * nx * D, bu = B * N * nu * D;
+    if (small) {
+      std::memcpy(pin + ox, s->x, bx);
+      std::memcpy(pin + ou, s->u, bu);
+      // x and u are adjacent in the staging layout (addo order, 256-byte aligned)
+      e = hipMemcpyAsync(base + ox, pin + ox, ou + bu - ox, hipMemcpyHostToDevice, h->stream);
+    } else {
+      e = hipMemcpyAsync(base + ox, s->x, bx, hipMemcpyHostToDevice, h->stream);
+      if (e == hipSuccess) e = hipMemcpyAsync(base + ou, s->u, bu, hipMemcpyHostToDevice, h->stream);
+    }
   }
   if (e != hipSuccess) {
     hipSetDevice(prev);
@@ -747,9 +782,17 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
   rc = solve_impl<T>(h, batch, st, &dd, &ss, nullptr);
   if (rc) return rc;
   hipSetDevice(h->device);
-  for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)
-    e = hipMemcpyAsync(outs[i].host, base + outs[i].off, outs[i].bytes, hipMemcpyDeviceToHost, h->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (small) {
+    if (e == hipSuccess && in_end < off)
+      e = hipMemcpyAsync(pin + in_end, base + in_end, off - in_end, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)
+      std::memcpy(outs[i].host, pin + outs[i].off, outs[i].bytes);
+  } else {
+    for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)
+      e = hipMemcpyAsync(outs[i].host, base + outs[i].off, outs[i].bytes, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  }
   hipSetDevice(prev);
   if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("device->host copy: ") + hipGetErrorString(e));
   return SRBD_QP_OK;

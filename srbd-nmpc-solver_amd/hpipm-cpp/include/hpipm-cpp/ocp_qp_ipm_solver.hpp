@@ -58,7 +58,7 @@ class OcpQpIpmSolver {
   OcpQpIpmSolver(OcpQpIpmSolver&&) noexcept;
   OcpQpIpmSolver& operator=(OcpQpIpmSolver&&) noexcept;
 
-  // checkSettings() and store (ocp_qp_ipm_solver.cpp:83-117)
+  // store, unchecked like the reference (ocp_qp_ipm_solver.cpp:83-117); solve() checks
   void setSolverSettings(const OcpQpIpmSolverSettings& solver_settings);
 
   // dimension check + device workspace for these dimensions (:120-178)

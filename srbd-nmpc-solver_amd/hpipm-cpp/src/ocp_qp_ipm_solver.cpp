@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 
@@ -81,6 +82,71 @@ Shape shape_of(const OcpQpDim& d) {
   return s;
 }
 
+// Process-wide pool of C-ABI handles.  The reference's caller builds a new
+// OcpQpIpmSolver for every SQP iteration (NMPC_solver.cpp:318-319); a handle owns a
+// HIP stream and a device workspace, so creating one per solver would put a stream
+// create, hipMallocs and a stream destroy around every single QP solve.  A solver
+// takes a handle of its shape from the pool (or creates one) and gives it back when it
+// is destroyed or resized; the next solver of the same shape reuses it.  A handle is
+// used by one solver at a time, so concurrent solvers on different threads stay
+// independent, as HPIPM instances with separate memory are.
+class HandlePool {
+ public:
+  static HandlePool& get() {
+    // never destroyed: handles still pooled at exit are reclaimed with the process
+    // (freeing them from a static destructor would race the HIP runtime's teardown)
+    static HandlePool* pool = new HandlePool();
+    return *pool;
+  }
+  srbd_qp_handle acquire(int device, const Shape& s, int batch, int* capacity) {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      size_t best = free_.size();
+      for (size_t i = 0; i < free_.size(); ++i) {
+        const Entry& e = free_[i];
+        if (e.device == device && e.shape == s && e.capacity >= batch &&
+            (best == free_.size() || e.capacity < free_[best].capacity))
+          best = i;
+      }
+      if (best != free_.size()) {
+        Entry e = free_[best];
+        free_.erase(free_.begin() + static_cast<long>(best));
+        *capacity = e.capacity;
+        return e.h;
+      }
+    }
+    srbd_qp_dims d{s.N, s.nx, s.nu, s.ng, s.box_u ? 1 : 0, s.box_x ? 1 : 0, SRBD_QP_LAYOUT_QP_MAJOR};
+    srbd_qp_handle h = nullptr;
+    if (srbd_qp_create(&d, batch, device, &h) != SRBD_QP_OK) abi_error("OcpQpIpmSolver::resize");
+    *capacity = batch;
+    return h;
+  }
+  void release(int device, const Shape& s, int capacity, srbd_qp_handle h) {
+    if (!h) return;
+    // big workspaces (batched solves) are freed, not parked
+    if (srbd_qp_workspace_bytes(h) <= kMaxPooledBytes) {
+      std::lock_guard<std::mutex> lk(m_);
+      if (free_.size() < kMaxPooled) {
+        free_.push_back(Entry{device, s, capacity, h});
+        return;
+      }
+    }
+    srbd_qp_destroy(h);
+  }
+
+ private:
+  struct Entry {
+    int device;
+    Shape shape;
+    int capacity;
+    srbd_qp_handle h;
+  };
+  static constexpr size_t kMaxPooled = 16;
+  static constexpr size_t kMaxPooledBytes = size_t(256) << 20;
+  std::mutex m_;
+  std::vector<Entry> free_;
+};
+
 }  // namespace
 
 struct OcpQpIpmSolver::Impl {
@@ -101,7 +167,7 @@ struct OcpQpIpmSolver::Impl {
 
   ~Impl() { release(); }
   void release() {
-    if (handle) srbd_qp_destroy(handle);
+    if (handle) HandlePool::get().release(device, shape, capacity, handle);
     handle = nullptr;
     capacity = 0;
   }
@@ -109,13 +175,8 @@ struct OcpQpIpmSolver::Impl {
   void ensure_handle(const Shape& s, int batch) {
     if (handle && s == shape && batch <= capacity) return;
     release();
-    srbd_qp_dims d{s.N, s.nx, s.nu, s.ng, s.box_u ? 1 : 0, s.box_x ? 1 : 0, SRBD_QP_LAYOUT_QP_MAJOR};
-    if (srbd_qp_create(&d, std::max(batch, 1), device, &handle) != SRBD_QP_OK) {
-      handle = nullptr;
-      abi_error("OcpQpIpmSolver::resize");
-    }
+    handle = HandlePool::get().acquire(device, s, std::max(batch, 1), &capacity);
     shape = s;
-    capacity = std::max(batch, 1);
   }
 
   srbd_qp_settings abi_settings() const {
@@ -331,8 +392,10 @@ OcpQpIpmSolver::~OcpQpIpmSolver() = default;
 OcpQpIpmSolver::OcpQpIpmSolver(OcpQpIpmSolver&&) noexcept = default;
 OcpQpIpmSolver& OcpQpIpmSolver::operator=(OcpQpIpmSolver&&) noexcept = default;
 
+// Stores the settings as the reference does (ocp_qp_ipm_solver.cpp:83-117: no
+// checkSettings() there); an invalid value is reported by solve(), whose C-ABI call
+// runs srbd_qp_check_settings.
 void OcpQpIpmSolver::setSolverSettings(const OcpQpIpmSolverSettings& solver_settings) {
-  solver_settings.checkSettings();
   impl_->settings = solver_settings;
 }
 

@@ -26,6 +26,7 @@ void OcpQpIpmSolverSettings::checkSettings() const {
   s.pred_corr = pred_corr;
   s.ric_alg = ric_alg;
   s.split_step = split_step;
+  s.f32_iters = f32_iters;
   if (srbd_qp_check_settings(&s) != SRBD_QP_OK) throw std::runtime_error(srbd_qp_last_error());
 }
 

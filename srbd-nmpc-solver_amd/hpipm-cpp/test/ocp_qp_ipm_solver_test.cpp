@@ -372,7 +372,16 @@ TEST(settings_errors, false) {
   EXPECT_THROW_MSG(s.checkSettings(), "alpha_min must be less than 1.0");
   s = hpipm::OcpQpIpmSolverSettings();
   s.tol_comp = 0.0;
-  EXPECT_THROW_MSG(hpipm::OcpQpIpmSolver solver(s), "tol_comp must be positive");
+  EXPECT_THROW_MSG(s.checkSettings(), "tol_comp must be positive");
+  {
+    // setSolverSettings stores without checking, as the reference does
+    // (ocp_qp_ipm_solver.cpp:83-117); solve() reports the invalid value
+    hpipm::OcpQpIpmSolver solver(s);
+    EXPECT_TRUE(solver.getIpmSolverSettings().tol_comp == 0.0);
+  }
+  s = hpipm::OcpQpIpmSolverSettings();
+  s.f32_iters = -1;  // the extension goes through the same shared check
+  EXPECT_THROW_MSG(s.checkSettings(), "f32_iters must be non-negative");
   s = hpipm::OcpQpIpmSolverSettings();
   s.reg_prim = -1.0;
   EXPECT_THROW_MSG(s.checkSettings(), "reg_prim must be non-negative");

@@ -147,6 +147,31 @@ def test_unconstrained_full_batch_kkt_and_oracle_windows(pkg, oracle):
             assert helpers.is_approx(got, ref[k], 1e-10), (k, w)
 
 
+def test_config2_n10_b4096_kkt_and_oracle_windows(pkg, oracle):
+    """BASELINE config 2 at its stated size: 4096 SRBD QPs, N = 10 (the one-lane-group-
+    per-QP bring-up shape: 1 wave per SIMD on the chip).  Every QP satisfies its KKT
+    system to 1e-10 relative to its terms (reg_prim = 0, as above) and three windows
+    across the batch equal the oracle at 1e-10."""
+    import torch
+    N, batch = 10, 4096
+    h, t = device_batch(pkg, N, "none", batch=batch)
+    st = dict(NMPC, reg_prim=0.0)
+    s = solve_on_device(pkg, h, t, N, st)
+    assert int((s["status"] != 0).sum()) == 0
+    assert int((s["iter"] != 0).sum()) == 0  # nc = 0: one Riccati sweep, iter 0
+    r = kkt_residuals(blocks(t, N), s, t["x0"])
+    assert r["x0"] == 0.0
+    for k in ("dyn", "gu", "gx", "gN"):
+        worst = r[k].max().item()
+        assert worst < 1e-10, (k, worst, int(torch.argmax(r[k])))
+    for w in (slice(0, 8), slice(batch // 2 - 4, batch // 2 + 4), slice(batch - 8, batch)):
+        qp, x0 = host_subset(pkg, t, N, "none", w)
+        ref = oracle.solve(qp, st, x0=x0)
+        for k in ("x", "u", "pi"):
+            got = s[k][w].cpu().numpy()
+            assert helpers.is_approx(got, ref[k], 1e-10), (k, w)
+
+
 def test_box_u_full_batch(pkg, oracle):
     """Config 3 (box on u, IPM, NMPC settings): every QP converges, stays inside its
     bounds, satisfies the dynamics to tol_eq, reports residuals below the
