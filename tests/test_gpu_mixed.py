@@ -118,3 +118,30 @@ def test_mixed_fallback_is_the_fp64_solve(pkg):
     for key in ("x", "u", "pi", "status", "iter", "res", "obj", "stat"):
         assert np.array_equal(mix[key][bad], plain[key][bad]), key
     assert np.all(plain["status"][~bad] != 0) or np.all(mix["res"][~bad] <= 1e-4)
+
+
+def test_one_handle_mixed_rescue_mixed_bit_identical(pkg):
+    """One handle serves, in turn, an fp64 solve with f32_iters, an fp32 solve with
+    f64_rescue whose unsolved set makes the rescue buffer grow, and the fp64 f32_iters
+    solve again: every result bit-identical to the same solve on a fresh handle.
+    (Growing the rescue buffer once freed the handle's mixed-precision buffer without
+    forgetting it, so the third solve wrote into freed device memory.)"""
+    N = 20
+    qp, x0 = pkg.srbd_model.generate_batch(64, N=N, seed=21, constraints="cone")
+    st64 = dict(NMPC, f32_iters=6)
+    # fp32 tolerances out of the fp32 pass's reach in 3 iterations: most of the batch
+    # continues in fp64
+    st32 = dict(iter_max=30, tol_stat=1e-6, tol_eq=1e-6, tol_ineq=1e-6, tol_comp=1e-6,
+                split_step=1, f64_rescue=3)
+    h = pkg.capi.Handle(N, 12, 12, 24, False, False, capacity=qp.batch)
+    a1 = pkg.capi.solve(qp, x0, st64, handle=h)
+    b1 = pkg.capi.solve(qp, x0, st32, handle=h, dtype=np.float32)
+    a2 = pkg.capi.solve(qp, x0, st64, handle=h)
+    h.close()
+    a_ref = pkg.capi.solve(qp, x0, st64)
+    b_ref = pkg.capi.solve(qp, x0, st32, dtype=np.float32)
+    assert np.all(a_ref["status"] == 0) and np.all(b_ref["status"] == 0)
+    for key in a_ref:
+        assert np.array_equal(a1[key], a_ref[key]), ("first fp64", key)
+        assert np.array_equal(a2[key], a_ref[key]), ("second fp64", key)
+        assert np.array_equal(b1[key], b_ref[key]), ("fp32 rescue", key)
