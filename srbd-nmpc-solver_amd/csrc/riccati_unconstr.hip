@@ -20,10 +20,6 @@
 #include "kernels.h"
 #include "riccati.h"
 
-#ifndef SRBD_WS_STAGE_MAJOR
-#define SRBD_WS_STAGE_MAJOR 1
-#endif
-
 #define SRBD_REAL double
 #define SRBD_NS ric_f64
 #include "riccati_unconstr_impl.h"

@@ -1,23 +1,25 @@
 // riccati_unconstr_impl.h -- body of the unconstrained batched solve, instantiated
 // per precision by riccati_unconstr.hip (SRBD_REAL, SRBD_NS).  No include guard.
-
-#ifndef SRBD_EARLY_LOADS
-#define SRBD_EARLY_LOADS 0
-#endif
-#ifndef SRBD_PREFETCH_AB
-#define SRBD_PREFETCH_AB 0
-#endif
-#ifndef SRBD_NT_REC
-#define SRBD_NT_REC 0
-#endif
-#ifndef SRBD_NT_INPUTS
-#define SRBD_NT_INPUTS 0
-#endif
+//
+// Two kernels share one per-QP body (solve_qp), differing only in where a QP's stage
+// blocks and forward records live:
+//   riccati_unconstr_kernel      (HbmSrc)  large batches: 16 lanes per QP, 16 QPs per
+//                                          workgroup; blocks streamed from HBM, records
+//                                          in the stage-major HBM workspace.
+//   riccati_unconstr_lds_kernel  (LdsSrc)  small batches (the reference's one QP per
+//                                          solve() call): one QP per workgroup; the whole
+//                                          QP is first copied into an LDS image with
+//                                          global->LDS DMA, the records overwrite the
+//                                          stage slots they were computed from.  The
+//                                          per-stage memory latency (three dependent HBM
+//                                          round trips per backward stage) becomes an
+//                                          LDS latency.
+// Same instructions on the same values: the two kernels' outputs are bit-identical
+// (tests/test_gpu_riccati.py::test_latency_kernel_bit_identical).
 namespace srbd {
 namespace SRBD_NS {
 
 using real = SRBD_REAL;
-
 
 // out[i] = v[i] for i < n (static register indices, predicated stores)
 __device__ __forceinline__ void store_n(real* out, int n, const real (&v)[12]) {
@@ -27,192 +29,111 @@ __device__ __forceinline__ void store_n(real* out, int n, const real (&v)[12]) {
   });
 }
 
-template <bool FULL>
-struct StageLoader {
-  int nx, nu;
-  // column `col` of an (rows x ncols) column-major block, zero-padded
-  __device__ __forceinline__ void col(const real* blk, int rows, int ld, int c, bool ok,
-                                      real (&v)[12]) const {
-    if constexpr (FULL) {
-#if SRBD_NT_INPUTS == 2
-      load12_nt(blk + c * 12, v);
-#elif SRBD_NT_INPUTS
-      // streamed once: non-temporal, so the records keep the caches
-      const real* q = blk + c * 12;
-      sfor<0, 12>([&](auto i) {
-        constexpr int I = decltype(i)::value;
-        v[I] = __builtin_nontemporal_load(q + I);
-      });
-#else
-      load12(blk + c * 12, v);
-#endif
-    } else {
-      load_col_pad(blk + (size_t)c * ld, rows, ok, v);
-    }
+// ---- where a QP's blocks and records are ----
+
+// HBM, the C-ABI layout: QP-major ([batch][stage][blk], Eigen order) or stage-major
+// ([stage][batch][blk]).  Records stage-major across the batch: stage k of QP q at
+// ws[(k * batch + q) * kWsStage], so a wavefront's four QPs write / read one
+// contiguous block per stage.
+struct HbmSrc {
+  const ProblemArgsT<real>& a;
+  int qp;
+  __device__ const real* at(const real* base, int nstage, int blk, int k) const {
+    return a.layout == 1 ? base + ((size_t)k * a.batch + qp) * blk
+                         : base + ((size_t)qp * nstage + k) * blk;
   }
+  __device__ const real* A(int k) const { return at(a.A, a.N, 144, k); }
+  __device__ const real* B(int k) const { return at(a.B, a.N, 144, k); }
+  __device__ const real* b(int k) const { return at(a.b, a.N, 12, k); }
+  __device__ const real* Q(int k) const { return at(a.Q, a.N + 1, 144, k); }
+  __device__ const real* S(int k) const { return at(a.S, a.N, 144, k); }
+  __device__ const real* R(int k) const { return at(a.R, a.N, 144, k); }
+  __device__ const real* q(int k) const { return at(a.q, a.N + 1, 12, k); }
+  __device__ const real* r(int k) const { return at(a.r, a.N, 12, k); }
+  __device__ real* rec(int k) const { return a.ws + ((size_t)k * a.batch + qp) * kWsStage; }
 };
 
-template <bool FULL>
-__global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<real> a) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int qp = gid >> 4;
-  const int lane = threadIdx.x & (kGroup - 1);
-  if (qp >= a.batch) return;
+// LDS image of one QP: stage slot k (k = 0..N) holds the stage's blocks at the offsets
+// below (slot N: Q and q only); after the backward sweep has used slot k's blocks, the
+// stage's forward record (kernels.h kWs*, 402 reals) is written over them.
+constexpr int kImgA = 0, kImgB = 144, kImgb = 288, kImgQ = 300, kImgS = 444, kImgR = 588,
+              kImgq = 732, kImgr = 744, kImgStage = 756;
+static_assert(kWsStage <= kImgStage, "a record fits its stage slot");
+
+struct LdsSrc {
+  real* img;
+  __device__ real* slot(int k) const { return img + k * kImgStage; }
+  __device__ const real* A(int k) const { return slot(k) + kImgA; }
+  __device__ const real* B(int k) const { return slot(k) + kImgB; }
+  __device__ const real* b(int k) const { return slot(k) + kImgb; }
+  __device__ const real* Q(int k) const { return slot(k) + kImgQ; }
+  __device__ const real* S(int k) const { return slot(k) + kImgS; }
+  __device__ const real* R(int k) const { return slot(k) + kImgR; }
+  __device__ const real* q(int k) const { return slot(k) + kImgq; }
+  __device__ const real* r(int k) const { return slot(k) + kImgr; }
+  __device__ real* rec(int k) const { return slot(k); }
+};
+
+// ---- the solve of one QP by its 16-lane group ----
+template <class Src>
+__device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src& src, const int qp,
+                                         const int lane) {
+  constexpr int nx = 12, nu = 12;
+  constexpr size_t nxx = 144, nxu = 144;
   const int N = a.N;
-  const int nx = FULL ? 12 : a.nx;
-  const int nu = FULL ? 12 : a.nu;
   const bool isv = lane == kVecLane;
-  const int col = lane < kMaxDim ? lane : kMaxDim - 1;
+  const bool own = lane < kMaxDim;  // lane owns a block column
+  const int col = own ? lane : kMaxDim - 1;
   const real reg = a.reg;
-
-  const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu, nuu = (size_t)nu * nu;
-#ifdef SRBD_DIAG_SHARED_INPUT  // diagnostic build only: every QP reads QP (qp & 63)'s data
-  const int qin = qp & 63;
-#else
-  const int qin = qp;
-#endif
-  // input block of stage k: QP-major ([batch][stage][blk], Eigen order) or
-  // stage-major ([stage][batch][blk]: a wavefront's QPs adjacent in memory)
-  const bool smaj = a.layout == 1;
-  auto at = [&](const real* base, int nstage, size_t blk, int k) -> const real* {
-    return smaj ? base + ((size_t)k * a.batch + qin) * blk : base + ((size_t)qin * nstage + k) * blk;
-  };
-  // forward records, stage-major: stage k of QP q at ws[(k * batch + q) * kWsStage], so the
-  // four QPs of a wavefront write / read one contiguous 15 KB block per stage
-  auto rec_at = [&](int k) -> real* {
-#if SRBD_WS_STAGE_MAJOR
-    return a.ws + ((size_t)k * a.batch + qp) * kWsStage;
-#else
-    return a.ws + (size_t)qp * a.ws_qp + (size_t)k * kWsStage;
-#endif
-  };
-
-  StageLoader<FULL> ld{nx, nu};
-  const bool xcol = lane < nx;  // lane owns a real state column
-  const bool ucol = lane < nu;  // lane owns a real input column
 
   // ---------------- terminal stage: P_N = Q_N, p_N = q_N ----------------
   real P[12];
   if (isv) {
-    ld.col(at(a.q, N + 1, nx, N), nx, nx, 0, true, P);
+    load12(src.q(N), P);
   } else {
-    ld.col(at(a.Q, N + 1, nxx, N), nx, nx, col, xcol, P);
+    load12(src.Q(N) + col * 12, P);
   }
   {
-    real* rec = rec_at(N);
-    if (lane < kMaxDim) store_packed_col(rec + kWsP, lane, P);
+    real* rec = src.rec(N);
+    if (own) store_packed_col(rec + kWsP, lane, P);
     if (isv) store12(rec + kWsp, P);
-    if (a.P && xcol) store_n(a.P + ((size_t)qp * (N + 1) + N) * nxx + (size_t)lane * nx, nx, P);
+    if (a.P && own) store_n(a.P + ((size_t)qp * (N + 1) + N) * nxx + (size_t)lane * nx, nx, P);
     if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + N) * nx, nx, P);
   }
 
   // ---------------- backward sweep ----------------
   real A_[12], B_[12];
-  // A, B (VL: b) of stage k: column-owned
-  auto loadAB = [&](int k, real (&Av)[12], real (&Bv)[12]) {
-    if (isv) {
-      ld.col(at(a.b, N, nx, k), nx, nx, 0, true, Av);
-      sfor<0, 12>([&](auto i) { Bv[decltype(i)::value] = real(0.0); });
-    } else {
-      ld.col(at(a.A, N, nxx, k), nx, nx, col, xcol, Av);
-      ld.col(at(a.B, N, nxu, k), nx, nx, col, ucol, Bv);
-    }
-  };
-#if SRBD_PREFETCH_AB == 3
-  // B of stage k only (VL: zeros)
-  auto loadB = [&](int k, real (&Bv)[12]) {
-    if (isv) {
-      sfor<0, 12>([&](auto i) { Bv[decltype(i)::value] = real(0.0); });
-    } else {
-      ld.col(at(a.B, N, nxu, k), nx, nx, col, ucol, Bv);
-    }
-  };
-  auto loadA = [&](int k, real (&Av)[12]) {
-    if (isv) {
-      ld.col(at(a.b, N, nx, k), nx, nx, 0, true, Av);
-    } else {
-      ld.col(at(a.A, N, nxx, k), nx, nx, col, xcol, Av);
-    }
-  };
-  if (N > 0) loadB(N - 1, B_);
-#elif SRBD_PREFETCH_AB
-  if (N > 0) loadAB(N - 1, A_, B_);
-#endif
 #pragma unroll 1
   for (int k = N - 1; k >= 0; --k) {
-#if SRBD_PREFETCH_AB == 3
-    loadA(k, A_);
-#elif !SRBD_PREFETCH_AB
-    loadAB(k, A_, B_);
-#endif
+    // A, B (VL: b) of stage k, column-owned
+    if (isv) {
+      load12(src.b(k), A_);
+      sfor<0, 12>([&](auto i) { B_[decltype(i)::value] = real(0.0); });
+    } else {
+      load12(src.A(k) + col * 12, A_);
+      load12(src.B(k) + col * 12, B_);
+    }
     auto loadR = [&](real (&Rc)[12]) {
       if (isv) {
         sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = real(0.0); });
       } else {
-        ld.col(at(a.R, N, nuu, k), nu, nu, col, ucol, Rc);
-        if constexpr (!FULL) {
-          // padded inputs: R = 1 on the diagonal keeps G positive definite
-          sfor<0, 12>([&](auto i) {
-            constexpr int I = decltype(i)::value;
-            if (lane == I && lane >= nu) Rc[I] = real(1.0);
-          });
-        }
+        load12(src.R(k) + col * 12, Rc);
       }
     };
     auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
       if (isv) {
-        ld.col(at(a.r, N, nu, k), nu, nu, 0, true, Sc);
-        ld.col(at(a.q, N + 1, nx, k), nx, nx, 0, true, Qc);
+        load12(src.r(k), Sc);
+        load12(src.q(k), Qc);
       } else {
-        ld.col(at(a.S, N, nxu, k), nu, nu, col, xcol, Sc);
-        ld.col(at(a.Q, N + 1, nxx, k), nx, nx, col, xcol, Qc);
+        load12(src.S(k) + col * 12, Sc);
+        load12(src.Q(k) + col * 12, Qc);
       }
     };
     StageFactor<real> f;
-#if SRBD_PREFETCH_AB
-    // the next stage's A, B are requested half-way through this stage (after the
-    // products, before the triangular solves), so their latency hides behind
-    // the solves, the P update and the record stores
-    real An[12], Bn[12];
-#if SRBD_PREFETCH_AB == 3
-    // B only (24 VGPRs): A is requested at the top of the stage and hides
-    // behind P B, G and the Cholesky
-    riccati_step<1>(P, A_, B_, loadR, loadSQ, lane, reg, f, [&]() {
-      if (k > 0) loadB(k - 1, Bn);
-    });
-#else
-    riccati_step<SRBD_PREFETCH_AB>(P, A_, B_, loadR, loadSQ, lane, reg, f, [&]() {
-      if (k > 0) loadAB(k - 1, An, Bn);
-    });
-#endif
-#elif SRBD_EARLY_LOADS
-    // all five blocks of the stage requested up front: one memory latency per
-    // stage instead of three (R, then S/Q, behind the phase fences)
-    real Re[12], Se[12], Qe[12];
-    loadR(Re);
-    loadSQ(Se, Qe);
-    riccati_step(
-        P, A_, B_,
-        [&](real (&Rc)[12]) {
-          sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = Re[decltype(i)::value]; });
-        },
-        [&](real (&Sc)[12], real (&Qc)[12]) {
-          sfor<0, 12>([&](auto i) {
-            Sc[decltype(i)::value] = Se[decltype(i)::value];
-            Qc[decltype(i)::value] = Qe[decltype(i)::value];
-          });
-        },
-        lane, reg, f);
-#else
     riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
-#endif
 
-    real* rec = rec_at(k);
-#ifdef SRBD_DIAG_NO_RECORD  // diagnostic build only: no record traffic
-    if (k == -7) {
-#else
-    if (lane < kMaxDim) {
-#endif
+    real* rec = src.rec(k);
+    if (own) {
       sfor<0, 12>([&](auto m) {
         constexpr int M = decltype(m)::value;
         rec[kWsK + M * 12 + lane] = f.Kc[M];
@@ -225,30 +146,21 @@ __global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<r
       store12(rec + kWsbcl, A_);
       store12(rec + kWsp, f.F);
     }
-    if (a.P && xcol) store_n(a.P + ((size_t)qp * (N + 1) + k) * nxx + (size_t)lane * nx, nx, f.F);
+    if (a.P && own) store_n(a.P + ((size_t)qp * (N + 1) + k) * nxx + (size_t)lane * nx, nx, f.F);
     if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + k) * nx, nx, f.F);
-    if (a.K && xcol) store_n(a.K + ((size_t)qp * N + k) * nxu + (size_t)lane * nu, nu, f.Kc);
+    if (a.K && own) store_n(a.K + ((size_t)qp * N + k) * nxu + (size_t)lane * nu, nu, f.Kc);
     if (a.k && isv) store_n(a.k + ((size_t)qp * N + k) * nu, nu, f.Kc);
     sfor<0, 12>([&](auto i) {
       constexpr int I = decltype(i)::value;
       P[I] = f.F[I];
     });
-#if SRBD_PREFETCH_AB == 3
-    sfor<0, 12>([&](auto i) { B_[decltype(i)::value] = Bn[decltype(i)::value]; });
-#elif SRBD_PREFETCH_AB
-    sfor<0, 12>([&](auto i) {
-      constexpr int I = decltype(i)::value;
-      A_[I] = An[I];
-      B_[I] = Bn[I];
-    });
-#endif
   }
 
   // ---------------- forward sweep (row-owned) ----------------
   // The record rows of stage k+1 are loaded while stage k computes (the loads
   // do not depend on x), so each stage pays one memory latency less.
-  const int row = lane < kMaxDim ? lane : kMaxDim - 1;
-  real xv = (lane < nx) ? a.x0[(size_t)qp * nx + lane] : real(0.0);
+  const int row = col;
+  real xv = own ? a.x0[(size_t)qp * nx + lane] : real(0.0);
   bool bad = false;
   real* xo = a.x + (size_t)qp * (N + 1) * nx;
   real* uo = a.u + (size_t)qp * N * nu;
@@ -256,25 +168,17 @@ __global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<r
   real Pr[12], Kr[12], Ar[12], pv, kv, bv;
   auto load_rows = [&](int k, real (&P_)[12], real (&K_)[12], real (&A__)[12], real& p_,
                        real& k_, real& b_) {
-    const real* rec = rec_at(k);
+    const real* rec = src.rec(k);
     load_packed_sym(rec + kWsP, row, P_);
     p_ = rec[kWsp + row];
     if (k < N) {
-#if SRBD_NT_REC
-      load12_nt(rec + kWsK + row * 12, K_);
-      load12_nt(rec + kWsAcl + row * 12, A__);
-#else
       load12(rec + kWsK + row * 12, K_);
       load12(rec + kWsAcl + row * 12, A__);
-#endif
       k_ = rec[kWsk + row];
       b_ = rec[kWsbcl + row];
     }
   };
   load_rows(0, Pr, Kr, Ar, pv, kv, bv);
-#ifdef SRBD_DIAG_NO_FWD  // diagnostic build only
-  if (N > 0) return;
-#endif
 #pragma unroll 1
   for (int k = 0; k <= N; ++k) {
     real Pn[12], Kn[12], An[12], pvn = real(0.0), kvn = real(0.0), bvn = real(0.0);
@@ -289,7 +193,7 @@ __global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<r
       constexpr int J = decltype(j)::value;
       pp = fmadd(Pr[J], bx[J], pp);
     });
-    if (lane < nx) {
+    if (own) {
       xo[(size_t)k * nx + lane] = xv;
       po[(size_t)k * nx + lane] = pp;
     }
@@ -300,8 +204,8 @@ __global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<r
       uu = fmadd(Kr[J], bx[J], uu);
       xn = fmadd(Ar[J], bx[J], xn);
     });
-    if (lane < nu) uo[(size_t)k * nu + lane] = uu;
-    bad |= (lane < nu && !(uu == uu)) || (lane < nx && !(xn == xn));
+    if (own) uo[(size_t)k * nu + lane] = uu;
+    bad |= own && (!(uu == uu) || !(xn == xn));
     xv = xn;
     sfor<0, 12>([&](auto j) {
       constexpr int J = decltype(j)::value;
@@ -324,20 +228,78 @@ __global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<r
   }
 }
 
+// Large batches: 16 QPs per 256-thread workgroup, 2 workgroups per CU (the kernel needs
+// 217-223 VGPRs; memory-bound with the compute overlapped).
+__global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<real> a) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int qp = gid >> 4;
+  if (qp >= a.batch) return;
+  solve_qp(a, HbmSrc{a, qp}, qp, threadIdx.x & (kGroup - 1));
+}
+
+// Small batches: one QP per 64-thread workgroup.  All 64 lanes copy the QP into the LDS
+// image with 16-byte global->LDS DMA (one wave-instruction fills 1 KiB of the image; each
+// lane gathers its own 16 bytes from the QP-major buffers), then lanes 0-15 solve.
+constexpr int kRealsPerDma = 16 / (int)sizeof(real);
+
+__device__ __forceinline__ const real* img_source(const ProblemArgsT<real>& a, int qp, int e) {
+  const int N = a.N;
+  const int k = e / kImgStage, o = e - k * kImgStage;
+  const size_t s = (size_t)qp * N + k, s1 = (size_t)qp * (N + 1) + k;
+  if (o >= kImgQ && o < kImgS) return a.Q + s1 * 144 + (o - kImgQ);
+  if (o >= kImgq && o < kImgr) return a.q + s1 * 12 + (o - kImgq);
+  if (k >= N) return nullptr;  // slot N holds Q_N and q_N only
+  if (o < kImgB) return a.A + s * 144 + o;
+  if (o < kImgb) return a.B + s * 144 + (o - kImgB);
+  if (o < kImgQ) return a.b + s * 12 + (o - kImgb);
+  if (o < kImgR) return a.S + s * 144 + (o - kImgS);
+  if (o < kImgq) return a.R + s * 144 + (o - kImgR);
+  return a.r + s * 12 + (o - kImgr);
+}
+
+__global__ void __launch_bounds__(64, 1) riccati_unconstr_lds_kernel(ProblemArgsT<real> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  real* img = reinterpret_cast<real*>(lds_raw);
+  const int qp = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int total = (a.N + 1) * kImgStage;
+  for (int c0 = 0; c0 < total; c0 += 64 * kRealsPerDma) {
+    const int e = c0 + lane * kRealsPerDma;
+    const real* g = e < total ? img_source(a, qp, e) : nullptr;
+    if (g)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                       (__attribute__((address_space(3))) void*)(img + c0), 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (lane >= kGroup) return;
+  solve_qp(a, LdsSrc{img}, qp, lane);
+}
+
+size_t lds_image_bytes(int N) { return (size_t)(N + 1) * kImgStage * sizeof(real); }
+
 
 // KKT residuals and objective of an unconstrained solution: HPIPM's
 // d_ocp_qp_res_compute (hpipm_d_ocp_qp_res.h:57-67) for nc = 0, as the oracle's
 // compute_residuals states it (oracle/ocp_qp_oracle.c):
 //   res_stat = max( |R u + S x + r + B'pi_{k+1}| (k < N), |Q x + S'u + q + A'pi_{k+1} - pi_k| (k >= 1) )
 //   res_eq   = max |A x + B u + b - x_{k+1}|,   res_ineq = res_comp = 0,
-//   obj      = sum_k u'(R u / 2 + r) + x'(Q x / 2 + q) (k >= 1) + u'S x.
-// Run only when the caller asks for res / obj.  One 32-lane group per QP, lane l
-// takes stages l, l + 32, ...; any dims (padded problems are checked unpadded).
-constexpr int kResGroup = 32;
-__global__ void __launch_bounds__(256) unconstr_residuals_kernel(ProblemArgsT<real> a) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int qp = gid / kResGroup, lane = gid % kResGroup;
-  if (qp >= a.batch) return;
+//   obj      = sum_k u'(R u / 2 + r + S x) (k < N) + x'(Q x / 2 + q) (k >= 1).
+// Run only when the caller asks for res / obj / stat.  One 256-thread workgroup per QP,
+// thread t on (stage t / 12 (+21 j), row t % 12): every row's dot products are
+// independent, so a single QP (the reference's call pattern) costs a few memory latencies
+// rather than a serial walk over its stages.  Any dims (padded problems are checked
+// unpadded).
+constexpr int kResThreads = 256;
+constexpr int kResStages = kResThreads / 12;  // 21 stages per pass
+
+__device__ __forceinline__ void max_nan(real& m, real v) {
+  v = v < real(0) ? -v : v;
+  if (v > m || v != v) m = v;  // NaN propagates
+}
+
+__global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(ProblemArgsT<real> a) {
+  const int qp = blockIdx.x;
   const int N = a.N, nx = a.nx, nu = a.nu;
   const bool smaj = a.layout == 1;
   auto at = [&](const real* base, int nstage, size_t blk, int k) -> const real* {
@@ -347,70 +309,75 @@ __global__ void __launch_bounds__(256) unconstr_residuals_kernel(ProblemArgsT<re
   const real* x = a.x + (size_t)qp * (N + 1) * nx;
   const real* u = a.u + (size_t)qp * N * nu;
   const real* pi = a.pi + (size_t)qp * (N + 1) * nx;
-  auto upd = [](real& m, real v) {
-    v = v < real(0) ? -v : v;
-    if (v > m || v != v) m = v;  // NaN propagates
-  };
+  const int i = threadIdx.x % 12;
   real mg = real(0), mb = real(0), ob = real(0);
-  for (int k = lane; k <= N; k += kResGroup) {
+  for (int k = threadIdx.x / 12; threadIdx.x < kResStages * 12 && k <= N; k += kResStages) {
     const real* xk = x + (size_t)k * nx;
-    const real* Q = at(a.Q, N + 1, nxx, k);
-    const real* q = at(a.q, N + 1, nx, k);
-    real Sx[12];
-    for (int i = 0; i < 12; ++i) Sx[i] = real(0);
     if (k < N) {
       const real* uk = u + (size_t)k * nu;
       const real* xn = x + (size_t)(k + 1) * nx;
       const real* pn = pi + (size_t)(k + 1) * nx;
       const real* A = at(a.A, N, nxx, k);
       const real* B = at(a.B, N, nxu, k);
-      const real* b = at(a.b, N, nx, k);
-      const real* S = at(a.S, N, nxu, k);
-      const real* R = at(a.R, N, nuu, k);
-      const real* r = at(a.r, N, nu, k);
-      for (int i = 0; i < nu; ++i) {  // column-major blocks: M[i][j] = M[j * rows + i]
+      if (i < nu) {  // column-major blocks: M[i][j] = M[j * rows + i]
+        const real* S = at(a.S, N, nxu, k);
+        const real* R = at(a.R, N, nuu, k);
+        const real* r = at(a.r, N, nu, k);
         real ru = real(0), sx = real(0), bp = real(0);
         for (int j = 0; j < nu; ++j) ru += R[(size_t)j * nu + i] * uk[j];
         for (int j = 0; j < nx; ++j) sx += S[(size_t)j * nu + i] * xk[j];
         for (int j = 0; j < nx; ++j) bp += B[(size_t)i * nx + j] * pn[j];
-        Sx[i] = sx;
-        upd(mg, ru + sx + r[i] + bp);
-        ob += uk[i] * (real(0.5) * ru + r[i]) + (k == 0 ? uk[i] * sx : real(0));
+        max_nan(mg, ru + sx + r[i] + bp);
+        ob += uk[i] * (real(0.5) * ru + r[i] + sx);
       }
-      for (int i = 0; i < nx; ++i) {
+      if (i < nx) {
+        const real* b = at(a.b, N, nx, k);
         real v = b[i] - xn[i];
         for (int j = 0; j < nx; ++j) v += A[(size_t)j * nx + i] * xk[j];
         for (int j = 0; j < nu; ++j) v += B[(size_t)j * nx + i] * uk[j];
-        upd(mb, v);
+        max_nan(mb, v);
       }
     }
-    if (k > 0) {
-      const real* uk = u + (size_t)k * nu;
-      const real* pn = pi + (size_t)(k + 1) * nx;
-      const real* A = k < N ? at(a.A, N, nxx, k) : nullptr;
-      const real* S = k < N ? at(a.S, N, nxu, k) : nullptr;
-      for (int i = 0; i < nx; ++i) {
-        real qx = real(0), g = q[i] - pi[(size_t)k * nx + i];
-        for (int j = 0; j < nx; ++j) qx += Q[(size_t)j * nx + i] * xk[j];
-        g += qx;
-        if (k < N) {
-          for (int j = 0; j < nu; ++j) g += S[(size_t)i * nu + j] * uk[j];
-          for (int j = 0; j < nx; ++j) g += A[(size_t)i * nx + j] * pn[j];
-        }
-        upd(mg, g);
-        ob += xk[i] * (real(0.5) * qx + q[i]);
+    if (k > 0 && i < nx) {
+      const real* Q = at(a.Q, N + 1, nxx, k);
+      const real* q = at(a.q, N + 1, nx, k);
+      real qx = real(0), g = q[i] - pi[(size_t)k * nx + i];
+      for (int j = 0; j < nx; ++j) qx += Q[(size_t)j * nx + i] * xk[j];
+      g += qx;
+      if (k < N) {
+        const real* uk = u + (size_t)k * nu;
+        const real* pn = pi + (size_t)(k + 1) * nx;
+        const real* A = at(a.A, N, nxx, k);
+        const real* S = at(a.S, N, nxu, k);
+        for (int j = 0; j < nu; ++j) g += S[(size_t)i * nu + j] * uk[j];
+        for (int j = 0; j < nx; ++j) g += A[(size_t)i * nx + j] * pn[j];
       }
-      if (k < N)
-        for (int i = 0; i < nu; ++i) ob += uk[i] * Sx[i];
+      max_nan(mg, g);
+      ob += xk[i] * (real(0.5) * qx + q[i]);
     }
   }
-  for (int m = kResGroup / 2; m >= 1; m >>= 1) {
-    const real og = __shfl_xor(mg, m, kResGroup), obb = __shfl_xor(mb, m, kResGroup);
+  // workgroup reduction: max (NaN-propagating) of mg, mb; sum of ob
+  for (int m = 32; m >= 1; m >>= 1) {
+    const real og = __shfl_xor(mg, m), obb = __shfl_xor(mb, m);
     if (og > mg || og != og) mg = og;
     if (obb > mb || obb != obb) mb = obb;
-    ob += __shfl_xor(ob, m, kResGroup);
+    ob += __shfl_xor(ob, m);
   }
-  if (lane == 0) {
+  __shared__ real part[3][kResThreads / 64];
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) {
+    part[0][w] = mg;
+    part[1][w] = mb;
+    part[2][w] = ob;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mg = part[0][0], mb = part[1][0], ob = part[2][0];
+    for (int j = 1; j < kResThreads / 64; ++j) {
+      if (part[0][j] > mg || part[0][j] != part[0][j]) mg = part[0][j];
+      if (part[1][j] > mb || part[1][j] != part[1][j]) mb = part[1][j];
+      ob += part[2][j];
+    }
     if (a.res) {
       a.res[(size_t)qp * 4 + 0] = mg;
       a.res[(size_t)qp * 4 + 1] = mb;
@@ -430,24 +397,39 @@ __global__ void __launch_bounds__(256) unconstr_residuals_kernel(ProblemArgsT<re
 
 hipError_t launch_residuals(const ProblemArgsT<real>& a, hipStream_t stream) {
   if (a.batch <= 0) return hipSuccess;
-  const long long n = (long long)a.batch * kResGroup;
-  hipLaunchKernelGGL(unconstr_residuals_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     stream, a);
+  hipLaunchKernelGGL(unconstr_residuals_kernel, dim3((unsigned)a.batch), dim3(kResThreads), 0, stream, a);
   return hipGetLastError();
+}
+
+// QP-major batches of at most this many QPs (one per CU) take the LDS kernel when the
+// image fits a workgroup's LDS (fp64: N <= 26, fp32: N <= 53)
+constexpr int kLdsBatchMax = 256;
+constexpr size_t kLdsBytesMax = 160 * 1024;
+
+bool use_lds_kernel(const ProblemArgsT<real>& a) {
+  return a.layout == 0 && a.batch <= kLdsBatchMax && lds_image_bytes(a.N) <= kLdsBytesMax;
 }
 
 hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {
   if (a.batch <= 0) return hipSuccess;
+  // 12 x 12 stages only: smaller problems arrive embedded by pad.hip
+  if (a.nx != 12 || a.nu != 12) return hipErrorInvalidValue;
+  if (use_lds_kernel(a)) {
+    const size_t bytes = lds_image_bytes(a.N);
+    static bool attr_set = false;  // (same value for every N: the LDS cap)
+    if (!attr_set) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_unconstr_lds_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytesMax);
+      if (e != hipSuccess) return e;
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(riccati_unconstr_lds_kernel, dim3((unsigned)a.batch), dim3(64), bytes, stream, a);
+    return hipGetLastError();
+  }
   const int threads = 256;
   const long long lanes = (long long)a.batch * kGroup;
   const int blocks = (int)((lanes + threads - 1) / threads);
-  // 12 x 12 stages only: smaller problems arrive embedded by pad.hip
-  if (a.nx != 12 || a.nu != 12) return hipErrorInvalidValue;
-#ifndef SRBD_UNC_DYN_LDS
-#define SRBD_UNC_DYN_LDS 0
-#endif
-  // (A/B knob) dynamic LDS the kernel does not use, to cap workgroups per CU
-  hipLaunchKernelGGL(riccati_unconstr_kernel<true>, dim3(blocks), dim3(threads), SRBD_UNC_DYN_LDS, stream, a);
+  hipLaunchKernelGGL(riccati_unconstr_kernel, dim3(blocks), dim3(threads), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -198,3 +198,18 @@ def test_unconstrained_residuals_and_objective(pkg, oracle, case):
         assert np.all(ref["res"][:, j] <= 1e-12 * mag), (j, ref["res"][:, j] / mag)
     zero = pkg.capi.solve(qp, x0, dict(iter_max=30, compute_residuals=0))
     assert np.all(zero["res"] == 0) and np.all(zero["obj"] == 0)
+
+
+@pytest.mark.parametrize("dtype,N", [(np.float64, 20), (np.float64, 26), (np.float32, 40)])
+def test_latency_kernel_bit_identical(pkg, dtype, N):
+    """Batches of up to 256 QPs (QP-major, image within a workgroup's LDS) run on the
+    LDS latency kernel, larger ones on the streaming kernel: the same instructions on
+    the same values, so a QP's outputs are bit-identical either way -- also the
+    reference's batch of one."""
+    qp, x0 = pkg.srbd_model.generate_batch(300, N=N, seed=77, constraints="none")
+    big = pkg.capi.solve(qp, x0, None, riccati=True, dtype=dtype)       # streaming
+    for idx in (slice(0, 1), slice(100, 164), slice(44, 300)):          # LDS kernel
+        small = pkg.capi.solve(qp.subset(idx), x0[idx], None, riccati=True, dtype=dtype)
+        for key in ("x", "u", "pi", "P", "p", "K", "k", "status", "iter"):
+            assert np.array_equal(small[key], big[key][idx]), (key, idx)
+    assert np.all(big["status"] == 0)
