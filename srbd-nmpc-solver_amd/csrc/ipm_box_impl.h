@@ -542,8 +542,9 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     };
     for (int k = 0; k <= N && lane < kMaxDim; ++k) {
       const real* w = wb + (size_t)k * warm_w;
-      if (k < N) chk_bar(w + lane, c.side_u(k, lane));  // (no u_N)
-      chk_bar(w + 48 + lane, c.side_x(k, lane));
+      // only the bound families the problem has (an absent family's slots hold no state)
+      if (k < N && c.has_bars(0)) chk_bar(w + lane, c.side_u(k, lane));  // (no u_N)
+      if (c.has_bars(1)) chk_bar(w + 48 + lane, c.side_x(k, lane));
       for (int ch = 0; ch < c.nch; ++ch) chk_bar(w + 96 + ch * 48 + lane, c.side_g(k, ch, lane));
       if (k < N && uel) chk(c.u()[(size_t)k * nu + lane], false);
       if (k > 0 && xel) {
