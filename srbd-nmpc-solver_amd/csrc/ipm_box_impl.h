@@ -113,6 +113,15 @@ struct Side {
   real ml, mu;   // 1 if the lower / upper bound is active, else 0
 };
 
+// Barrier state of one variable / row from a warm-start buffer (p[0] lam_l, p[12] lam_u,
+// p[24] t_l, p[36] t_u): the stored values on active sides, the cold init's defaults
+// (lam 0, t 1) on inactive ones -- whatever the buffer holds there (an fp32 pass never
+// steps the state of a bound family the problem does not have) is not taken over.
+__device__ __forceinline__ Bar warm_bar(const real* p, const Side& s) {
+  const bool l = s.ml != real(0.0), u = s.mu != real(0.0);
+  return Bar{l ? p[0] : real(0.0), u ? p[12] : real(0.0), l ? p[24] : real(1.0), u ? p[36] : real(1.0)};
+}
+
 // The RB sweep's per-group LDS blocks (A, B, S: 3 x 144 reals per QP group).  One
 // function, so one allocation per kernel: the fused RB -> F1 kernel's F1 reuses them.
 __device__ __forceinline__ real* group_lds_blocks() {
@@ -531,20 +540,24 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   bool cont = false;
   if (wb) {
     int bad = 0;
-    // every t > 0; every lam >= 0, and > 0 on an active side (a multiplier that
-    // underflowed to 0 there would pin the fraction-to-boundary step at 0)
-    auto chk = [&](real v, bool pos) { bad |= !__builtin_isfinite(v) || (pos ? !(v > real(0.0)) : v < real(0.0)); };
+    // an active side needs a finite lam > 0 and t > 0 (a multiplier that underflowed to 0
+    // would pin the fraction-to-boundary step at 0); inactive sides and absent families
+    // are not read (warm_bar substitutes the cold defaults there)
+    auto chk = [&](real v, bool pos) { bad |= !__builtin_isfinite(v) || (pos && !(v > real(0.0))); };
     auto chk_bar = [&](const real* p, const Side& s) {
-      chk(p[0], s.ml != real(0.0));
-      chk(p[12], s.mu != real(0.0));
-      chk(p[24], true);
-      chk(p[36], true);
+      if (s.ml != real(0.0)) {
+        chk(p[0], true);
+        chk(p[24], true);
+      }
+      if (s.mu != real(0.0)) {
+        chk(p[12], true);
+        chk(p[36], true);
+      }
     };
     for (int k = 0; k <= N && lane < kMaxDim; ++k) {
       const real* w = wb + (size_t)k * warm_w;
-      // only the bound families the problem has (an absent family's slots hold no state)
-      if (k < N && c.has_bars(0)) chk_bar(w + lane, c.side_u(k, lane));  // (no u_N)
-      if (c.has_bars(1)) chk_bar(w + 48 + lane, c.side_x(k, lane));
+      if (k < N) chk_bar(w + lane, c.side_u(k, lane));  // (no u_N)
+      chk_bar(w + 48 + lane, c.side_x(k, lane));
       for (int ch = 0; ch < c.nch; ++ch) chk_bar(w + 96 + ch * 48 + lane, c.side_g(k, ch, lane));
       if (k < N && uel) chk(c.u()[(size_t)k * nu + lane], false);
       if (k > 0 && xel) {
@@ -559,12 +572,9 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       real* stk = c.st(k);
       const real* w = wb + (size_t)k * warm_w;
       if (lane < kMaxDim) {
-        for (int j = 4; j < 8; ++j) stk[kStLam + j * 12 + lane] = w[j * 12 + lane];
-        if (k < N) {
-          for (int j = 0; j < 4; ++j) stk[kStLam + j * 12 + lane] = w[j * 12 + lane];
-        } else {
-          store_bar(stk, 0, lane, Bar{real(0.0), real(0.0), real(1.0), real(1.0)});
-        }
+        store_bar(stk, 1, lane, warm_bar(w + 48 + lane, c.side_x(k, lane)));
+        store_bar(stk, 0, lane, k < N ? warm_bar(w + lane, c.side_u(k, lane))
+                                      : Bar{real(0.0), real(0.0), real(1.0), real(1.0)});
       }
       const real ui = (k < N && uel) ? c.u()[(size_t)k * nu + li] : real(0.0);
       real xi;
@@ -595,7 +605,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           ncl += s.ml + s.mu;
           if (lane < kMaxDim) {
             real* g = c.gs(k, ch);
-            for (int j = 0; j < 4; ++j) g[j * 12 + lane] = w[96 + ch * 48 + j * 12 + lane];
+            store_gbar(g, lane, warm_bar(w + 96 + ch * 48 + lane, s));
             store_gstep(g, lane, BarStep{0, 0, 0, 0});
             g[kGenVal + lane] = v;
           }
