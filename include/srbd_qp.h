@@ -134,7 +134,7 @@ typedef struct srbd_qp_settings {
   double reg_prim;
   int warm_start;   /* 1: x/u output buffers hold the primal warm start     */
   int pred_corr;
-  int ric_alg;      /* accepted; both values run the classical recursion   */
+  int ric_alg;      /* 0: classical Riccati; else the square-root recursion  */
   int split_step;
   int compute_residuals; /* unconstrained QPs (nc = 0): 1 (default) = res/obj, when
                           * given, hold the solution's KKT residual norms and

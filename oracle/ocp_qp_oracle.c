@@ -257,9 +257,15 @@ typedef struct {
   size_t hstride, gstride;
 } ric_ws_t;
 
-static int riccati_factor(const dims_t* d, ric_ws_t* w, double reg) {
+/* ric_alg = 0: the textbook recursion (test/ocp_qp_ipm_solver.cpp:67-90).
+ * ric_alg != 0: HPIPM's square-root variant (square_root_alg, hpipm-cpp default
+ * ocp_qp_ipm_solver_settings.hpp:81): with Lp = chol(P_{k+1}), the stage terms are
+ * sums of squares, G = R + (Lp'B)'(Lp'B), H = S + (Lp'B)'(Lp'A), F = Q + (Lp'A)'(Lp'A),
+ * and P_k = Lx Lx' with Lx = chol(F - H'G^-1 H) (the trailing factor of the
+ * stage's dsyrk_dpotrf); equal to the textbook P_k in exact arithmetic.        */
+static int riccati_factor(const dims_t* d, ric_ws_t* w, double reg, int sqrt_alg) {
   const int nx = d->nx, nu = d->nu, n = nx + nu, N = d->N;
-  double PA[32 * 32], PB[32 * 32], G[32 * 32], Hm[32 * 32], F[32 * 32];
+  double PA[32 * 32], PB[32 * 32], G[32 * 32], Hm[32 * 32], F[32 * 32], Lp[32 * 32];
   double* PN = w->P + (size_t)N * nx * nx;
   const double* HtN = w->Ht + (size_t)N * w->hstride;
   memcpy(PN, HtN, sizeof(double) * nx * nx);
@@ -268,11 +274,22 @@ static int riccati_factor(const dims_t* d, ric_ws_t* w, double reg) {
     const double* B = qB(d, k);
     const double* P1 = w->P + (size_t)(k + 1) * nx * nx;
     const double* Ht = w->Ht + (size_t)k * w->hstride;
-    mm(nx, nx, nx, P1, A, PA);
-    mm(nx, nu, nx, P1, B, PB);
-    mtm(nu, nu, nx, B, PB, G);
-    mtm(nu, nx, nx, B, PA, Hm);
-    mtm(nx, nx, nx, A, PA, F);
+    if (sqrt_alg) {
+      /* PA := Lp'A, PB := Lp'B; G = PB'PB, H = PB'PA, F = PA'PA */
+      memcpy(Lp, P1, sizeof(double) * nx * nx);
+      chol(nx, Lp);
+      mtm(nx, nx, nx, Lp, A, PA);
+      mtm(nx, nu, nx, Lp, B, PB);
+      mtm(nu, nu, nx, PB, PB, G);
+      mtm(nu, nx, nx, PB, PA, Hm);
+      mtm(nx, nx, nx, PA, PA, F);
+    } else {
+      mm(nx, nx, nx, P1, A, PA);
+      mm(nx, nu, nx, P1, B, PB);
+      mtm(nu, nu, nx, B, PB, G);
+      mtm(nu, nx, nx, B, PA, Hm);
+      mtm(nx, nx, nx, A, PA, F);
+    }
     for (int j = 0; j < nu; ++j)
       for (int i = 0; i < nu; ++i) M_(G, nu, i, j) += M_(Ht, n, i, j);
     for (int i = 0; i < nu; ++i) M_(G, nu, i, i) += reg;
@@ -304,6 +321,16 @@ static int riccati_factor(const dims_t* d, ric_ws_t* w, double reg) {
         double s = 0.5 * (M_(P, nx, i, j) + M_(P, nx, j, i));
         M_(P, nx, i, j) = s; M_(P, nx, j, i) = s;
       }
+    if (sqrt_alg) { /* P_k = Lx Lx' */
+      memcpy(Lp, P, sizeof(double) * nx * nx);
+      chol(nx, Lp);
+      for (int j = 0; j < nx; ++j)
+        for (int i = 0; i < nx; ++i) {
+          double s = 0.0;
+          for (int l = 0; l < nx; ++l) s += M_(Lp, nx, i, l) * M_(Lp, nx, j, l);
+          M_(P, nx, i, j) = s;
+        }
+    }
   }
   return 0;
 }
@@ -562,7 +589,7 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
      * (pinned by test/ocp_qp_ipm_solver.cpp:55-56)                   */
     for (int s = 0; s <= N; ++s) fill_stage_H(&d, s, w.Ht + s * w.hstride, w.gt + s * w.gstride);
     memcpy(w.bt, qp->b, sizeof(double) * N * nx);
-    if (riccati_factor(&d, &w, set->reg_prim)) { res->status = 3; rc = 0; goto done_nan; }
+    if (riccati_factor(&d, &w, set->reg_prim, set->ric_alg)) { res->status = 3; rc = 0; goto done_nan; }
     riccati_vectors(&d, &w);
     riccati_forward(&d, &w, x0, x, u, pi);
     compute_residuals(&d, st, x, u, pi, rg, rb, res->res, &res->obj, w.gstride);
@@ -650,7 +677,7 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
       }
       if (s < N) memcpy(w.bt + (size_t)s * nx, rb + (size_t)s * nx, sizeof(double) * nx);
     }
-    if (riccati_factor(&d, &w, set->reg_prim)) { res->status = 3; break; }
+    if (riccati_factor(&d, &w, set->reg_prim, set->ric_alg)) { res->status = 3; break; }
     riccati_vectors(&d, &w);
     riccati_forward(&d, &w, zero, dx, du, dpi);
 #ifdef ORACLE_DEBUG
@@ -819,7 +846,7 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
         row_syr(&d, rw, nu_k, G, Ht);
       }
     }
-    if (riccati_factor(&d, &w, set->reg_prim) != 0) res->status = 3;
+    if (riccati_factor(&d, &w, set->reg_prim, set->ric_alg) != 0) res->status = 3;
   }
   write_outputs(&d, &w, x, u, pi, P, p, K, k);
   goto done;

@@ -56,6 +56,8 @@ typedef struct oracle_settings {
   int iter_max;
   double alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp, reg_prim;
   int warm_start, pred_corr, split_step;
+  int ric_alg;  /* 0 classical Riccati; else square root: P_k = Lx Lx', with the
+                 * stage products formed from chol(P_{k+1}) (HPIPM square_root_alg) */
 } oracle_settings;
 
 typedef struct oracle_result {

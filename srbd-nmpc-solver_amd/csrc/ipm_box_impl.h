@@ -3,23 +3,6 @@
 // generates its d_ and s_ solvers from one source.  No include guard: included twice.
 // The kernel code is documented in ipm_box.hip.
 
-#ifndef SRBD_IPM_FUSE
-#define SRBD_IPM_FUSE 1
-#endif
-#ifndef SRBD_FWD_PREFETCH
-#define SRBD_FWD_PREFETCH 0
-#endif
-#ifndef SRBD_FWD_PREFETCH_F2
-#define SRBD_FWD_PREFETCH_F2 0
-#endif
-// 1: C-free general rows (GEN == 1): B2 takes the corrector's D'gamma as
-// D'gamma_pred + sigma mu D'e (RB) + D'z (F1) instead of re-reading D and the rows' state
-#ifndef SRBD_B2_GENVEC
-#define SRBD_B2_GENVEC 1
-#endif
-#ifndef SRBD_RB_ACC_LDS
-#define SRBD_RB_ACC_LDS 1
-#endif
 namespace srbd {
 namespace SRBD_NS {
 
@@ -149,14 +132,7 @@ struct Ctx {
     asm volatile("" : "+v"(v));
     return (size_t)v;
   }
-  // input QP index (diagnostic build only: every QP reads QP (qp & 63)'s data)
-  __device__ size_t iq() const {
-#ifdef SRBD_DIAG_SHARED_INPUT
-    return oq() & 63;
-#else
-    return oq();
-#endif
-  }
+  __device__ size_t iq() const { return oq(); }  // input QP index
   __device__ size_t sN() const { return iq() * N; }
   __device__ size_t sN1() const { return iq() * (N + 1); }
   __device__ size_t oN() const { return oq() * N; }
@@ -439,7 +415,10 @@ __device__ __forceinline__ void gather12(real v, real (&out)[12]) {
   });
 }
 
-template <bool FULL, int GEN, int PH>
+// SQRT (RB only): ric_alg = 1, the square-root factorization (riccati.h riccati_step_sqrt);
+// the factor record holds the same quantities (P_k = F - Y'Y, which Lx factors), so F1, B2
+// and F2 are shared.
+template <bool FULL, int GEN, int PH, bool SQRT = false>
 __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int qp = gid >> 4;
@@ -890,7 +869,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     // fp64 register file is at its limit: there they live in one LDS slot per lane
     // (box-u RB 68 B of scratch -> none, -2.4%); fp32 keeps them in registers (no
     // spills there, and the LDS round trips cost 1%).
-    constexpr bool kAccLds = SRBD_RB_ACC_LDS && sizeof(real) == 8;
+    constexpr bool kAccLds = sizeof(real) == 8;
     __shared__ real rb_acc[kAccLds ? 6 * 256 : 1];
     real acc_r[6];
     real& mg = kAccLds ? rb_acc[0 * 256 + threadIdx.x] : acc_r[0];
@@ -1003,7 +982,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           }
           rgu = dot_bcast(Dc, dl, rgu);
           gra = dot_bcast(Dc, gg, gra);
-          if constexpr (GEN == 1 && SRBD_B2_GENVEC) {
+          if constexpr (GEN == 1) {
             // gamma is affine in sigma mu: d gamma / d(sigma mu) = mu_row / t_u - ml / t_l
             real e = real(0.0);
             if (lane < kMaxDim) {
@@ -1058,7 +1037,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         gamma_of(su, bu, uk, real(0.0), real(0.0), real(0.0), Gu, gu);
         gamma_of(sx, bx, xk, real(0.0), real(0.0), real(0.0), Gx, gx);
       }
-      if constexpr (GEN == 1 && SRBD_B2_GENVEC) {
+      if constexpr (GEN == 1) {
         if (lane < kMaxDim) {
           real* v = c.gv(k);
           v[lane] = gra;
@@ -1106,6 +1085,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         });
         if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
         if (c.isv) store12(rec + kRecPv, P);
+        if constexpr (SQRT) sqrt_factor(P, lane);
       } else {
         // ---- A, B (kept by the factorization), S (kept in LDS): residual products ----
         real A_[12], B_[12];
@@ -1180,7 +1160,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           });
         };
         StageFactor<real> f;
-        riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
+        if constexpr (SQRT) {
+          riccati_step_sqrt(P, A_, B_, loadR, loadSQ, lane, reg, f);
+        } else {
+          riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
+        }
         if (lane < kMaxDim) {
           store_packed_col(rec + kRecL, lane, f.Lc);
           store12(rec + kRecK + lane * 12, f.Kc);
@@ -1197,6 +1181,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           constexpr int I = decltype(i)::value;
           P[I] = f.F[I];
         });
+        if constexpr (SQRT) sqrt_factor(P, lane);
         // the next stage overwrites this group's LDS blocks: reads done first
         lds_wave_fence();
       }
@@ -1266,7 +1251,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             gamma_of(sx, c.bar(stN, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, G, g);
           }
           pnext = lane < kMaxDim && xel ? stN[kStRes + 12 + lane] + g : real(0.0);
-          if constexpr (GEN == 2 || (GEN == 1 && !SRBD_B2_GENVEC)) {
+          if constexpr (GEN == 2) {
             // (C = NULL: the terminal stage has no general-row gradient, D_N is absent)
             real ra, qa;
             g_grad(N, true, sigma_mu, ra, qa);
@@ -1290,7 +1275,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           }
           real rt = lane < kMaxDim && uel ? stk[kStRes + lane] + gu : real(0.0);
           real qt = lane < kMaxDim && xel ? stk[kStRes + 12 + lane] + gx : real(0.0);
-          if constexpr (GEN == 1 && SRBD_B2_GENVEC) {
+          if constexpr (GEN == 1) {
             // D'gamma_corr = D'gamma_pred + sigma mu D'e + D'z (gamma is affine in both)
             if (lane < kMaxDim && uel) {
               const real* v = c.gv(k);
@@ -1361,11 +1346,6 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       ap = real(1e30);
       ad = real(1e30);
       real dxk = real(0.0);  // dx_0 = 0 (x0 fixed)
-      // The rows of K and Acl (and k, bcl) of stage k+1 are requested while stage k
-      // computes: they do not depend on dx, so each stage pays one latency less
-      // (F1 shares RB's register budget; F2 only with SRBD_FWD_PREFETCH_F2).
-      constexpr bool kPf = SRBD_FWD_PREFETCH && (!corr || SRBD_FWD_PREFETCH_F2);
-      real Kn[12], An[12], kn = real(0.0), bn = real(0.0);
       auto load_rows = [&](int k, real (&Kr)[12], real (&Ar)[12], real& kv, real& bv) {
         const real* rk = c.st(k) + par * kRecSize;
         sfor<0, 12>([&](auto j) {
@@ -1376,7 +1356,6 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         kv = rk[kRecKv + li];
         bv = rk[kRecBcl + li];
       };
-      if (kPf && N > 0) load_rows(0, Kn, An, kn, bn);
       for (int k = 0; k <= N; ++k) {
         real* stk = c.st(k);
         const real* rec = stk + par * kRecSize;
@@ -1390,18 +1369,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         real du = real(0.0), dxn = real(0.0);
         if (k < N) {
           real Kr[12], Ar[12];
-          if constexpr (kPf) {
-            sfor<0, 12>([&](auto j) {
-              constexpr int J = decltype(j)::value;
-              Kr[J] = Kn[J];
-              Ar[J] = An[J];
-            });
-            du = kn;
-            dxn = bn;
-            if (k + 1 < N) load_rows(k + 1, Kn, An, kn, bn);
-          } else {
-            load_rows(k, Kr, Ar, du, dxn);
-          }
+          load_rows(k, Kr, Ar, du, dxn);
           dot_bcast2(Kr, Ar, dxk, du, dxn);
         }
         if (!uel || k == N) du = real(0.0);
@@ -1413,7 +1381,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           // general rows: dv = C dx + D du, dt / dlam, step ratios
           // (GEN == 1, F1: z_i = ml dlam_l dt_l / t_l - mu dlam_u dt_u / t_u and D'z, the
           // predictor-product part of the corrector's D'gamma, for B2)
-          constexpr bool kZ = GEN == 1 && SRBD_B2_GENVEC && !corr;
+          constexpr bool kZ = GEN == 1 && !corr;
           real gza = real(0.0);
           for (int ch = 0; ch < c.nch; ++ch) {
             real* g = c.gs(k, ch);
@@ -1548,9 +1516,9 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 template <int GEN>
 constexpr int kIpmMinBlocks = sizeof(real) == 4 && GEN < 2 ? 3 : 2;
 
-template <bool FULL, int GEN, int PH>
+template <bool FULL, int GEN, int PH, bool SQRT = false>
 __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase_kernel(ProblemArgsT<real> a) {
-  ipm_phase<FULL, GEN, PH>(a);
+  ipm_phase<FULL, GEN, PH, SQRT>(a);
 }
 
 // Two consecutive sweeps of one iteration in one launch (RB -> F1, B2 -> F2):
@@ -1558,14 +1526,14 @@ __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase_
 // their records are still in L2 / the Infinity Cache, and the launch count halves.
 // The second phase re-reads the per-QP state the first one wrote (same wave:
 // visible after the workgroup-scope fence).
-template <bool FULL, int GEN, int PH1, int PH2>
+template <bool FULL, int GEN, int PH1, int PH2, bool SQRT = false>
 __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase2_kernel(ProblemArgsT<real> a) {
-  ipm_phase<FULL, GEN, PH1>(a);
+  ipm_phase<FULL, GEN, PH1, SQRT>(a);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  ipm_phase<FULL, GEN, PH2>(a);
+  ipm_phase<FULL, GEN, PH2, SQRT>(a);
 }
 
-template <bool FULL, int GEN>
+template <bool FULL, int GEN, bool SQRT>
 static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream) {
   const int threads = 256;
   const long long lanes = (long long)a.batch * kGroup;
@@ -1575,39 +1543,23 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
   // at the top of every later launch.  iter_max + 1 factorization sweeps at
   // most: the last one always decides (converged or MaxIterReached).
   hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhInit>), grid, block, 0, stream, a);
-#if SRBD_IPM_FUSE == 3
-  // (diagnostic schedule) RB and F1 as launches of their own, B2 -> F2 fused
-  for (int it = 0;; ++it) {
-    hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB>), grid, block, 0, stream, a);
-    if (it >= a.iter_max) break;
-    hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF1>), grid, block, 0, stream, a);
-    if (a.pred_corr)
-      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhB2, kPhF2>), grid, block, 0, stream, a);
-  }
-#elif SRBD_IPM_FUSE
   for (int it = 0;; ++it) {
     if (it >= a.iter_max) {
       if (!a.skip_last_rb)
-        hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB>), grid, block, 0, stream, a);
+        hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT>), grid, block, 0, stream, a);
       break;
     }
-    hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT>), grid, block, 0, stream, a);
     if (a.pred_corr)
       hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhB2, kPhF2>), grid, block, 0, stream, a);
   }
-#else
-  for (int it = 0;; ++it) {
-    hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB>), grid, block, 0, stream, a);
-    if (it >= a.iter_max) break;
-    hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF1>), grid, block, 0, stream, a);
-    if (a.pred_corr) {
-      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhB2>), grid, block, 0, stream, a);
-      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF2>), grid, block, 0, stream, a);
-    }
-  }
-#endif
   hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut>), grid, block, 0, stream, a);
   return hipGetLastError();
+}
+
+template <bool FULL, int GEN>
+static hipError_t launch_alg(const ProblemArgsT<real>& a, hipStream_t stream) {
+  return a.ric_alg ? launch_phases<FULL, GEN, true>(a, stream) : launch_phases<FULL, GEN, false>(a, stream);
 }
 
 hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {
@@ -1616,9 +1568,9 @@ hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {
   if (a.nx != 12 || a.nu != 12) return hipErrorInvalidValue;
   // general rows: GEN 2 with C, GEN 1 when C is absent (NULL = 0, e.g. the friction
   // cone, SRBD_model.cpp:237-260, which constrains u only)
-  if (a.ng > 0 && a.C) return launch_phases<true, 2>(a, stream);
-  if (a.ng > 0) return launch_phases<true, 1>(a, stream);
-  return launch_phases<true, 0>(a, stream);
+  if (a.ng > 0 && a.C) return launch_alg<true, 2>(a, stream);
+  if (a.ng > 0) return launch_alg<true, 1>(a, stream);
+  return launch_alg<true, 0>(a, stream);
 }
 
 }  // namespace SRBD_NS

@@ -42,6 +42,7 @@ struct ProblemArgsT {
   T reg;
   // IPM settings (hpipm-cpp OcpQpIpmSolverSettings semantics)
   int iter_max, pred_corr, split_step, warm_start;
+  int ric_alg;    // 0: classical Riccati, else the square-root recursion (riccati.h)
   int stat_rows;  // rows per QP of `stat` (the caller's iter_max + 2)
   // warm_start 2 only (internal: the fp64 continuation of srbd_qp_settings.f64_rescue):
   // per QP and stage the barrier state [kStLam block 96][nch chunks x 48], see ipm_box.hip

@@ -13,6 +13,11 @@
 // for one-column-per-lane.  A non-positive pivot zeroes its direction like
 // BLASFEO's dpotrf_l instead of producing NaN.
 //
+// Square-root Riccati (ric_alg = 1, hpipm-cpp's default,
+// ocp_qp_ipm_solver_settings.hpp:81; HPIPM's square_root_alg): the cost-to-go
+// travels as its Cholesky factor, P = Lp Lp', p = Lp s, so every Hessian term of
+// the stage is a sum of squares (riccati_step_sqrt below).
+//
 // The phases are ordered to keep the live register set at ~6 column arrays
 // (the arch-VGPR file is 256 x 32 bit per lane = 128 doubles): P is
 // broadcast twice (for WB, then for W) and B twice (for G, then for H)
@@ -20,6 +25,7 @@
 //
 // Register conventions inside a group (lane l, VL = 15):
 //   P[i]  : lane l < 12 -> P[i][l] (= P[l][i]); VL -> p[i]
+//           (square root: lane l -> Lp[i][l], zero above the diagonal; VL -> s[i])
 //   A_[i] : lane l < 12 -> A[i][l];             VL -> b[i]
 //   B_[i] : lane l < 12 -> B[i][l]              (VL: zeros)
 //   Rc[i] : R[i][l];  Sc[i]: S[i][l] (VL: r[i]);  Qc[i]: Q[i][l] (VL: q[i])
@@ -31,78 +37,32 @@
 // the previous phase (which blows the 256-VGPR budget).
 #define SRBD_PHASE_FENCE() __builtin_amdgcn_sched_barrier(0)
 
-// 1: the dense 12x12 products use the fused v_fmac_f64_dpp asm blocks
-// (qp_group.h); 0: compiler-generated v_mov_b64_dpp + v_fma_f64.
-#ifndef SRBD_FUSED_DPP
-#define SRBD_FUSED_DPP 1
-#endif
-// 1: K = -L^-T Y by column sweeps (12 independent updates per step) instead of
-// dot-product back substitution (a serial chain of up to 11 FMAs per step)
-#ifndef SRBD_TRSV_AXPY
-#define SRBD_TRSV_AXPY 1
-#endif
-// 1: Cholesky pivot reciprocals by v_rcp + two Newton steps instead of IEEE division
-#ifndef SRBD_FAST_RCP
-#define SRBD_FAST_RCP 0
-#endif
-
 namespace srbd {
 
-// C[:,l] = P M[:,l] (+ init): P symmetric & column-owned, M column-owned.
+// C[:,l] += P M[:,l]: P symmetric & column-owned, M column-owned (fused
+// v_fmac_*_dpp blocks of qp_group.h: the broadcast rides on the FMA).
 template <typename T>
 __device__ __forceinline__ void sym_mul_col(const T (&P)[12], const T (&M)[12], T (&C)[12]) {
-  if constexpr ((std::is_same_v<T, double> || std::is_same_v<T, float>) && SRBD_FUSED_DPP) {
-    sfor<0, 12>([&](auto kk) {
-      constexpr int K = decltype(kk)::value;
-      fma_bcast_src<K>(C, P, M[K]);
-    });
-  } else {
-    sfor<0, 12>([&](auto kk) {
-      constexpr int K = decltype(kk)::value;
-      sfor<0, 12>([&](auto i) {
-        constexpr int I = decltype(i)::value;
-        C[I] = fmadd(bc<K>(P[I]), M[K], C[I]);
-      });
-    });
-  }
+  sfor<0, 12>([&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    fma_bcast_src<K>(C, P, M[K]);
+  });
 }
 
 // C[i][l] += X[:,i]' Y[:,l] for i < 12 (X, Y column-owned)
 template <typename T>
 __device__ __forceinline__ void tmul_acc(const T (&X)[12], const T (&Y)[12], T (&C)[12]) {
-  if constexpr ((std::is_same_v<T, double> || std::is_same_v<T, float>) && SRBD_FUSED_DPP) {
-    sfor<0, 12>([&](auto kk) {
-      constexpr int K = decltype(kk)::value;
-      fma_bcast_lanes(C, X[K], Y[K]);
-    });
-  } else {
-    sfor<0, 12>([&](auto i) {
-      constexpr int I = decltype(i)::value;
-      sfor<0, 12>([&](auto kk) {
-        constexpr int K = decltype(kk)::value;
-        C[I] = fmadd(bc<I>(X[K]), Y[K], C[I]);
-      });
-    });
-  }
+  sfor<0, 12>([&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    fma_bcast_lanes(C, X[K], Y[K]);
+  });
 }
 
 // Right-looking Cholesky of the column-owned symmetric G (lane l holds
 // G[:,l]); `reg` is added to each pivot.  On exit Lc holds column l of L
 // (rows > l meaningful) and rs = 1 / L[l][l] (0 for a non-positive pivot).
-template <typename T>
-__device__ __forceinline__ T pivot_inv(T d) {
-#if SRBD_FAST_RCP
-  if constexpr (std::is_same_v<T, double>) {
-    double r = __builtin_amdgcn_rcp(d);
-    double e = __builtin_fma(-d, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    e = __builtin_fma(-d, r, 1.0);
-    return __builtin_fma(r, e, r);
-  }
-#endif
-  return T(1) / d;
-}
-
+// A lane past the last column (VL) is eliminated as a border column: with G
+// holding a vector v there, Lc[i] * bc<i>(rs) = (L^-1 v)[i] on exit.
 template <typename T>
 __device__ __forceinline__ void chol_cols(T (&G)[12], const int lane, const T reg, T (&Lc)[12],
                                           T& rs) {
@@ -110,7 +70,7 @@ __device__ __forceinline__ void chol_cols(T (&G)[12], const int lane, const T re
   sfor<0, 12>([&](auto kk) {
     constexpr int K = decltype(kk)::value;
     const T dk = bc<K>(G[K]) + reg;
-    const T inv = dk > T(0) ? pivot_inv(dk) : T(0);
+    const T inv = dk > T(0) ? T(1) / dk : T(0);
     const T s = lane > K ? G[K] * inv : T(0);
     sfor<K + 1, 12>([&](auto i) {
       constexpr int I = decltype(i)::value;
@@ -139,23 +99,9 @@ __device__ __forceinline__ void trsv_lower(const T (&Lc)[12], const T rs, T (&H)
   });
 }
 
-// z = L^-T y (column-owned right-hand sides), dot-product back substitution.
-template <typename T>
-__device__ __forceinline__ void trsv_upper_t(const T (&Lc)[12], const T rs, const T (&y)[12],
-                                             T (&z)[12]) {
-  sfor_down<0, 12>([&](auto kk) {
-    constexpr int K = decltype(kk)::value;
-    T s = y[K];
-    sfor<K + 1, 12>([&](auto i) {
-      constexpr int I = decltype(i)::value;
-      s = fmadd(-bc<K>(Lc[I]), z[I], s);
-    });
-    z[K] = s * bc<K>(rs);
-  });
-}
-
 // Kc = -L^-T y by column sweeps: for K = 11..0: z_K = y_K / L_KK, then
-// y_I -= L_KI z_K for I < K (L_KI = lane I's column, row K).  y is kept.
+// y_I -= L_KI z_K for I < K (L_KI = lane I's column, row K): 12 independent
+// updates per step instead of a serial dot-product chain.  y is kept.
 template <typename T>
 __device__ __forceinline__ void trsv_upper_t_neg_axpy(const T (&Lc)[12], const T rs,
                                                       const T (&y)[12], T (&Kc)[12]) {
@@ -182,14 +128,46 @@ struct StageFactor {
   T Kc[12];  // K column (VL: k)
 };
 
-// One backward Riccati step.  `P` holds P_{k+1} (VL: p_{k+1}) on entry.
-// A_ is overwritten with the closed-loop column Acl (VL: bcl) on exit.
-// The S/Q/R columns are fetched through the callables so that their loads
-// are issued late (short live ranges).
 struct NoMid {
   __device__ __forceinline__ void operator()() const {}
 };
 
+// The common tail of both step variants: given L = chol(G) and the column-owned
+// H (VL: g) and F (VL: f) of the stage,
+//   Y = L^-1 H, K = -L^-T Y, P_k = F - Y'Y (VL: p_k = f - Y'y), Acl = A + B K.
+// `mid` runs before the triangular solves (MidAt = 1) or after them (MidAt = 2).
+template <int MidAt, typename T, typename Mid>
+__device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], StageFactor<T>& o, Mid&& mid) {
+  if constexpr (MidAt == 1) {
+    mid();
+    SRBD_PHASE_FENCE();
+  }
+  // ---- Y = L^-1 H, K = -L^-T Y
+  trsv_lower(o.Lc, o.rs, o.H);
+  SRBD_PHASE_FENCE();
+  launder(o.Lc);
+  trsv_upper_t_neg_axpy(o.Lc, o.rs, o.H, o.Kc);
+  SRBD_PHASE_FENCE();
+  if constexpr (MidAt == 2) {
+    mid();
+    SRBD_PHASE_FENCE();
+  }
+  // ---- P_k = F - Y'Y (VL: p_k = f - Y'y)
+  {
+    T Hn[12];
+    sfor<0, 12>([&](auto i) { Hn[decltype(i)::value] = -o.H[decltype(i)::value]; });
+    tmul_acc(o.H, Hn, o.F);
+  }
+  SRBD_PHASE_FENCE();
+  // ---- Acl = A + B K (VL: bcl = b + B k)
+  launder(B_);
+  sym_mul_col(B_, o.Kc, A_);  // A[i][l] += B[i][m] K[m][l]: bc<m>(B_[i]) * Kc[m]
+}
+
+// One backward Riccati step.  `P` holds P_{k+1} (VL: p_{k+1}) on entry.
+// A_ is overwritten with the closed-loop column Acl (VL: bcl) on exit.
+// The S/Q/R columns are fetched through the callables so that their loads
+// are issued late (short live ranges).
 // `mid` runs between the products and the triangular solves (MidAt = 1: P is
 // dead there) or after the solves (MidAt = 2: L is dead too): the caller may
 // issue the next stage's loads into registers of its own.
@@ -234,41 +212,66 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
     tmul_acc(A_, W, o.F);
   }
   SRBD_PHASE_FENCE();
-  if constexpr (MidAt == 1) {
-    mid();
-    SRBD_PHASE_FENCE();
-  }
-  // ---- Y = L^-1 H, K = -L^-T Y
-  trsv_lower(o.Lc, o.rs, o.H);
+  riccati_tail<MidAt>(A_, B_, o, mid);
+}
+
+// Square-root step (ric_alg = 1).  `Lp` holds the factor of P_{k+1} (lane l: column l,
+// zero above the diagonal; VL: s_{k+1} with p_{k+1} = Lp s_{k+1}) on entry:
+//   MB = Lp'B,  MA = Lp'A,  m = Lp'b + s
+//   G = R + MB'MB,  H = S + MB'MA,  F = Q + MA'MA,  g = r + MB'm,  f = q + MA'm
+// -- in exact arithmetic the classical B'PB, B'PA, A'PA, B'(Pb + p), A'(Pb + p) --
+// then the common tail.  The caller continues the recursion with sqrt_factor(P_k).
+template <int MidAt = 1, typename T, typename LoadR, typename LoadSQ, typename Mid = NoMid>
+__device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12], T (&B_)[12],
+                                                  LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
+                                                  const T reg, StageFactor<T>& o, Mid&& mid = Mid{}) {
+  const bool isv = lane == kVecLane;
+  // ---- MB = Lp'B (VL: 0, its B_ column is 0); G = R + MB'MB, L = chol(G)
+  T MB[12];
+  sfor<0, 12>([&](auto i) { MB[decltype(i)::value] = T(0); });
+  tmul_acc(Lp, B_, MB);
   SRBD_PHASE_FENCE();
-  launder(o.Lc);
-#if SRBD_TRSV_AXPY
-  trsv_upper_t_neg_axpy(o.Lc, o.rs, o.H, o.Kc);
-#else
   {
-    T z[12];
-    trsv_upper_t(o.Lc, o.rs, o.H, z);
+    T G[12];
+    loadR(G);
+    tmul_acc(MB, MB, G);
+    SRBD_PHASE_FENCE();
+    chol_cols(G, lane, reg, o.Lc, o.rs);
+  }
+  SRBD_PHASE_FENCE();
+  // ---- MA = Lp'[A | b] + [0 | s]; H = S + MB'MA; F = Q + MA'MA
+  {
+    T MA[12];
     sfor<0, 12>([&](auto i) {
       constexpr int I = decltype(i)::value;
-      o.Kc[I] = -z[I];
+      MA[I] = isv ? Lp[I] : T(0);
     });
-  }
-#endif
-  SRBD_PHASE_FENCE();
-  if constexpr (MidAt == 2) {
-    mid();
+    tmul_acc(Lp, A_, MA);
     SRBD_PHASE_FENCE();
-  }
-  // ---- P_k = F - Y'Y (VL: p_k = f - Y'y)
-  {
-    T Hn[12];
-    sfor<0, 12>([&](auto i) { Hn[decltype(i)::value] = -o.H[decltype(i)::value]; });
-    tmul_acc(o.H, Hn, o.F);
+    loadSQ(o.H, o.F);
+    tmul_acc(MB, MA, o.H);
+    SRBD_PHASE_FENCE();
+    tmul_acc(MA, MA, o.F);
   }
   SRBD_PHASE_FENCE();
-  // ---- Acl = A + B K (VL: bcl = b + B k)
-  launder(B_);
-  sym_mul_col(B_, o.Kc, A_);  // A[i][l] += B[i][m] K[m][l]: bc<m>(B_[i]) * Kc[m]
+  riccati_tail<MidAt>(A_, B_, o, mid);
+}
+
+// P (lane l: column l of P_k; VL: p_k) -> its square-root form for the next
+// riccati_step_sqrt: Lp = chol(P) (column l, zeros above the diagonal) and, on VL,
+// s = Lp^-1 p (the border column of the same elimination).  A non-positive pivot
+// zeroes its column and its s entry (BLASFEO dpotrf_l), like chol_cols.
+template <typename T>
+__device__ __forceinline__ void sqrt_factor(T (&P)[12], const int lane) {
+  T rs;
+  chol_cols(P, lane, T(0), P, rs);
+  const bool isv = lane == kVecLane;
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    const T ri = bc<I>(rs);
+    if (isv) P[I] *= ri;
+    else if (lane > I) P[I] = T(0);
+  });
 }
 
 }  // namespace srbd

@@ -75,7 +75,9 @@ struct LdsSrc {
 };
 
 // ---- the solve of one QP by its 16-lane group ----
-template <class Src>
+// SQRT: ric_alg = 1, the square-root recursion (riccati.h riccati_step_sqrt); the records
+// and outputs are the same (P_k = F - Y'Y of the stage, which Lx factors).
+template <bool SQRT, class Src>
 __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src& src, const int qp,
                                          const int lane) {
   constexpr int nx = 12, nu = 12;
@@ -100,6 +102,7 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
     if (a.P && own) store_n(a.P + ((size_t)qp * (N + 1) + N) * nxx + (size_t)lane * nx, nx, P);
     if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + N) * nx, nx, P);
   }
+  if constexpr (SQRT) sqrt_factor(P, lane);
 
   // ---------------- backward sweep ----------------
   real A_[12], B_[12];
@@ -130,7 +133,11 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
       }
     };
     StageFactor<real> f;
-    riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
+    if constexpr (SQRT) {
+      riccati_step_sqrt(P, A_, B_, loadR, loadSQ, lane, reg, f);
+    } else {
+      riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
+    }
 
     real* rec = src.rec(k);
     if (own) {
@@ -154,6 +161,7 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
       constexpr int I = decltype(i)::value;
       P[I] = f.F[I];
     });
+    if constexpr (SQRT) sqrt_factor(P, lane);
   }
 
   // ---------------- forward sweep (row-owned) ----------------
@@ -230,11 +238,12 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
 
 // Large batches: 16 QPs per 256-thread workgroup, 2 workgroups per CU (the kernel needs
 // 217-223 VGPRs; memory-bound with the compute overlapped).
+template <bool SQRT>
 __global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<real> a) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int qp = gid >> 4;
   if (qp >= a.batch) return;
-  solve_qp(a, HbmSrc{a, qp}, qp, threadIdx.x & (kGroup - 1));
+  solve_qp<SQRT>(a, HbmSrc{a, qp}, qp, threadIdx.x & (kGroup - 1));
 }
 
 // Small batches: one QP per 64-thread workgroup.  All 64 lanes copy the QP into the LDS
@@ -257,6 +266,7 @@ __device__ __forceinline__ const real* img_source(const ProblemArgsT<real>& a, i
   return a.r + s * 12 + (o - kImgr);
 }
 
+template <bool SQRT>
 __global__ void __launch_bounds__(64, 1) riccati_unconstr_lds_kernel(ProblemArgsT<real> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   real* img = reinterpret_cast<real*>(lds_raw);
@@ -273,7 +283,7 @@ __global__ void __launch_bounds__(64, 1) riccati_unconstr_lds_kernel(ProblemArgs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (lane >= kGroup) return;
-  solve_qp(a, LdsSrc{img}, qp, lane);
+  solve_qp<SQRT>(a, LdsSrc{img}, qp, lane);
 }
 
 size_t lds_image_bytes(int N) { return (size_t)(N + 1) * kImgStage * sizeof(real); }
@@ -410,27 +420,32 @@ bool use_lds_kernel(const ProblemArgsT<real>& a) {
   return a.layout == 0 && a.batch <= kLdsBatchMax && lds_image_bytes(a.N) <= kLdsBytesMax;
 }
 
-hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {
-  if (a.batch <= 0) return hipSuccess;
-  // 12 x 12 stages only: smaller problems arrive embedded by pad.hip
-  if (a.nx != 12 || a.nu != 12) return hipErrorInvalidValue;
+template <bool SQRT>
+static hipError_t launch_alg(const ProblemArgsT<real>& a, hipStream_t stream) {
   if (use_lds_kernel(a)) {
     const size_t bytes = lds_image_bytes(a.N);
     static bool attr_set = false;  // (same value for every N: the LDS cap)
     if (!attr_set) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_unconstr_lds_kernel),
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_unconstr_lds_kernel<SQRT>),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytesMax);
       if (e != hipSuccess) return e;
       attr_set = true;
     }
-    hipLaunchKernelGGL(riccati_unconstr_lds_kernel, dim3((unsigned)a.batch), dim3(64), bytes, stream, a);
+    hipLaunchKernelGGL(riccati_unconstr_lds_kernel<SQRT>, dim3((unsigned)a.batch), dim3(64), bytes, stream, a);
     return hipGetLastError();
   }
   const int threads = 256;
   const long long lanes = (long long)a.batch * kGroup;
   const int blocks = (int)((lanes + threads - 1) / threads);
-  hipLaunchKernelGGL(riccati_unconstr_kernel, dim3(blocks), dim3(threads), 0, stream, a);
+  hipLaunchKernelGGL(riccati_unconstr_kernel<SQRT>, dim3(blocks), dim3(threads), 0, stream, a);
   return hipGetLastError();
+}
+
+hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {
+  if (a.batch <= 0) return hipSuccess;
+  // 12 x 12 stages only: smaller problems arrive embedded by pad.hip
+  if (a.nx != 12 || a.nu != 12) return hipErrorInvalidValue;
+  return a.ric_alg ? launch_alg<true>(a, stream) : launch_alg<false>(a, stream);
 }
 
 }  // namespace SRBD_NS

@@ -307,6 +307,7 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   if (rescue && st->f64_rescue < a.iter_max) a.iter_max = st->f64_rescue;
   a.pred_corr = st->pred_corr;
   a.split_step = st->split_step;
+  a.ric_alg = st->ric_alg != 0;  // HPIPM: any nonzero square_root_alg
   a.warm_start = st->warm_start;
   a.alpha_min = st->alpha_min;
   a.mu0 = st->mu0;

@@ -14,9 +14,10 @@ import helpers
 pytestmark = pytest.mark.gpu
 
 
-def test_compare_results_osqp_golden(pkg):
+@pytest.mark.parametrize("ric_alg", [0, 1])
+def test_compare_results_osqp_golden(pkg, ric_alg):
     qp, d, goldens, A, B, b = helpers.quadcopter(pkg.OcpQpBatch)
-    st = dict(d["settings"])
+    st = dict(d["settings"], ric_alg=ric_alg)
     N, nx, nu = qp.N, qp.nx, qp.nu
     x = np.zeros(nx)
     xw = np.zeros((1, N + 1, nx))
@@ -52,11 +53,12 @@ def test_compare_results_batched(pkg, oracle):
         assert helpers.is_approx(cat, goldens[t], 1e-9), t
 
 
+@pytest.mark.parametrize("ric_alg", [0, 1])
 @pytest.mark.parametrize("dims", [(5, 3), (12, 12), (12, 4)])
-def test_constrained_vs_oracle(pkg, oracle, dims):
+def test_constrained_vs_oracle(pkg, oracle, dims, ric_alg):
     nx, nu = dims
     qp, x0 = helpers.random_constrained(24, 15, nx, nu, 0, 17 + nx, pkg.OcpQpBatch)
-    st = dict(iter_max=40, mode="Balance")
+    st = dict(iter_max=40, mode="Balance", ric_alg=ric_alg)
     out = pkg.capi.solve(qp, x0, st, riccati=True)
     ref = oracle.solve(qp, st, x0=x0)
     assert np.all(out["status"] == 0), (out["status"], out["res"])
@@ -194,11 +196,12 @@ def test_masked_general_rows_are_absent(pkg):
         np.testing.assert_allclose(out[key], ref[key], rtol=0, atol=1e-12 * np.abs(ref[key]).max())
 
 
-def test_srbd_friction_cone_vs_oracle(pkg, oracle):
+@pytest.mark.parametrize("ric_alg", [0, 1])
+def test_srbd_friction_cone_vs_oracle(pkg, oracle, ric_alg):
     """BASELINE config 5's constraint set: 24 friction-cone rows on du per stage
     (SRBD_model.cpp:237-260 as linear inequalities), N = 20."""
     qp, x0 = pkg.srbd_model.generate_batch(24, N=20, seed=12, constraints="cone")
-    st = dict(iter_max=40)
+    st = dict(iter_max=40, ric_alg=ric_alg)
     out = pkg.capi.solve(qp, x0, st)
     ref = oracle.solve(qp, st, x0=x0)
     assert np.all(ref["status"] == 0), ref["status"]

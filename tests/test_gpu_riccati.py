@@ -28,17 +28,20 @@ def _assert_riccati_matches(qp, x0, out, prec=1e-10, qps=None):
                 assert helpers.is_approx(k[j], out["k"][i, j], prec), (i, j, "k")
 
 
-def test_reference_unconstrained_dims(pkg):
-    """nx=5, nu=3, N=20 exactly as the reference test (padded path)."""
+@pytest.mark.parametrize("ric_alg", [0, 1])
+def test_reference_unconstrained_dims(pkg, ric_alg):
+    """nx=5, nu=3, N=20 exactly as the reference test (padded path); both Riccati
+    variants (1, the square root, is hpipm-cpp's default)."""
     qp, x0 = helpers.random_unconstrained(37, 20, 5, 3, 1, pkg.OcpQpBatch)
-    out = pkg.capi.solve(qp, x0, {"mode": "Balance"}, riccati=True)
+    out = pkg.capi.solve(qp, x0, {"mode": "Balance", "ric_alg": ric_alg}, riccati=True)
     assert np.all(out["status"] == 0) and np.all(out["iter"] == 0)
     assert np.all(out["x"][:, 0] == x0)
     _assert_riccati_matches(qp, x0, out)
 
 
+@pytest.mark.parametrize("ric_alg", [0, 1])
 @pytest.mark.parametrize("N", [1, 10, 20, 40])
-def test_full_12x12_fast_path(pkg, N):
+def test_full_12x12_fast_path(pkg, N, ric_alg):
     qp, x0 = helpers.random_unconstrained(67, N, 12, 12, 100 + N, pkg.OcpQpBatch)
     if N > 10:
         # random 12x12 A has spectral radius ~2: over 20+ stages P grows like
@@ -46,7 +49,7 @@ def test_full_12x12_fast_path(pkg, N):
         # implementation (numpy included).  Keep the long horizons well-posed.
         rho = np.max(np.abs(np.linalg.eigvals(qp.A)), axis=-1)
         qp.A = qp.A / rho[..., None, None]
-    out = pkg.capi.solve(qp, x0, None, riccati=True)
+    out = pkg.capi.solve(qp, x0, dict(ric_alg=ric_alg), riccati=True)
     assert np.all(out["status"] == 0)
     _assert_riccati_matches(qp, x0, out, prec=1e-9, qps=range(0, 67, 11))
 
@@ -106,12 +109,15 @@ def test_host_entry_point_matches_device(pkg):
     assert np.all(st == 0)
 
 
-def test_srbd_qps_vs_oracle(pkg, oracle):
-    """The reference's own QP: SRBD NMPC linearisation (N=20, nx=nu=12)."""
+@pytest.mark.parametrize("ric_alg", [0, 1])
+def test_srbd_qps_vs_oracle(pkg, oracle, ric_alg):
+    """The reference's own QP: SRBD NMPC linearisation (N=20, nx=nu=12); its Q has
+    zero weights, so the square-root variant meets singular P_N (zero pivots)."""
     gen = pkg.srbd_model
     qp, x0 = gen.generate_batch(24, N=20, seed=2024)
-    out = pkg.capi.solve(qp, x0, None, riccati=True)
-    ref = oracle.solve(qp, None, x0=x0)
+    st = dict(ric_alg=ric_alg)
+    out = pkg.capi.solve(qp, x0, st, riccati=True)
+    ref = oracle.solve(qp, st, x0=x0)
     assert np.all(out["status"] == 0)
     for key in ("x", "u", "pi", "P", "K"):
         for i in range(qp.batch):
@@ -200,16 +206,18 @@ def test_unconstrained_residuals_and_objective(pkg, oracle, case):
     assert np.all(zero["res"] == 0) and np.all(zero["obj"] == 0)
 
 
+@pytest.mark.parametrize("ric_alg", [0, 1])
 @pytest.mark.parametrize("dtype,N", [(np.float64, 20), (np.float64, 26), (np.float32, 40)])
-def test_latency_kernel_bit_identical(pkg, dtype, N):
+def test_latency_kernel_bit_identical(pkg, dtype, N, ric_alg):
     """Batches of up to 256 QPs (QP-major, image within a workgroup's LDS) run on the
     LDS latency kernel, larger ones on the streaming kernel: the same instructions on
     the same values, so a QP's outputs are bit-identical either way -- also the
     reference's batch of one."""
     qp, x0 = pkg.srbd_model.generate_batch(300, N=N, seed=77, constraints="none")
-    big = pkg.capi.solve(qp, x0, None, riccati=True, dtype=dtype)       # streaming
+    st = dict(ric_alg=ric_alg)
+    big = pkg.capi.solve(qp, x0, st, riccati=True, dtype=dtype)         # streaming
     for idx in (slice(0, 1), slice(100, 164), slice(44, 300)):          # LDS kernel
-        small = pkg.capi.solve(qp.subset(idx), x0[idx], None, riccati=True, dtype=dtype)
+        small = pkg.capi.solve(qp.subset(idx), x0[idx], st, riccati=True, dtype=dtype)
         for key in ("x", "u", "pi", "P", "p", "K", "k", "status", "iter"):
             assert np.array_equal(small[key], big[key][idx]), (key, idx)
     assert np.all(big["status"] == 0)

@@ -15,10 +15,13 @@ import pytest
 import helpers
 
 
-def test_unconstrained_textbook(OcpQpBatch, oracle):
+@pytest.mark.parametrize("ric_alg", [0, 1])
+def test_unconstrained_textbook(OcpQpBatch, oracle, ric_alg):
+    """Both Riccati variants (ric_alg 0: classical, 1: square root, the hpipm-cpp
+    default) against the reference test's textbook recursion."""
     for seed in range(4):
         qp, x0 = helpers.random_unconstrained(1, 20, 5, 3, seed, OcpQpBatch)
-        out = oracle.solve(qp, dict(iter_max=15), x0=x0)
+        out = oracle.solve(qp, dict(iter_max=15, ric_alg=ric_alg), x0=x0)
         assert out["status"][0] == 0
         assert out["iter"][0] == 0
         x, u, lmd, P, s, K, k = helpers.textbook_riccati(qp, x0[0])
@@ -48,10 +51,12 @@ def test_unconstrained_dense_kkt(OcpQpBatch, oracle, dims):
         assert out["res"][i, 0] < 1e-9 and out["res"][i, 1] < 1e-9
 
 
-def test_compare_results_osqp_golden(OcpQpBatch, oracle):
-    """test/ocp_qp_ipm_solver.cpp:170-315 against sol{t}.txt."""
+@pytest.mark.parametrize("ric_alg", [0, 1])
+def test_compare_results_osqp_golden(OcpQpBatch, oracle, ric_alg):
+    """test/ocp_qp_ipm_solver.cpp:170-315 against sol{t}.txt (the reference runs it at
+    ric_alg 0; the square-root variant must land on the same goldens)."""
     qp, d, goldens, A, B, b = helpers.quadcopter(OcpQpBatch)
-    st = dict(d["settings"])
+    st = dict(d["settings"], ric_alg=ric_alg)
     N, nx, nu = qp.N, qp.nx, qp.nu
     x = np.zeros(nx)
     xw = np.zeros((1, N + 1, nx))
