@@ -151,17 +151,22 @@ typedef struct srbd_qp_settings {
                      * obj, stat) are the fp64 solve's, narrowed.  The call
                      * then waits for the fp32 pass (it counts the QPs to
                      * re-solve on the host).                               */
-  int f32_iters;    /* fp64 solves with constraints on 12 x 12 stages only
-                     * (ignored otherwise): 0 (default) = fp64 throughout;
-                     * n > 0 = a mixed-precision IPM: the data is narrowed
-                     * once to fp32, the first min(n, iter_max) iterations run
-                     * in fp32 (half the bytes per sweep), and the fp64 IPM
-                     * continues from that iterate (x, u, pi, lam, t) on the
-                     * caller's fp64 data to the fp64 tolerances; iter and stat
-                     * count the fp64 iterations.  A QP the continuation leaves
-                     * unsolved is solved again cold in fp64 (its outputs are
-                     * then the fp64 path's); the call waits once to count
-                     * them.                                                */
+  int f32_iters;    /* fp64 solves with constraints on 12 x 12 stages and
+                     * iter_max >= 2 only (ignored otherwise): 0 (default) =
+                     * fp64 throughout; n > 0 = a mixed-precision IPM: the data
+                     * is narrowed once to fp32, the first m = min(n,
+                     * iter_max - 1) iterations run in fp32 (half the bytes per
+                     * sweep), and the fp64 IPM continues from that iterate (x,
+                     * u, pi, lam, t) on the caller's fp64 data to the fp64
+                     * tolerances for at most iter_max - m iterations, so the
+                     * iteration budget stays iter_max; iter and stat count the
+                     * fp64 iterations.  A QP the continuation ends with
+                     * MinStepLengthReached or NaNDetected (a numerical
+                     * breakdown) is solved again cold in fp64, iter_max
+                     * iterations, and then carries the fp64 path's outputs; the
+                     * call waits once to count them.  Worst case per QP: iter_max
+                     * iterations (m fp32) plus, for a breakdown only, iter_max
+                     * fp64 ones.                                           */
 } srbd_qp_settings;
 
 typedef struct srbd_qp_data_f64 {

@@ -123,9 +123,10 @@ hipError_t launch_srbd_linearize(const srbd_model_params& p, int batch, int N, i
                                  const double* xs, const double* us,
                                  const srbd_qp_data_f64& out, hipStream_t stream);
 
-// rescue.hip (srbd_qp_settings.f64_rescue): list the QPs with status != 0 in batch
-// order, widen / narrow QP-major rows of `elems` values between fp32 and fp64
-hipError_t launch_select_unsolved(const int* status, int batch, int* idx, int* count, hipStream_t s);
+// rescue.hip (srbd_qp_settings.f64_rescue / f32_iters): list the QPs with status >=
+// min_status in batch order, widen / narrow QP-major rows of `elems` values between fp32 and fp64
+hipError_t launch_select_unsolved(const int* status, int batch, int min_status, int* idx, int* count,
+                                  hipStream_t s);
 hipError_t launch_gather_widen(const float* src, double* dst, const int* idx, int rows, size_t elems,
                                hipStream_t s);
 hipError_t launch_scatter_narrow(const double* src, float* dst, const int* idx, int rows, size_t elems,

@@ -26,7 +26,8 @@ constexpr int kSelThreads = 1024;
 // unsolved flags and its prefix popcount, per tile a 16-entry prefix over the
 // waves, so idx[] lists the unsolved QPs in ascending order (deterministic).
 __global__ __launch_bounds__(kSelThreads) void select_unsolved_kernel(const int* __restrict__ status,
-                                                                      int batch, int* __restrict__ idx,
+                                                                      int batch, int min_status,
+                                                                      int* __restrict__ idx,
                                                                       int* __restrict__ count) {
   __shared__ int wave_tot[kSelThreads / 64];
   __shared__ int wave_off[kSelThreads / 64];
@@ -34,7 +35,7 @@ __global__ __launch_bounds__(kSelThreads) void select_unsolved_kernel(const int*
   int base_out = 0;
   for (int base = 0; base < batch; base += kSelThreads) {
     const int i = base + (int)threadIdx.x;
-    const bool flag = i < batch && status[i] != 0;
+    const bool flag = i < batch && status[i] >= min_status;
     const unsigned long long m = __ballot(flag);
     const int before = __popcll(m & ((1ull << lane) - 1ull));
     if (lane == 0) wave_tot[wave] = __popcll(m);
@@ -118,8 +119,10 @@ dim3 copy_grid(size_t total) {
 
 }  // namespace
 
-hipError_t launch_select_unsolved(const int* status, int batch, int* idx, int* count, hipStream_t s) {
-  hipLaunchKernelGGL(select_unsolved_kernel, dim3(1), dim3(kSelThreads), 0, s, status, batch, idx, count);
+hipError_t launch_select_unsolved(const int* status, int batch, int min_status, int* idx, int* count,
+                                  hipStream_t s) {
+  hipLaunchKernelGGL(select_unsolved_kernel, dim3(1), dim3(kSelThreads), 0, s, status, batch, min_status,
+                     idx, count);
   return hipGetLastError();
 }
 

@@ -250,17 +250,19 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
 static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                      const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s, hipStream_t strm);
 
-// warm_bars: warm_start 2 only (the fp64 continuation of rescue_f32), see ProblemArgsT
+// warm_bars: warm_start 2 only (the fp64 continuation of rescue_f32), see ProblemArgsT;
+// iter_cap >= 0 (the f32_iters continuation): at most that many iterations, while the stat
+// table keeps the caller's st->iter_max + 2 rows
 template <typename T, typename DataT, typename SolT>
 static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, const DataT* d,
                       const SolT* s, void* stream, const T* warm_bars = nullptr,
-                      int skip_last_rb = 0) {
+                      int skip_last_rb = 0, int iter_cap = -1) {
   int rc = validate_call(h, batch, st, d, s);
   if (rc) return rc;
   if (batch == 0) return SRBD_QP_OK;
   hipStream_t strm = stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;
   if constexpr (std::is_same_v<T, double>) {
-    if (st->f32_iters > 0 && st->iter_max > 0 && constrained(h->dims) && h->dims.nx == 12 &&
+    if (st->f32_iters > 0 && st->iter_max > 1 && constrained(h->dims) && h->dims.nx == 12 &&
         h->dims.nu == 12)
       return mixed_f64(h, batch, st, d, s, strm);
   }
@@ -305,6 +307,7 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   a.skip_last_rb = skip_last_rb;
   // f64_rescue = n: the fp32 pass stops after n iterations at most, the rest is fp64's
   if (rescue && st->f64_rescue < a.iter_max) a.iter_max = st->f64_rescue;
+  if (iter_cap >= 0 && iter_cap < a.iter_max) a.iter_max = iter_cap;
   a.pred_corr = st->pred_corr;
   a.split_step = st->split_step;
   a.ric_alg = st->ric_alg != 0;  // HPIPM: any nonzero square_root_alg
@@ -377,7 +380,7 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
   hipSetDevice(h->device);
   int* idx = h->resc_idx;
   int* count = h->resc_idx + 2 * (size_t)h->capacity;
-  hipError_t e = srbd::launch_select_unsolved(status, batch, idx, count, strm);
+  hipError_t e = srbd::launch_select_unsolved(status, batch, 1, idx, count, strm);
   if (e == hipSuccess) e = hipMemcpyAsync(h->resc_count_host, count, sizeof(int), hipMemcpyDeviceToHost, strm);
   if (e == hipSuccess) e = hipStreamSynchronize(strm);
   const int R = e == hipSuccess ? *h->resc_count_host : 0;
@@ -482,7 +485,9 @@ static int fallback_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   hipSetDevice(h->device);
   int* idx = h->resc_idx;
   int* count = h->resc_idx + 2 * (size_t)h->capacity;
-  hipError_t e = srbd::launch_select_unsolved(sc->status, batch, idx, count, strm);
+  // numerical breakdowns only (MinStepLengthReached, NaNDetected): a MaxIterReached QP has
+  // spent the iteration budget, as the fp64 path would have
+  hipError_t e = srbd::launch_select_unsolved(sc->status, batch, 2, idx, count, strm);
   if (e == hipSuccess) e = hipMemcpyAsync(h->resc_count_host, count, sizeof(int), hipMemcpyDeviceToHost, strm);
   if (e == hipSuccess) e = hipStreamSynchronize(strm);
   const int R = e == hipSuccess ? *h->resc_count_host : 0;
@@ -614,9 +619,11 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("mixed precision: ") + hipGetErrorString(e));
   // fp32 iterations: tolerances out of reach, so every QP runs them all (a QP that stops
   // early on NaN / min step continues cold in fp64: its iterate fails the finiteness test
-  // or is simply where it stopped)
+  // or is simply where it stopped).  They count against iter_max: n = min(f32_iters,
+  // iter_max - 1) fp32 iterations, then at most iter_max - n fp64 ones.
+  const int n32 = st->f32_iters < st->iter_max - 1 ? st->f32_iters : st->iter_max - 1;
   srbd_qp_settings st32 = *st;
-  st32.iter_max = st->f32_iters < st->iter_max ? st->f32_iters : st->iter_max;
+  st32.iter_max = n32;
   st32.tol_stat = st32.tol_eq = st32.tol_ineq = st32.tol_comp = 1e-30;
   st32.f64_rescue = 0;
   st32.f32_iters = 0;
@@ -640,7 +647,7 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   }
   srbd_qp_solution_f64 sc = *s;
   if (!sc.status) sc.status = h->resc_idx + h->capacity;
-  rc = solve_impl<double>(h, batch, &st64, d, &sc, strm, warm);
+  rc = solve_impl<double>(h, batch, &st64, d, &sc, strm, warm, 0, st->iter_max - n32);
   if (rc) return rc;
   return fallback_f64(h, batch, st, d, &sc, s, strm);
 }

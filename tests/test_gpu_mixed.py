@@ -70,13 +70,15 @@ def test_mixed_ignored_when_padded_or_unconstrained(pkg):
 
 
 def test_mixed_iter_max_bounds_the_fp32_pass(pkg):
-    """f32_iters >= iter_max: the fp32 pass runs iter_max iterations and the fp64
-    continuation still has its own iter_max; warm-started calls narrow the caller's
+    """f32_iters >= iter_max: the fp32 pass runs iter_max - 1 iterations and the fp64
+    continuation the one left of the budget; warm-started calls narrow the caller's
     x / u for the fp32 pass."""
     qp, x0 = pkg.srbd_model.generate_batch(32, N=20, seed=9, constraints="box_u")
     o64 = pkg.capi.solve(qp, x0, NMPC)
     mix = pkg.capi.solve(qp, x0, dict(NMPC, iter_max=8, f32_iters=50))
-    assert np.all(mix["status"] == 0), mix["status"]
+    assert np.all(mix["iter"] == 1), mix["iter"]
+    assert np.all(mix["status"] <= 1), mix["status"]
+    assert np.all(mix["res"][mix["status"] == 0] <= 1e-4)
     warm = pkg.capi.solve(qp, x0, dict(NMPC, warm_start=1, f32_iters=4),
                           x_init=o64["x"], u_init=o64["u"])
     assert np.all(warm["status"] == 0), warm["status"]
@@ -106,18 +108,39 @@ def test_mixed_host_entry_point_matches_device(pkg):
 
 
 def test_mixed_fallback_is_the_fp64_solve(pkg):
-    """A QP the fp64 continuation leaves unsolved is solved again cold in fp64, so it ends
-    exactly as the fp64 path ends it.  iter_max = 3 leaves most QPs unsolved either way:
-    every QP the mixed call reports unsolved carries the plain fp64 outputs bit for bit."""
+    """A QP the fp64 continuation ends with a numerical breakdown (here NaNDetected: a NaN
+    in its data) is solved again cold in fp64, so it ends exactly as the fp64 path ends it,
+    bit for bit; the rest of the batch is not re-solved."""
+    qp, x0 = pkg.srbd_model.generate_batch(64, N=20, seed=23, constraints="box_u")
+    bad = [5, 40]
+    for i in bad:
+        qp.q[i, 7, 3] = np.nan
+    st = dict(NMPC)
+    plain = pkg.capi.solve(qp, x0, st, stats=True)
+    mix = pkg.capi.solve(qp, x0, dict(st, f32_iters=6), stats=True)
+    assert np.all(plain["status"][bad] == 3) and np.all(mix["status"][bad] == 3)
+    for key in ("x", "u", "pi", "status", "iter", "res", "obj", "stat"):
+        assert np.array_equal(mix[key][bad], plain[key][bad], equal_nan=key not in ("status", "iter")), key
+    ok = np.setdiff1d(np.arange(qp.batch), bad)
+    assert np.all(mix["status"][ok] == 0) and np.all(mix["res"][ok] <= 1e-4)
+
+
+@pytest.mark.parametrize("f32_iters", [2, 3, 8])
+def test_mixed_iteration_budget(pkg, f32_iters):
+    """The fp32 iterations count against iter_max: m = min(f32_iters, iter_max - 1) fp32
+    iterations, then at most iter_max - m fp64 ones (reported in iter).  At iter_max = 3
+    most QPs end MaxIterReached and are returned as they are, not solved again."""
     qp, x0 = pkg.srbd_model.generate_batch(300, N=20, seed=23, constraints="box_u")
     st = dict(NMPC, iter_max=3)
-    plain = pkg.capi.solve(qp, x0, st, stats=True)
-    mix = pkg.capi.solve(qp, x0, dict(st, f32_iters=3), stats=True)
-    bad = mix["status"] != 0
-    assert bad.sum() > 100, np.bincount(mix["status"])
-    for key in ("x", "u", "pi", "status", "iter", "res", "obj", "stat"):
-        assert np.array_equal(mix[key][bad], plain[key][bad]), key
-    assert np.all(plain["status"][~bad] != 0) or np.all(mix["res"][~bad] <= 1e-4)
+    mix = pkg.capi.solve(qp, x0, dict(st, f32_iters=f32_iters), stats=True)
+    m = min(f32_iters, 2)
+    assert np.all(mix["iter"] <= 3 - m) and np.all(mix["iter"] >= 1)
+    assert np.all(mix["status"] <= 1), np.bincount(mix["status"])
+    assert (mix["status"] == 1).sum() > 100, np.bincount(mix["status"])
+    # the stat table keeps the caller's iter_max + 2 rows; rows past the last fp64 one are 0
+    assert mix["stat"].shape[1] == 5
+    for i in range(qp.batch):
+        assert np.all(mix["stat"][i, mix["iter"][i] + 1:] == 0)
 
 
 def test_one_handle_mixed_rescue_mixed_bit_identical(pkg):
