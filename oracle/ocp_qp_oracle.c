@@ -579,6 +579,12 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
   double* du = (double*)calloc((size_t)N * nu + 1, sizeof(double));
   double* dpi = (double*)calloc((size_t)(N + 1) * nx, sizeof(double));
   double* zero = (double*)calloc((size_t)nx, sizeof(double));
+  double* itg = (double*)calloc((size_t)(N + 1) * w.gstride, sizeof(double));
+  double* itb = (double*)calloc((size_t)N * nx + 1, sizeof(double));
+  double* cdx = (double*)calloc((size_t)(N + 1) * nx, sizeof(double));
+  double* cdu = (double*)calloc((size_t)N * nu + 1, sizeof(double));
+  double* cdpi = (double*)calloc((size_t)(N + 1) * nx, sizeof(double));
+  int itref_g[1025];
   int nc = 0;
   stage_rows_t* st = build_rows(&d, &nc);
   int rc = 0;
@@ -767,6 +773,53 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
       riccati_forward(&d, &w, zero, dx, du, dpi);
       STEP_TLAM();
     }
+    /* iterative refinement of the final step on the reduced (Gamma-augmented) KKT
+     * system: the dt / dlam equations hold exactly by construction (STEP_TLAM), so
+     * the residual lives in the stationarity and dynamics rows; solve again with the
+     * same factors and add the correction.                                           */
+    for (int ir = 0; ir < set->itref_corr_max; ++ir) {
+      double* gsave = rg; (void)gsave;
+      for (int s = 0; s <= N; ++s) {
+        int nu_k = st[s].nu_k, ns = nu_k + nx;
+        const double* Ht = w.Ht + s * w.hstride;
+        double* gt = w.gt + s * w.gstride;
+        double v[64], r1[64];
+        for (int i = 0; i < nu_k; ++i) v[i] = du[(size_t)s * nu + i];
+        for (int i = 0; i < nx; ++i) v[nu_k + i] = dx[(size_t)s * nx + i];
+        for (int i = 0; i < ns; ++i) {
+          double acc = gt[i];
+          for (int j = 0; j < ns; ++j) acc += M_(Ht, ns, i, j) * v[j];
+          r1[i] = acc;
+        }
+        if (s < N) {
+          double t[32];
+          mtv(nx, nu, qB(&d, s), dpi + (size_t)(s + 1) * nx, t);
+          for (int i = 0; i < nu; ++i) r1[i] += t[i];
+          mtv(nx, nx, qA(&d, s), dpi + (size_t)(s + 1) * nx, t);
+          for (int i = 0; i < nx; ++i) r1[nu_k + i] += t[i];
+        }
+        if (s > 0) for (int i = 0; i < nx; ++i) r1[nu_k + i] -= dpi[(size_t)s * nx + i];
+        else for (int i = 0; i < nx; ++i) r1[nu_k + i] = 0.0;
+        itref_g[s] = 0;
+        memcpy(itg + (size_t)s * w.gstride, r1, sizeof(double) * ns);
+        if (s < N) {
+          double t1[32], t2[32];
+          mv(nx, nx, qA(&d, s), dx + (size_t)s * nx, t1);
+          mv(nx, nu, qB(&d, s), du + (size_t)s * nu, t2);
+          for (int i = 0; i < nx; ++i)
+            itb[(size_t)s * nx + i] = t1[i] + t2[i] + w.bt[(size_t)s * nx + i] - dx[(size_t)(s + 1) * nx + i];
+        }
+      }
+      /* correction: same factors, rhs = the residual */
+      double* gkeep = w.gt; double* bkeep = w.bt;
+      w.gt = itg; w.bt = itb;
+      riccati_vectors(&d, &w);
+      riccati_forward(&d, &w, zero, cdx, cdu, cdpi);
+      w.gt = gkeep; w.bt = bkeep;
+      for (size_t i = 0; i < (size_t)(N + 1) * nx; ++i) { dx[i] += cdx[i]; if (i >= (size_t)nx) dpi[i] += cdpi[i]; }
+      for (size_t i = 0; i < (size_t)N * nu; ++i) du[i] += cdu[i];
+      STEP_TLAM();
+    }
 #undef STEP_TLAM
 
     /* step lengths (fraction to boundary) */
@@ -857,6 +910,7 @@ done:
   free_rows(&d, st);
   free(w.Ht); free(w.gt); free(w.bt); free(w.P); free(w.p); free(w.K); free(w.kk); free(w.Lg);
   free(rg); free(rb); free(dx); free(du); free(dpi); free(zero);
+  free(itg); free(itb); free(cdx); free(cdu); free(cdpi);
   return rc;
 }
 

@@ -58,6 +58,7 @@ typedef struct oracle_settings {
   int warm_start, pred_corr, split_step;
   int ric_alg;  /* 0 classical Riccati; else square root: P_k = Lx Lx', with the
                  * stage products formed from chol(P_{k+1}) (HPIPM square_root_alg) */
+  int itref_corr_max; /* iterative refinement steps of the final (corrector) step        */
 } oracle_settings;
 
 typedef struct oracle_result {

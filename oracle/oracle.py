@@ -35,7 +35,8 @@ class _Settings(C.Structure):
     _fields_ = [("iter_max", C.c_int), ("alpha_min", C.c_double), ("mu0", C.c_double),
                 ("tol_stat", C.c_double), ("tol_eq", C.c_double), ("tol_ineq", C.c_double),
                 ("tol_comp", C.c_double), ("reg_prim", C.c_double), ("warm_start", C.c_int),
-                ("pred_corr", C.c_int), ("split_step", C.c_int), ("ric_alg", C.c_int)]
+                ("pred_corr", C.c_int), ("split_step", C.c_int), ("ric_alg", C.c_int),
+                ("itref_corr_max", C.c_int)]
 
 
 class _Result(C.Structure):
@@ -76,7 +77,7 @@ def _ptr(a: Optional[np.ndarray]):
 
 DEFAULT_SETTINGS = dict(iter_max=15, alpha_min=1e-8, mu0=1e2, tol_stat=1e-8, tol_eq=1e-8,
                         tol_ineq=1e-8, tol_comp=1e-8, reg_prim=1e-12, warm_start=0, pred_corr=1,
-                        split_step=0, ric_alg=1)  # hpipm-cpp defaults (settings.hpp:26-86)
+                        split_step=0, ric_alg=1, itref_corr_max=0)  # hpipm-cpp defaults (settings.hpp:26-86)
 
 
 def _settings(s: Optional[Dict]) -> _Settings:

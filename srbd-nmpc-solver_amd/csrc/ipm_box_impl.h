@@ -415,9 +415,11 @@ __device__ __forceinline__ void gather12(real v, real (&out)[12]) {
   });
 }
 
-// SQRT (RB only): ric_alg = 1, the square-root factorization (riccati.h riccati_step_sqrt);
-// the factor record holds the same quantities (P_k = F - Y'Y, which Lx factors), so F1, B2
-// and F2 are shared.
+// SQRT: ric_alg = 1, the square-root factorization (riccati.h riccati_step_sqrt).  The
+// record's kRecP slot then holds the factor Lp of P = Lp Lp' (packed lower triangle, the
+// same 78 reals) and every sweep applies P as Lp (Lp' v): the solves use exactly the P the
+// next stage's factorization used (ric_alg 0 gets the same consistency by symmetrizing its
+// register P_k, riccati.h SYMP).
 template <bool FULL, int GEN, int PH, bool SQRT = false>
 __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -450,6 +452,21 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   c.blg = a.lg; c.bug = a.ug; c.blgm = a.lg_mask; c.bugm = a.ug_mask;
   c.bxo = a.x; c.buo = a.u; c.bpi = a.pi; c.bws = a.ws;
   const real reg = a.reg;
+  // (P x)_col + acc for an element-owned x (lane j holds x_j), P from a stage record's kRecP
+  // slot: packed P (ric_alg 0) or its factor Lp (ric_alg 1)
+  auto rec_P_mul = [&](const real* rec, real xv, real acc) -> real {
+    if constexpr (SQRT) {
+      real Lv[12];
+      load_packed_lcol_d(rec + kRecP, col, Lv);
+      const real t = dot_bcast(Lv, xv, real(0.0));  // (Lp' x)_col
+      load_packed_lrow_d(rec + kRecP, col, Lv);
+      return dot_bcast(Lv, t, acc);                 // (Lp t)_col + acc
+    } else {
+      real Pc[12];
+      load_packed_sym(rec + kRecP, col, Pc);
+      return dot_bcast(Pc, xv, acc);
+    }
+  };
 
   // ---- general rows (GEN): Gamma / gamma and their images under C, D ----
   // Gamma / gamma of row `lane` of chunk ch (corrector: + dlam_aff dt_aff - sigma mu)
@@ -481,24 +498,28 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     }
   };
   // Hessian adds (column-owned): which 0: M1 = R += D'Gamma D;
-  // 1: M1 = S += D'Gamma C, M2 = Q += C'Gamma C;  2: M1 = Q += C'Gamma C
+  // 1: M1 = S += D'Gamma C, M2 = Q += C'Gamma C;  2: M1 = Q += C'Gamma C.
+  // Formed from the scaled rows sqrt(Gamma) D, sqrt(Gamma) C, so D'Gamma D and C'Gamma C
+  // are sums of the same products in both triangles: exactly symmetric (a Gamma of 1e12
+  // times rounding-level asymmetry stalled degenerate endgames).
   auto g_hess = [&](int k, int which, real (&M1)[12], real (&M2)[12]) {
     for (int ch = 0; ch < c.nch; ++ch) {
-      real G, gg, Gb[12], Cc[12], Dc[12], Y[12];
+      real G, gg, Gb[12], Cc[12], Dc[12];
       g_gamma(k, ch, false, real(0.0), G, gg);
-      gather12(G, Gb);
+      gather12(__builtin_sqrt(G), Gb);
       c.g_col(k, ch, col, Cc, Dc);
       sfor<0, 12>([&](auto i) {
         constexpr int I = decltype(i)::value;
-        Y[I] = Gb[I] * (which == 0 ? Dc[I] : Cc[I]);
+        Dc[I] *= Gb[I];
+        Cc[I] *= Gb[I];
       });
       if (which == 0) {
-        tmul_acc(Dc, Y, M1);
+        tmul_acc(Dc, Dc, M1);
       } else if (which == 1) {
-        tmul_acc(Dc, Y, M1);
-        tmul_acc(Cc, Y, M2);
+        tmul_acc(Dc, Cc, M1);
+        tmul_acc(Cc, Cc, M2);
       } else {
-        tmul_acc(Cc, Y, M1);
+        tmul_acc(Cc, Cc, M1);
       }
     }
   };
@@ -762,14 +783,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     real bx0[12], bu0[12];
     gather12(xel ? c.x()[li] : real(0.0), bx0);
     gather12(uel ? c.u()[li] : real(0.0), bu0);
-    real P1c[12], brb[12];
-    load_packed_sym(st1 + kRecP, col, P1c);
-    gather12(lane < kMaxDim ? st0[kStRes + 24 + lane] : real(0.0), brb);
-    real t = xel ? c.pi()[(size_t)nx + lane] : real(0.0);
-    sfor<0, 12>([&](auto j) {
-      constexpr int J = decltype(j)::value;
-      t = fmadd(P1c[J], brb[J], t);
-    });
+    real t = rec_P_mul(st1, lane < kMaxDim ? st0[kStRes + 24 + lane] : real(0.0),
+                       xel ? c.pi()[(size_t)nx + lane] : real(0.0));
     if (!xel) t = real(0.0);
     real bt[12];
     gather12(t, bt);
@@ -795,18 +810,21 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       real bxk[12];
       gather12(xel ? c.x()[(size_t)k * nx + li] : real(0.0), bxk);
       real Pc[12];
-      load_packed_sym(stk + kRecP, col, Pc);
+      if constexpr (SQRT) {  // P = Lp Lp': column l = sum_K Lp[:, K] Lp[l][K]
+        real Lr[12];
+        load_packed_lrow_d(stk + kRecP, col, Lr);
+        sfor<0, 12>([&](auto i) { Pc[decltype(i)::value] = real(0.0); });
+        tmul_acc(Lr, Lr, Pc);
+      } else {
+        load_packed_sym(stk + kRecP, col, Pc);
+      }
       if (a.P && xel)
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
           if (I < nx) a.P[((size_t)qp * (N + 1) + k) * nxx + (size_t)lane * nx + I] = Pc[I];
         });
       if (a.p) {
-        real px = real(0.0);
-        sfor<0, 12>([&](auto j) {
-          constexpr int J = decltype(j)::value;
-          px = fmadd(Pc[J], bxk[J], px);
-        });
+        const real px = rec_P_mul(stk, xel ? c.x()[(size_t)k * nx + li] : real(0.0), real(0.0));
         if (xel) a.p[((size_t)qp * (N + 1) + k) * nx + lane] = c.pi()[(size_t)k * nx + lane] - px;
       }
       if (k < N) {
@@ -992,13 +1010,14 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             gea = dot_bcast(Dc, e, gea);
           }
           if constexpr (GEN == 1) {
-            real Gb[12], Y[12];
-            gather12(G, Gb);
+            // D'Gamma D from sqrt(Gamma) D: exactly symmetric (see g_hess)
+            real Gb[12];
+            gather12(__builtin_sqrt(G), Gb);
             sfor<0, 12>([&](auto i) {
               constexpr int I = decltype(i)::value;
-              Y[I] = Gb[I] * Dc[I];
+              Dc[I] *= Gb[I];
             });
-            tmul_acc(Dc, Y, RG);
+            tmul_acc(Dc, Dc, RG);
           }
         }
       }
@@ -1083,9 +1102,9 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           if (lane == I) P[I] += Gx;
           if (c.isv) P[I] = qv[I];
         });
-        if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
         if (c.isv) store12(rec + kRecPv, P);
-        if constexpr (SQRT) sqrt_factor(P, lane);
+        if constexpr (SQRT) sqrt_factor(P, lane);  // (the record keeps the factor)
+        if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
       } else {
         // ---- A, B (kept by the factorization), S (kept in LDS): residual products ----
         real A_[12], B_[12];
@@ -1163,13 +1182,13 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         if constexpr (SQRT) {
           riccati_step_sqrt(P, A_, B_, loadR, loadSQ, lane, reg, f);
         } else {
-          riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
+          riccati_step<1, true>(P, A_, B_, loadR, loadSQ, lane, reg, f);  // P_k symmetrized
         }
         if (lane < kMaxDim) {
           store_packed_col(rec + kRecL, lane, f.Lc);
           store12(rec + kRecK + lane * 12, f.Kc);
           store12(rec + kRecAcl + lane * 12, A_);
-          store_packed_col(rec + kRecP, lane, f.F);
+          if constexpr (!SQRT) store_packed_col(rec + kRecP, lane, f.F);
           rec[kRecRs + lane] = f.rs;
         }
         if (c.isv) {
@@ -1181,7 +1200,10 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           constexpr int I = decltype(i)::value;
           P[I] = f.F[I];
         });
-        if constexpr (SQRT) sqrt_factor(P, lane);
+        if constexpr (SQRT) {
+          sqrt_factor(P, lane);
+          if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
+        }
         // the next stage overwrites this group's LDS blocks: reads done first
         lds_wave_fence();
       }
@@ -1289,9 +1311,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           }
           const real bt = lane < kMaxDim ? stk[kStRes + 24 + lane] : real(0.0);
           // w = P_{k+1} b~ + p_{k+1}
-          real Pc[12];
-          load_packed_sym(recn + kRecP, col, Pc);
-          const real w = dot_bcast(Pc, bt, pnext);
+          const real w = rec_P_mul(recn, bt, pnext);
           // g = r~ + B'w ; f = q~ + A'w
           real Bc[12], Ac[12];
           c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, Bc);
@@ -1361,11 +1381,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         const real* rec = stk + par * kRecSize;
         // dpi = P dx + p is part of the final step only (F2, or F1 without corrector)
         real dpi = real(0.0);
-        if (corr || !a.pred_corr) {
-          real Pc[12];
-          load_packed_sym(rec + kRecP, col, Pc);
-          dpi = dot_bcast(Pc, dxk, rec[kRecPv + li]);
-        }
+        if (corr || !a.pred_corr) dpi = rec_P_mul(rec, dxk, rec[kRecPv + li]);
         real du = real(0.0), dxn = real(0.0);
         if (k < N) {
           real Kr[12], Ar[12];
@@ -1543,6 +1559,7 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
   // at the top of every later launch.  iter_max + 1 factorization sweeps at
   // most: the last one always decides (converged or MaxIterReached).
   hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhInit>), grid, block, 0, stream, a);
+  // (SQRT changes RB and how B2, F1, F2 and the outputs apply the record's P)
   for (int it = 0;; ++it) {
     if (it >= a.iter_max) {
       if (!a.skip_last_rb)
@@ -1551,9 +1568,9 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
     }
     hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT>), grid, block, 0, stream, a);
     if (a.pred_corr)
-      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhB2, kPhF2>), grid, block, 0, stream, a);
+      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhB2, kPhF2, SQRT>), grid, block, 0, stream, a);
   }
-  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut>), grid, block, 0, stream, a);
+  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut, SQRT>), grid, block, 0, stream, a);
   return hipGetLastError();
 }
 

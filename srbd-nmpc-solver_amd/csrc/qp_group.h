@@ -391,6 +391,23 @@ __device__ __forceinline__ void load_packed_sym(const T* pk, int r, T (&v)[12]) 
     v[J] = J <= r ? pk[packed_col(J) + r - J] : pk[cr + J];
   });
 }
+// row r of a packed lower-triangular L, diagonal included: v[j] = L[r][j] (j <= r), else 0
+template <typename T>
+__device__ __forceinline__ void load_packed_lrow_d(const T* pk, int r, T (&v)[12]) {
+  sfor<0, 12>([&](auto j) {
+    constexpr int J = decltype(j)::value;
+    v[J] = J <= r ? pk[packed_col(J) + r - J] : T(0);
+  });
+}
+// column c of a packed lower-triangular L, diagonal included: v[i] = L[i][c] (i >= c), else 0
+template <typename T>
+__device__ __forceinline__ void load_packed_lcol_d(const T* pk, int c, T (&v)[12]) {
+  const int cc = packed_col(c) - c;
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    v[I] = I >= c ? pk[cc + I] : T(0);
+  });
+}
 // strictly-lower row r of a packed lower-triangular L: v[j] = L[r][j] (j < r), else 0
 template <typename T>
 __device__ __forceinline__ void load_packed_lrow(const T* pk, int r, T (&v)[12]) {

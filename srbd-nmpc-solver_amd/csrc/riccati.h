@@ -132,12 +132,36 @@ struct NoMid {
   __device__ __forceinline__ void operator()() const {}
 };
 
+// Column-owned M (lane l holds M[:, l]) made exactly symmetric from its lower triangle:
+// lane l's entries above the diagonal (rows I < l) are replaced by lane I's entry of row l
+// (only lanes J > I change M[I], so no source is overwritten before it is read).
+template <typename T>
+__device__ __forceinline__ void symmetrize_lower(T (&M)[12], const int lane) {
+  sfor<1, 12>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    sfor<0, J>([&](auto ii) {
+      constexpr int I = decltype(ii)::value;
+      const T v = bc<I>(M[J]);
+      M[I] = lane == J ? v : M[I];
+    });
+    SRBD_PHASE_FENCE();
+  });
+}
+
 // The common tail of both step variants: given L = chol(G) and the column-owned
 // H (VL: g) and F (VL: f) of the stage,
 //   Y = L^-1 H, K = -L^-T Y, P_k = F - Y'Y (VL: p_k = f - Y'y), Acl = A + B K.
 // `mid` runs before the triangular solves (MidAt = 1) or after them (MidAt = 2).
-template <int MidAt, typename T, typename Mid>
-__device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], StageFactor<T>& o, Mid&& mid) {
+// SYMP: P_k is made exactly symmetric from its lower triangle before it continues the
+// recursion.  The column-wise products leave rounding-level asymmetry in F - Y'Y, while
+// the stage record keeps the lower triangle only: with the IPM's barrier Hessians of
+// ~1e12 the next stage's factorization (register P) and the sweeps that read the record P
+// then solve systems that differ far above the factorization's own error, which stalled
+// degenerate endgames.  (The square-root step needs no such step: its
+// Hessian terms are sums of squares, symmetric by construction.)
+template <int MidAt, bool SYMP, typename T, typename Mid>
+__device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], const int lane, StageFactor<T>& o,
+                                             Mid&& mid) {
   if constexpr (MidAt == 1) {
     mid();
     SRBD_PHASE_FENCE();
@@ -162,6 +186,10 @@ __device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], StageFact
   // ---- Acl = A + B K (VL: bcl = b + B k)
   launder(B_);
   sym_mul_col(B_, o.Kc, A_);  // A[i][l] += B[i][m] K[m][l]: bc<m>(B_[i]) * Kc[m]
+  if constexpr (SYMP) {
+    SRBD_PHASE_FENCE();
+    symmetrize_lower(o.F, lane);  // (B dead here: fewer live registers)
+  }
 }
 
 // One backward Riccati step.  `P` holds P_{k+1} (VL: p_{k+1}) on entry.
@@ -171,7 +199,8 @@ __device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], StageFact
 // `mid` runs between the products and the triangular solves (MidAt = 1: P is
 // dead there) or after the solves (MidAt = 2: L is dead too): the caller may
 // issue the next stage's loads into registers of its own.
-template <int MidAt = 1, typename T, typename LoadR, typename LoadSQ, typename Mid = NoMid>
+template <int MidAt = 1, bool SYMP = false, typename T, typename LoadR, typename LoadSQ,
+          typename Mid = NoMid>
 __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&B_)[12],
                                              LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
                                              const T reg, StageFactor<T>& o, Mid&& mid = Mid{}) {
@@ -212,7 +241,7 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
     tmul_acc(A_, W, o.F);
   }
   SRBD_PHASE_FENCE();
-  riccati_tail<MidAt>(A_, B_, o, mid);
+  riccati_tail<MidAt, SYMP>(A_, B_, lane, o, mid);
 }
 
 // Square-root step (ric_alg = 1).  `Lp` holds the factor of P_{k+1} (lane l: column l,
@@ -221,7 +250,8 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
 //   G = R + MB'MB,  H = S + MB'MA,  F = Q + MA'MA,  g = r + MB'm,  f = q + MA'm
 // -- in exact arithmetic the classical B'PB, B'PA, A'PA, B'(Pb + p), A'(Pb + p) --
 // then the common tail.  The caller continues the recursion with sqrt_factor(P_k).
-template <int MidAt = 1, typename T, typename LoadR, typename LoadSQ, typename Mid = NoMid>
+template <int MidAt = 1, bool SYMP = false, typename T, typename LoadR, typename LoadSQ,
+          typename Mid = NoMid>
 __device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12], T (&B_)[12],
                                                   LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
                                                   const T reg, StageFactor<T>& o, Mid&& mid = Mid{}) {
@@ -254,7 +284,7 @@ __device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12]
     tmul_acc(MA, MA, o.F);
   }
   SRBD_PHASE_FENCE();
-  riccati_tail<MidAt>(A_, B_, o, mid);
+  riccati_tail<MidAt, SYMP>(A_, B_, lane, o, mid);
 }
 
 // P (lane l: column l of P_k; VL: p_k) -> its square-root form for the next

@@ -156,22 +156,23 @@ def test_iteration_statistics(pkg, oracle):
         assert np.all(S[it + 1:] == 0) and np.all(S[:, 11:] == 0)
 
 
+@pytest.mark.parametrize("ric_alg", [0, 1])
 @pytest.mark.parametrize("dims", [(5, 3, 2, 103), (12, 12, 4, 105), (12, 4, 14, 200)])
-def test_general_constraints_vs_oracle(pkg, oracle, dims):
+def test_general_constraints_vs_oracle(pkg, oracle, dims, ric_alg):
     """lg <= C x + D u <= ug (the reference 'constrained' test's ng rows,
-    test/ocp_qp_ipm_solver.cpp:149-158), 1 and 2 chunks of 12 rows."""
+    test/ocp_qp_ipm_solver.cpp:149-158), 1 and 2 chunks of 12 rows.  (12, 4, 14) seed 200
+    holds a near-degenerate QP (#12: 5 active rows at a stage with nu = 4) whose endgame
+    runs at barrier Hessians of ~1e13: every QP converges on both Riccati variants
+    (endgame consistency)."""
     nx, nu, ng, seed = dims
     qp, x0 = helpers.random_constrained(20, 12, nx, nu, ng, seed, pkg.OcpQpBatch)
-    st = dict(iter_max=50, mode="Balance")
+    st = dict(iter_max=50, mode="Balance", ric_alg=ric_alg)
     out = pkg.capi.solve(qp, x0, st)
     ref = oracle.solve(qp, st, x0=x0)
     assert np.all(ref["status"] == 0), ref["status"]
-    # (12, 4, 14) seed 200 holds one near-degenerate QP (#12: 5 active rows at a
-    # stage with nu = 4) whose IPM endgame stalls at res_stat ~3e-8 > tol on the
-    # GPU while the oracle's rounding reaches 7e-9; every other QP must agree.
+    assert np.all(out["status"] == 0), (out["status"], out["res"])
     ok = out["status"] == 0
-    assert ok.sum() >= qp.batch - (1 if ng > 12 else 0), (out["status"], out["res"])
-    assert np.all(np.abs(out["iter"] - ref["iter"])[ok] <= 1), (out["iter"], ref["iter"])
+    assert np.all(np.abs(out["iter"] - ref["iter"]) <= 1), (out["iter"], ref["iter"])
     for i in np.nonzero(ok)[0]:
         for key in ("x", "u"):
             assert helpers.is_approx(out[key][i], ref[key][i], 1e-7), (key, i)
@@ -236,9 +237,9 @@ def test_extreme_sizes_vs_oracle(pkg, oracle, dims):
     st = dict(iter_max=60, mode="Balance")
     out = pkg.capi.solve(qp, x0, st)
     ref = oracle.solve(qp, st, x0=x0)
-    ok = (out["status"] == 0) & (ref["status"] == 0)
-    assert ok.sum() >= qp.batch - 1, (out["status"], ref["status"])
-    for i in np.nonzero(ok)[0]:
+    assert np.all(ref["status"] == 0), ref["status"]
+    assert np.all(out["status"] == 0), (out["status"], out["res"])
+    for i in range(qp.batch):
         for key in ("x", "u"):
             assert helpers.is_approx(out[key][i], ref[key][i], 1e-6), (key, i)
 
