@@ -6,7 +6,8 @@ import numpy as np
 import helpers
 pkg = helpers.load_package()
 np.set_printoptions(linewidth=220, precision=3)
-F32 = dict(iter_max=30, tol_stat=3e-2, tol_eq=1e-3, tol_ineq=1e-3, tol_comp=1e-3, split_step=1)
+F32 = dict(iter_max=30, tol_stat=3e-2, tol_eq=1e-3, tol_ineq=1e-3, tol_comp=1e-3, split_step=1,
+           ric_alg=int(sys.argv[1]) if len(sys.argv) > 1 else 0)
 N = 40
 qp, x0 = pkg.srbd_model.generate_batch(2048, N=N, seed=1005, constraints="cone")
 o = pkg.capi.solve(qp, x0, F32, dtype=np.float32, stats=True)
