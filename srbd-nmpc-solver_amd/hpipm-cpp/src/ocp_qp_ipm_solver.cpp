@@ -48,7 +48,25 @@ void copy_block(std::vector<double>& dst, size_t off, const double* src, size_t 
   if (n) std::memcpy(dst.data() + off, src, n * sizeof(double));
 }
 
-// Uniform stage dimensions of one problem (the C-ABI's model).
+// rows x cols column-major src (ld = rows) into dst at off with leading dimension ld
+void copy_mat(std::vector<double>& dst, size_t off, size_t ld, const double* src, size_t rows,
+              size_t cols) {
+  for (size_t c = 0; c < cols; ++c)
+    if (rows) std::memcpy(dst.data() + off + c * ld, src + c * rows, rows * sizeof(double));
+}
+// the leading rows x cols block of a column-major ld x * src into dst (ld = rows)
+void take_mat(double* dst, const double* src, size_t ld, size_t rows, size_t cols) {
+  for (size_t c = 0; c < cols; ++c)
+    if (rows) std::memcpy(dst + c * rows, src + c * ld, rows * sizeof(double));
+}
+
+// Stage dimensions of the C-ABI problem: nx, nu are the largest over the stages.
+// hpipm-cpp lets nx[i], nu[i] vary per stage (ocp_qp_dim.cpp:37-53); the C-ABI takes
+// uniform dimensions, so a stage with fewer states or inputs is embedded in the uniform
+// one (pack): its A, B rows / columns beyond its dimensions are zero, so those states stay
+// 0 and cost nothing, and its extra inputs get R = 1 on the diagonal (u = 0 there) -- the
+// same embedding pad.hip applies below 12 x 12.  The solution is cut back per stage
+// (unpack).
 struct Shape {
   int N = 0, nx = 0, nu = 0, ng = 0;
   bool box_u = false, box_x = false;
@@ -62,17 +80,9 @@ struct Shape {
 Shape shape_of(const OcpQpDim& d) {
   Shape s;
   s.N = static_cast<int>(d.N);
-  s.nx = d.nx[0];
-  s.nu = d.N > 0 ? d.nu[0] : 0;
   for (unsigned int i = 0; i <= d.N; ++i) {
-    if (d.nx[i] != s.nx)
-      throw std::runtime_error("OcpQpIpmSolver: nx must be uniform over the stages (nx[" +
-                               std::to_string(i) + "] = " + std::to_string(d.nx[i]) +
-                               ", nx[0] = " + std::to_string(s.nx) + ")");
-    if (i < d.N && d.nu[i] != s.nu)
-      throw std::runtime_error("OcpQpIpmSolver: nu must be uniform over the stages (nu[" +
-                               std::to_string(i) + "] = " + std::to_string(d.nu[i]) +
-                               ", nu[0] = " + std::to_string(s.nu) + ")");
+    s.nx = std::max(s.nx, d.nx[i]);
+    if (i < d.N) s.nu = std::max(s.nu, d.nu[i]);
     if (d.nsbx[i] != 0 || d.nsbu[i] != 0 || d.nsg[i] != 0)
       throw std::runtime_error("OcpQpIpmSolver: soft constraints are not supported");
     s.ng = std::max(s.ng, d.ng[i]);
@@ -229,29 +239,33 @@ void OcpQpIpmSolver::Impl::pack(const std::vector<VectorXd>& x0s,
     sized(D, nb * N * ng * nu);
     for (auto* v : {&lg, &ug, &lg_m, &ug_m}) sized(*v, nb * (N + 1) * ng);
   }
+  const size_t nx0 = static_cast<size_t>(dim.nx[0]);
   for (size_t bi = 0; bi < nb; ++bi) {
     const std::vector<OcpQp>& qp = qps[bi];
-    if (static_cast<size_t>(x0s[bi].size()) != nx)
-      throw std::runtime_error("x0.size() must be " + std::to_string(nx));
-    copy_block(x0, bi * nx, x0s[bi].data(), nx);
+    if (static_cast<size_t>(x0s[bi].size()) != nx0)
+      throw std::runtime_error("x0.size() must be " + std::to_string(nx0));
+    copy_block(x0, bi * nx, x0s[bi].data(), nx0);
     for (size_t k = 0; k <= N; ++k) {
       const OcpQp& s = qp[k];
       const size_t sk = bi * (N + 1) + k;  // stage index, N+1 stages
-      copy_block(Q, sk * nx * nx, s.Q.data(), nx * nx);
-      copy_block(q, sk * nx, s.q.data(), nx);
+      const size_t xk = static_cast<size_t>(dim.nx[k]);  // this stage's dimensions
+      copy_mat(Q, sk * nx * nx, nx, s.Q.data(), xk, xk);
+      copy_block(q, sk * nx, s.q.data(), xk);
       if (k < N) {
         const size_t si = bi * N + k;  // stage index, N stages
-        copy_block(A, si * nx * nx, s.A.data(), nx * nx);
-        copy_block(B, si * nx * nu, s.B.data(), nx * nu);
-        copy_block(b, si * nx, s.b.data(), nx);
-        copy_block(S, si * nu * nx, s.S.data(), nu * nx);
-        copy_block(R, si * nu * nu, s.R.data(), nu * nu);
-        copy_block(r, si * nu, s.r.data(), nu);
+        const size_t uk = static_cast<size_t>(dim.nu[k]), xn = static_cast<size_t>(dim.nx[k + 1]);
+        copy_mat(A, si * nx * nx, nx, s.A.data(), xn, xk);
+        copy_mat(B, si * nx * nu, nx, s.B.data(), xn, uk);
+        copy_block(b, si * nx, s.b.data(), xn);
+        copy_mat(S, si * nu * nx, nu, s.S.data(), uk, xk);
+        copy_mat(R, si * nu * nu, nu, s.R.data(), uk, uk);
+        for (size_t j = uk; j < nu; ++j) R[si * nu * nu + j * nu + j] = 1.0;  // embedded inputs
+        copy_block(r, si * nu, s.r.data(), uk);
         if (shape.box_u) {
           // index form -> dense per-variable bounds + masks (include/srbd_qp.h)
           for (size_t j = 0; j < s.idxbu.size(); ++j) {
             const int v = s.idxbu[j];
-            if (v < 0 || static_cast<size_t>(v) >= nu)
+            if (v < 0 || static_cast<size_t>(v) >= uk)
               throw std::runtime_error("ocp_qp[" + std::to_string(k) + "].idxbu[" +
                                        std::to_string(j) + "] out of range");
             const size_t o = si * nu + v;
@@ -263,16 +277,13 @@ void OcpQpIpmSolver::Impl::pack(const std::vector<VectorXd>& x0s,
         }
         if (ng && s.D.size()) {
           // pad to ng rows: column-major ng x nu block, extra rows stay 0
-          const size_t rows = s.D.rows();
-          for (size_t c = 0; c < nu; ++c)
-            for (size_t rr = 0; rr < rows; ++rr)
-              D[si * ng * nu + c * ng + rr] = s.D.data()[c * rows + rr];
+          copy_mat(D, si * ng * nu, ng, s.D.data(), static_cast<size_t>(s.D.rows()), uk);
         }
       }
       if (shape.box_x && k > 0) {
         for (size_t j = 0; j < s.idxbx.size(); ++j) {
           const int v = s.idxbx[j];
-          if (v < 0 || static_cast<size_t>(v) >= nx)
+          if (v < 0 || static_cast<size_t>(v) >= xk)
             throw std::runtime_error("ocp_qp[" + std::to_string(k) + "].idxbx[" +
                                      std::to_string(j) + "] out of range");
           const size_t o = sk * nx + v;
@@ -284,11 +295,7 @@ void OcpQpIpmSolver::Impl::pack(const std::vector<VectorXd>& x0s,
       }
       if (ng) {
         const size_t rows = s.lg.size();
-        if (rows && s.C.size()) {
-          for (size_t c = 0; c < nx; ++c)
-            for (size_t rr = 0; rr < rows; ++rr)
-              C[sk * ng * nx + c * ng + rr] = s.C.data()[c * rows + rr];
-        }
+        if (rows && s.C.size()) copy_mat(C, sk * ng * nx, ng, s.C.data(), rows, xk);
         for (size_t rr = 0; rr < rows; ++rr) {
           const size_t o = sk * ng + rr;
           lg[o] = s.lg[rr];
@@ -316,8 +323,8 @@ void OcpQpIpmSolver::Impl::pack(const std::vector<VectorXd>& x0s,
     for (size_t bi = 0; bi < nb; ++bi) {
       const std::vector<OcpQpSolution>& w = (*warm)[bi];
       for (size_t kk = 0; kk < N; ++kk) {
-        copy_block(x, (bi * (N + 1) + kk + 1) * nx, w[kk + 1].x.data(), nx);
-        copy_block(u, (bi * N + kk) * nu, w[kk].u.data(), nu);
+        copy_block(x, (bi * (N + 1) + kk + 1) * nx, w[kk + 1].x.data(), static_cast<size_t>(dim.nx[kk + 1]));
+        copy_block(u, (bi * N + kk) * nu, w[kk].u.data(), static_cast<size_t>(dim.nu[kk]));
       }
     }
   }
@@ -334,22 +341,23 @@ std::vector<HpipmStatus> OcpQpIpmSolver::Impl::unpack(
     for (size_t kk = 0; kk <= N; ++kk) {
       OcpQpSolution& s = sol[kk];
       const size_t sk = bi * (N + 1) + kk;
-      s.x.resize(nx);
-      s.pi.resize(nx);
-      s.P.resize(nx, nx);
-      s.p.resize(nx);
-      std::memcpy(s.x.data(), x.data() + sk * nx, nx * sizeof(double));
-      std::memcpy(s.pi.data(), pi.data() + sk * nx, nx * sizeof(double));
-      std::memcpy(s.P.data(), P.data() + sk * nx * nx, nx * nx * sizeof(double));
-      std::memcpy(s.p.data(), p.data() + sk * nx, nx * sizeof(double));
+      const size_t xk = static_cast<size_t>(dim.nx[kk]);  // the stage's own dimensions
+      s.x.resize(xk);
+      s.pi.resize(xk);
+      s.P.resize(xk, xk);
+      s.p.resize(xk);
+      std::memcpy(s.x.data(), x.data() + sk * nx, xk * sizeof(double));
+      std::memcpy(s.pi.data(), pi.data() + sk * nx, xk * sizeof(double));
+      take_mat(s.P.data(), P.data() + sk * nx * nx, nx, xk, xk);
+      std::memcpy(s.p.data(), p.data() + sk * nx, xk * sizeof(double));
       if (kk < N) {
-        const size_t si = bi * N + kk;
-        s.u.resize(nu);
-        s.K.resize(nu, nx);
-        s.k.resize(nu);
-        std::memcpy(s.u.data(), u.data() + si * nu, nu * sizeof(double));
-        std::memcpy(s.K.data(), K.data() + si * nu * nx, nu * nx * sizeof(double));
-        std::memcpy(s.k.data(), k.data() + si * nu, nu * sizeof(double));
+        const size_t si = bi * N + kk, uk = static_cast<size_t>(dim.nu[kk]);
+        s.u.resize(uk);
+        s.K.resize(uk, xk);
+        s.k.resize(uk);
+        std::memcpy(s.u.data(), u.data() + si * nu, uk * sizeof(double));
+        take_mat(s.K.data(), K.data() + si * nu * nx, nu, uk, xk);
+        std::memcpy(s.k.data(), k.data() + si * nu, uk * sizeof(double));
       } else {
         s.k.resize(0);  // nu[N] = 0 (ocp_qp_ipm_solver.cpp:221-223)
       }
@@ -438,9 +446,9 @@ std::vector<HpipmStatus> OcpQpIpmSolver::solveBatch(
   for (size_t bi = 1; bi < ocp_qp.size(); ++bi) {
     OcpQpDim d(ocp_qp[bi]);
     Shape si = shape_of(d);
-    if (si.N != s0.N || si.nx != s0.nx || si.nu != s0.nu)
+    if (d.N != m.dim.N || d.nx != m.dim.nx || d.nu != m.dim.nu)
       throw std::runtime_error("ocp_qp[" + std::to_string(bi) +
-                               "]: every QP of a batch must have the same N, nx, nu");
+                               "]: every QP of a batch must have the same N, nx[i], nu[i]");
     s.ng = std::max(s.ng, si.ng);
     s.box_u = s.box_u || si.box_u;
     s.box_x = s.box_x || si.box_x;
@@ -454,13 +462,13 @@ std::vector<HpipmStatus> OcpQpIpmSolver::solveBatch(
     if (sol.size() != static_cast<size_t>(s.N) + 1) sol.resize(s.N + 1);
     if (m.settings.warm_start) {
       for (int i = 0; i <= s.N; ++i)
-        if (sol[i].x.size() != s.nx)
+        if (sol[i].x.size() != m.dim.nx[i])
           throw std::runtime_error("qp_sol[" + std::to_string(i) + "].x.size() must be " +
-                                   std::to_string(s.nx));
+                                   std::to_string(m.dim.nx[i]));
       for (int i = 0; i < s.N; ++i)
-        if (sol[i].u.size() != s.nu)
+        if (sol[i].u.size() != m.dim.nu[i])
           throw std::runtime_error("qp_sol[" + std::to_string(i) + "].u.size() must be " +
-                                   std::to_string(s.nu));
+                                   std::to_string(m.dim.nu[i]));
     }
   }
   m.pack(x0, ocp_qp, m.settings.warm_start ? &qp_sol : nullptr);

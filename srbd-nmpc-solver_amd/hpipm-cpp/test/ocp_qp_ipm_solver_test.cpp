@@ -319,6 +319,153 @@ TEST(batch_matches_single, true) {
   }
 }
 
+// Stage-varying dimensions (OcpQpDim allows nx[i], nu[i] per stage,
+// hpipm-cpp/src/ocp_qp_dim.cpp:37-53): A_i is nx[i+1] x nx[i], B_i nx[i+1] x nu[i].
+RandomQp random_varying_qp(const std::vector<int>& nxs, const std::vector<int>& nus) {
+  const unsigned N = static_cast<unsigned>(nxs.size() - 1);
+  RandomQp p;
+  p.qp.resize(N + 1);
+  for (unsigned i = 0; i < N; ++i) {
+    const int nx = nxs[i], nu = nus[i], nn = nxs[i + 1];
+    p.qp[i].A = Random(nn, nx);
+    p.qp[i].B = Random(nn, nu);
+    p.qp[i].b = RandomVec(nn);
+    const MatrixXd H = Random(nx + nu, nx + nu);
+    const MatrixXd HH = H * H.transpose();
+    p.qp[i].Q = block(HH, nu, nu, nx, nx);
+    p.qp[i].S = block(HH, 0, nu, nu, nx);
+    p.qp[i].R = block(HH, 0, 0, nu, nu);
+    const VectorXd d = AbsRandomVec(nu);
+    for (int j = 0; j < nu; ++j) p.qp[i].R(j, j) += d(j);
+    p.qp[i].q = RandomVec(nx);
+    p.qp[i].r = RandomVec(nu);
+  }
+  const MatrixXd H = Random(nxs[N], nxs[N]);
+  p.qp[N].Q = H * H.transpose();
+  p.qp[N].q = RandomVec(nxs[N]);
+  p.x0 = RandomVec(nxs[0]);
+  return p;
+}
+
+const std::vector<int> kVaryNx = {4, 6, 3, 5, 6, 2, 4, 5, 6, 4, 3};
+const std::vector<int> kVaryNu = {2, 3, 1, 3, 2, 2, 3, 1, 2, 3};
+
+// unconstrained, nx / nu varying per stage: the textbook recursion (reference test
+// :60-90, rectangular A, B) at the reference's 1e-10, on both Riccati variants
+TEST(varying_dims, true) {
+  for (int ric = 0; ric <= 1; ++ric) {
+    RandomQp p = random_varying_qp(kVaryNx, kVaryNu);
+    const unsigned N = static_cast<unsigned>(kVaryNx.size() - 1);
+    hpipm::OcpQpIpmSolverSettings settings;
+    settings.mode = hpipm::HpipmMode::Balance;
+    settings.ric_alg = ric;
+    std::vector<hpipm::OcpQpSolution> sol(N + 1);
+    hpipm::OcpQpIpmSolver solver(p.qp, settings);
+    EXPECT_EQ(solver.solve(p.x0, p.qp, sol), hpipm::HpipmStatus::Success);
+    std::vector<MatrixXd> P(N + 1), K(N);
+    std::vector<VectorXd> s(N + 1), k(N);
+    P[N] = p.qp[N].Q;
+    s[N] = -1.0 * p.qp[N].q;
+    for (int i = static_cast<int>(N) - 1; i >= 0; --i) {
+      const hpipm::OcpQp& q = p.qp[i];
+      const MatrixXd At = q.A.transpose(), Bt = q.B.transpose();
+      const MatrixXd F = q.Q + At * P[i + 1] * q.A;
+      const MatrixXd H = q.S + Bt * P[i + 1] * q.A;
+      const MatrixXd G = q.R + Bt * P[i + 1] * q.B;
+      const MatrixXd Ginv = inverse(G);
+      K[i] = -1.0 * (Ginv * H);
+      k[i] = -1.0 * (Ginv * (Bt * P[i + 1] * q.b - Bt * s[i + 1] + q.r));
+      P[i] = F - K[i].transpose() * G * K[i];
+      s[i] = At * (s[i + 1] - P[i + 1] * q.b) - q.q - H.transpose() * k[i];
+    }
+    std::vector<VectorXd> x(N + 1), u(N);
+    x[0] = p.x0;
+    for (unsigned i = 0; i < N; ++i) {
+      u[i] = K[i] * x[i] + k[i];
+      x[i + 1] = p.qp[i].A * x[i] + p.qp[i].B * u[i] + p.qp[i].b;
+    }
+    const double prec = 1.0e-10;
+    for (unsigned i = 0; i <= N; ++i) {
+      EXPECT_EQ(sol[i].x.size(), static_cast<long>(kVaryNx[i]));
+      EXPECT_TRUE(x[i].isApprox(sol[i].x, prec));
+      EXPECT_TRUE(VectorXd(P[i] * x[i] - s[i]).isApprox(sol[i].pi, prec));
+      EXPECT_TRUE(P[i].isApprox(sol[i].P, prec));
+      EXPECT_TRUE(s[i].isApprox(-1.0 * sol[i].p, prec));
+    }
+    for (unsigned i = 0; i < N; ++i) {
+      EXPECT_EQ(sol[i].u.size(), static_cast<long>(kVaryNu[i]));
+      EXPECT_TRUE(u[i].isApprox(sol[i].u, prec));
+      EXPECT_TRUE(K[i].isApprox(sol[i].K, prec));
+      EXPECT_TRUE(k[i].isApprox(sol[i].k, prec));
+    }
+  }
+}
+
+// box-constrained with varying dims: the IPM solution equals that of the same problem
+// embedded by hand in uniform dimensions (zero A / B rows and columns, R = 1 on the
+// extra inputs) -- the embedding stays exact through the IPM.
+TEST(varying_dims_constrained, true) {
+  RandomQp p = random_varying_qp(kVaryNx, kVaryNu);
+  const unsigned N = static_cast<unsigned>(kVaryNx.size() - 1);
+  const int NX = 6, NU = 3;
+  for (unsigned i = 0; i < N; ++i) {
+    p.qp[i].A = (0.9 / std::max(1.0, norm2(p.qp[i].A))) * p.qp[i].A;
+    p.qp[i].idxbu = {0};
+    p.qp[i].lbu = VectorXd::Constant(1, -0.1);
+    p.qp[i].ubu = VectorXd::Constant(1, 0.1);
+  }
+  std::vector<hpipm::OcpQp> pad(N + 1);
+  for (unsigned i = 0; i <= N; ++i) {
+    const int nx = kVaryNx[i];
+    pad[i].Q = MatrixXd::Zero(NX, NX);
+    pad[i].q = VectorXd::Zero(NX);
+    for (int c = 0; c < nx; ++c) {
+      pad[i].q(c) = p.qp[i].q(c);
+      for (int r = 0; r < nx; ++r) pad[i].Q(r, c) = p.qp[i].Q(r, c);
+    }
+    if (i == N) continue;
+    const int nu = kVaryNu[i], nn = kVaryNx[i + 1];
+    pad[i].A = MatrixXd::Zero(NX, NX);
+    pad[i].B = MatrixXd::Zero(NX, NU);
+    pad[i].b = VectorXd::Zero(NX);
+    pad[i].S = MatrixXd::Zero(NU, NX);
+    pad[i].R = MatrixXd::Zero(NU, NU);
+    pad[i].r = VectorXd::Zero(NU);
+    for (int r = 0; r < nn; ++r) {
+      pad[i].b(r) = p.qp[i].b(r);
+      for (int c = 0; c < nx; ++c) pad[i].A(r, c) = p.qp[i].A(r, c);
+      for (int c = 0; c < nu; ++c) pad[i].B(r, c) = p.qp[i].B(r, c);
+    }
+    for (int r = 0; r < nu; ++r) {
+      pad[i].r(r) = p.qp[i].r(r);
+      for (int c = 0; c < nx; ++c) pad[i].S(r, c) = p.qp[i].S(r, c);
+      for (int c = 0; c < nu; ++c) pad[i].R(r, c) = p.qp[i].R(r, c);
+    }
+    for (int j = nu; j < NU; ++j) pad[i].R(j, j) = 1.0;
+    pad[i].idxbu = p.qp[i].idxbu;
+    pad[i].lbu = p.qp[i].lbu;
+    pad[i].ubu = p.qp[i].ubu;
+  }
+  VectorXd x0p = VectorXd::Zero(NX);
+  for (int j = 0; j < kVaryNx[0]; ++j) x0p(j) = p.x0(j);
+  hpipm::OcpQpIpmSolverSettings settings;
+  settings.iter_max = 40;
+  std::vector<hpipm::OcpQpSolution> sol, solp;
+  hpipm::OcpQpIpmSolver a(settings), b(settings);
+  EXPECT_EQ(a.solve(p.x0, p.qp, sol), hpipm::HpipmStatus::Success);
+  EXPECT_EQ(b.solve(x0p, pad, solp), hpipm::HpipmStatus::Success);
+  EXPECT_EQ(a.getSolverStatistics().iter, b.getSolverStatistics().iter);
+  for (unsigned i = 0; i <= N; ++i) {
+    for (int j = 0; j < kVaryNx[i]; ++j) EXPECT_TRUE(std::abs(sol[i].x(j) - solp[i].x(j)) < 1e-9);
+    if (i < N)
+      for (int j = 0; j < kVaryNu[i]; ++j) {
+        EXPECT_TRUE(std::abs(sol[i].u(j) - solp[i].u(j)) < 1e-9);
+        EXPECT_TRUE(sol[i].u(j) >= -0.1 - 1e-8 || j > 0);
+        EXPECT_TRUE(sol[i].u(j) <= 0.1 + 1e-8 || j > 0);
+      }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // CPU tests: interface errors, raised before any device work
 // ---------------------------------------------------------------------------
@@ -392,15 +539,19 @@ TEST(unsupported_shapes, false) {
   RandomQp p = random_qp(4, 2, 5, true);
   std::vector<hpipm::OcpQpSolution> sol;
   {
-    auto bad = p.qp;  // nx[3] = 3, all other stages 4
-    bad[3].Q = Random(3, 3);
-    bad[3].q = RandomVec(3);
-    bad[3].A = Random(4, 3);
-    bad[3].S = Random(2, 3);
-    bad[2].A = Random(3, 4);
-    bad[2].B = Random(3, 2);
-    bad[2].b = RandomVec(3);
-    EXPECT_THROW_MSG(solver.solve(p.x0, bad, sol), "nx must be uniform");
+    // a batch whose QPs differ in their per-stage dimensions
+    auto other = p.qp;  // nx[3] = 3, all other stages 4
+    other[3].Q = Random(3, 3);
+    other[3].q = RandomVec(3);
+    other[3].A = Random(4, 3);
+    other[3].S = Random(2, 3);
+    other[2].A = Random(3, 4);
+    other[2].B = Random(3, 2);
+    other[2].b = RandomVec(3);
+    std::vector<std::vector<hpipm::OcpQp>> qps{p.qp, other};
+    std::vector<VectorXd> x0s{p.x0, p.x0};
+    std::vector<std::vector<hpipm::OcpQpSolution>> sols;
+    EXPECT_THROW_MSG(solver.solveBatch(x0s, qps, sols), "same N, nx[i], nu[i]");
   }
   {
     auto bad = p.qp;

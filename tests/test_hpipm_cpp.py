@@ -15,7 +15,7 @@ EXE = ROOT / "build" / "hpipm_cpp_test"
 GOLDEN = ROOT / "tests" / "golden"
 
 GPU_CASES = ["unconstrained", "constrained_box", "constrained", "compareResults",
-             "batch_matches_single"]
+             "batch_matches_single", "varying_dims", "varying_dims_constrained"]
 
 
 def _run(args, timeout):
