@@ -724,7 +724,6 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
   hipError_t e = hipSuccess;
   if (off > h->stage_bytes) {
     if (h->stage) hipFree(h->stage);
-  if (h->pinned) hipHostFree(h->pinned);
     h->stage = nullptr;
     h->stage_bytes = 0;
     e = hipMalloc(reinterpret_cast<void**>(&h->stage), off);

@@ -109,6 +109,28 @@ def test_host_entry_point_matches_device(pkg):
     assert np.all(st == 0)
 
 
+def test_host_staging_growth_keeps_pinned_mirror(pkg):
+    """One handle serves host solves of 1, 64 and 1 QPs: the device staging buffer grows on
+    the second call and the pinned mirror with it; every result equals the device call's.
+    (Growing the device staging once also freed the pinned mirror without forgetting it, so
+    the third call staged through freed host memory.)"""
+    capi = pkg.capi
+    qp, x0 = helpers.random_unconstrained(64, 20, 12, 12, 31, pkg.OcpQpBatch)
+    dev = capi.solve(qp, x0)
+    h = capi.Handle(20, 12, 12, capacity=64)
+    try:
+        for b in (1, 64, 1):
+            p = {k: (None if v is None else np.ascontiguousarray(v[:b])) for k, v in qp.packed().items()}
+            p["x0"] = np.ascontiguousarray(x0[:b])
+            out = {k: np.zeros_like(dev[k][:b]) for k in ("x", "u", "pi", "status")}
+            data = capi.Data(**{k: (None if p.get(k) is None else p[k].ctypes.data) for k in capi.DATA_FIELDS})
+            h.solve_host(b, capi.settings_struct(), data, capi.Solution(**{k: v.ctypes.data for k, v in out.items()}))
+            for key in out:
+                assert np.array_equal(out[key], dev[key][:b]), (b, key)
+    finally:
+        h.close()
+
+
 @pytest.mark.parametrize("ric_alg", [0, 1])
 def test_srbd_qps_vs_oracle(pkg, oracle, ric_alg):
     """The reference's own QP: SRBD NMPC linearisation (N=20, nx=nu=12); its Q has
