@@ -452,6 +452,10 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   c.blg = a.lg; c.bug = a.ug; c.blgm = a.lg_mask; c.bugm = a.ug_mask;
   c.bxo = a.x; c.buo = a.u; c.bpi = a.pi; c.bws = a.ws;
   const real reg = a.reg;
+  // precision of the stage factorization G = R + D'Gamma D + B'PB (riccati.h chol_g):
+  // double in the fp32 kernels with C-free general rows (the friction cone), whose fp32
+  // factorization broke down on the cone's Gamma of 1e8-1e10
+  using greal = std::conditional_t<sizeof(real) == 4 && GEN == 1, double, real>;
   // (P x)_col + acc for an element-owned x (lane j holds x_j), P from a stage record's kRecP
   // slot: packed P (ric_alg 0) or its factor Lp (ric_alg 1)
   auto rec_P_mul = [&](const real* rec, real xv, real acc) -> real {
@@ -945,8 +949,12 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       // (GEN == 1) the Hessian add D'Gamma D, accumulated for the factorization
       real gra = real(0.0), gqa = real(0.0);  // D'gamma, C'gamma (lane j)
       real gea = real(0.0);                   // D'e, e = d gamma / d(sigma mu) (GEN == 1)
-      real RG[12];                            // D'Gamma D, column j (GEN == 1)
-      sfor<0, 12>([&](auto i) { RG[decltype(i)::value] = real(0.0); });
+      // D'Gamma D, column j (GEN == 1); in double (fp32 kernel) it waits for the
+      // factorization in this lane's LDS slots rather than in 24 registers
+      constexpr bool kRgLds = !std::is_same_v<greal, real>;
+      __shared__ greal rg_lds[kRgLds ? 12 * 256 : 1];
+      greal RG[12];
+      sfor<0, 12>([&](auto i) { RG[decltype(i)::value] = greal(0.0); });
       if constexpr (GEN) {
         for (int ch = 0; ch < c.nch; ++ch) {
           real* g = c.gs(k, ch);
@@ -1010,14 +1018,20 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             gea = dot_bcast(Dc, e, gea);
           }
           if constexpr (GEN == 1) {
-            // D'Gamma D from sqrt(Gamma) D: exactly symmetric (see g_hess)
-            real Gb[12];
-            gather12(__builtin_sqrt(G), Gb);
+            // D'Gamma D from sqrt(Gamma) D: exactly symmetric (see g_hess); formed in greal
+            const greal sG = __builtin_sqrt(greal(G));
+            greal Dg[12];
             sfor<0, 12>([&](auto i) {
               constexpr int I = decltype(i)::value;
-              Dc[I] *= Gb[I];
+              Dg[I] = greal(Dc[I]) * bc<I>(sG);
             });
-            tmul_acc(Dc, Dc, RG);
+            if constexpr (kRgLds) {
+              if (ch > 0) sfor<0, 12>([&](auto i) { RG[decltype(i)::value] = rg_lds[decltype(i)::value * 256 + threadIdx.x]; });
+              tmul_acc(Dg, Dg, RG);
+              sfor<0, 12>([&](auto i) { rg_lds[decltype(i)::value * 256 + threadIdx.x] = RG[decltype(i)::value]; });
+            } else {
+              tmul_acc(Dg, Dg, RG);
+            }
           }
         }
       }
@@ -1145,20 +1159,19 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         });
         SRBD_PHASE_FENCE();
         real rt = real(0.0);
-        auto loadR = [&](real (&Rc)[12]) {
-          c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, Rc);
-          const real ru = dot_bcast(Rc, uk, real(0.0));  // R u, before the barrier Hessian goes in
+        auto loadR = [&](greal (&Rc)[12]) {
+          real Rr[12];
+          c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, Rr);
+          const real ru = dot_bcast(Rr, uk, real(0.0));  // R u, before the barrier Hessian goes in
           objl += uk * (real(0.5) * ru + rk + sxu);
           rt = finish_u(rgu + ru);
-          if constexpr (GEN == 1) {
-            sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] += RG[decltype(i)::value]; });
-          } else if constexpr (GEN == 2) {
-            g_hess(k, 0, Rc, Rc);
-          }
+          if constexpr (GEN == 2) g_hess(k, 0, Rr, Rr);
           sfor<0, 12>([&](auto i) {
             constexpr int I = decltype(i)::value;
-            if (lane == I) Rc[I] += (I < nu) ? Gu : real(1.0);  // padded inputs: R = 1
-            if (c.isv) Rc[I] = real(0.0);
+            Rc[I] = greal(Rr[I]);
+            if constexpr (GEN == 1) Rc[I] += greal(kRgLds ? rg_lds[I * 256 + threadIdx.x] : RG[I]);
+            if (lane == I) Rc[I] += (I < nu) ? greal(Gu) : greal(1.0);  // padded inputs: R = 1
+            if (c.isv) Rc[I] = greal(0.0);
           });
         };
         auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
@@ -1180,9 +1193,9 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         };
         StageFactor<real> f;
         if constexpr (SQRT) {
-          riccati_step_sqrt(P, A_, B_, loadR, loadSQ, lane, reg, f);
+          riccati_step_sqrt<1, false, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f);
         } else {
-          riccati_step<1, true>(P, A_, B_, loadR, loadSQ, lane, reg, f);  // P_k symmetrized
+          riccati_step<1, true, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f);  // P_k symmetrized
         }
         if (lane < kMaxDim) {
           store_packed_col(rec + kRecL, lane, f.Lc);
@@ -1528,7 +1541,9 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 
 // fp64: 2 workgroups per CU (<= 256 VGPRs); fp32 boxes / C-free rows: 3 (<= 168 VGPRs, 3 waves
 // per SIMD -- the fp32 RB sweep sits just under that cliff and a free allocator crosses it:
-// cone 175 -> 194 ms); fp32 rows with C need 216 and stay at 2
+// cone 175 -> 194 ms; with the fp64 stage factorization of C-free rows the sweep needs 178
+// and spills 60-76 B at 168, still faster than 2 waves: cone 188.6 vs 205.7 ms); fp32 rows
+// with C need 216 and stay at 2
 template <int GEN>
 constexpr int kIpmMinBlocks = sizeof(real) == 4 && GEN < 2 ? 3 : 2;
 

@@ -128,6 +128,41 @@ struct StageFactor {
   T Kc[12];  // K column (VL: k)
 };
 
+template <typename TO, typename TI>
+__device__ __forceinline__ void convert12(const TI (&in)[12], TO (&out)[12]) {
+  sfor<0, 12>([&](auto i) { out[decltype(i)::value] = TO(in[decltype(i)::value]); });
+}
+
+// G (in TG) -> the stage's factor L (o.Lc, o.rs, in T).  TG = double in the fp32 IPM
+// with general rows: with the friction cone's Gamma of 1e8-1e10 on active rows, R (1e-2)
+// is below the fp32 rounding of D'Gamma D, and G must be formed and factorized in fp64
+// to keep it; the triangular solves with the rounded factor are
+// backward stable entry by entry and stay in fp32.
+template <typename TG, typename T>
+__device__ __forceinline__ void chol_g(TG (&G)[12], const int lane, const T reg, StageFactor<T>& o) {
+  if constexpr (std::is_same_v<TG, T>) {
+    chol_cols(G, lane, reg, o.Lc, o.rs);
+  } else {
+    TG rsg;
+    chol_cols(G, lane, TG(reg), G, rsg);  // (in place)
+    convert12(G, o.Lc);
+    o.rs = T(rsg);
+  }
+}
+
+// C += X'Y with C in TG and X, Y in T (widened first when the precisions differ)
+template <typename TG, typename T>
+__device__ __forceinline__ void tmul_acc_g(const T (&X)[12], const T (&Y)[12], TG (&C)[12]) {
+  if constexpr (std::is_same_v<TG, T>) {
+    tmul_acc(X, Y, C);
+  } else {
+    sfor<0, 12>([&](auto kk) {
+      constexpr int K = decltype(kk)::value;
+      fma_bcast_lanes(C, TG(X[K]), TG(Y[K]));
+    });
+  }
+}
+
 struct NoMid {
   __device__ __forceinline__ void operator()() const {}
 };
@@ -199,23 +234,24 @@ __device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], const int
 // `mid` runs between the products and the triangular solves (MidAt = 1: P is
 // dead there) or after the solves (MidAt = 2: L is dead too): the caller may
 // issue the next stage's loads into registers of its own.
-template <int MidAt = 1, bool SYMP = false, typename T, typename LoadR, typename LoadSQ,
-          typename Mid = NoMid>
+template <int MidAt = 1, bool SYMP = false, typename TGin = void, typename T, typename LoadR,
+          typename LoadSQ, typename Mid = NoMid>
 __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&B_)[12],
                                              LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
                                              const T reg, StageFactor<T>& o, Mid&& mid = Mid{}) {
+  using TG = std::conditional_t<std::is_void_v<TGin>, T, TGin>;
   const bool isv = lane == kVecLane;
-  // ---- G = R + B'(P B), L = chol(G)
+  // ---- G = R + B'(P B), L = chol(G)  (loadR fills a TG column)
   {
     T WB[12];
     sfor<0, 12>([&](auto i) { WB[decltype(i)::value] = T(0); });
     sym_mul_col(P, B_, WB);
     SRBD_PHASE_FENCE();
-    T G[12];
+    TG G[12];
     loadR(G);
-    tmul_acc(B_, WB, G);
+    tmul_acc_g(B_, WB, G);
     SRBD_PHASE_FENCE();
-    chol_cols(G, lane, reg, o.Lc, o.rs);
+    chol_g(G, lane, reg, o);
   }
   SRBD_PHASE_FENCE();
   // ---- W = P [A | b] (+ p on VL); H = S + B'W; F = Q + A'W
@@ -250,11 +286,13 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
 //   G = R + MB'MB,  H = S + MB'MA,  F = Q + MA'MA,  g = r + MB'm,  f = q + MA'm
 // -- in exact arithmetic the classical B'PB, B'PA, A'PA, B'(Pb + p), A'(Pb + p) --
 // then the common tail.  The caller continues the recursion with sqrt_factor(P_k).
-template <int MidAt = 1, bool SYMP = false, typename T, typename LoadR, typename LoadSQ,
-          typename Mid = NoMid>
+template <int MidAt = 1, bool SYMP = false, typename TGin = void, typename T, typename LoadR,
+          typename LoadSQ, typename Mid = NoMid>
 __device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12], T (&B_)[12],
                                                   LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
-                                                  const T reg, StageFactor<T>& o, Mid&& mid = Mid{}) {
+                                                  const T reg, StageFactor<T>& o,
+                                                  Mid&& mid = Mid{}) {
+  using TG = std::conditional_t<std::is_void_v<TGin>, T, TGin>;
   const bool isv = lane == kVecLane;
   // ---- MB = Lp'B (VL: 0, its B_ column is 0); G = R + MB'MB, L = chol(G)
   T MB[12];
@@ -262,11 +300,11 @@ __device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12]
   tmul_acc(Lp, B_, MB);
   SRBD_PHASE_FENCE();
   {
-    T G[12];
+    TG G[12];
     loadR(G);
-    tmul_acc(MB, MB, G);
+    tmul_acc_g(MB, MB, G);
     SRBD_PHASE_FENCE();
-    chol_cols(G, lane, reg, o.Lc, o.rs);
+    chol_g(G, lane, reg, o);
   }
   SRBD_PHASE_FENCE();
   // ---- MA = Lp'[A | b] + [0 | s]; H = S + MB'MA; F = Q + MA'MA

@@ -59,6 +59,9 @@ struct srbd_qp_handle_s {
   int* resc_count_host = nullptr;  // pinned
   void* resc = nullptr;
   size_t resc_bytes = 0;
+  // the cold fp64 re-solve of rescued QPs the continuation left unsolved (first use)
+  void* resc2 = nullptr;
+  size_t resc2_bytes = 0;
   // settings.f32_iters: fp32 copy of the data, fp32 iterate, barrier state (first use)
   void* mixed = nullptr;
   size_t mixed_bytes = 0;
@@ -202,6 +205,7 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   if (h->nmpc_active_host) hipHostFree(h->nmpc_active_host);
   if (h->resc_idx) hipFree(h->resc_idx);
   if (h->resc) hipFree(h->resc);
+  if (h->resc2) hipFree(h->resc2);
   if (h->mixed) hipFree(h->mixed);
   if (h->resc_count_host) hipHostFree(h->resc_count_host);
   if (h->stream) hipStreamDestroy(h->stream);
@@ -249,6 +253,10 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
                              const int* status, hipStream_t strm, int* rc);
 static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                      const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s, hipStream_t strm);
+static int fallback_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                        const srbd_qp_data_f64* d, const srbd_qp_solution_f64* sc,
+                        const srbd_qp_solution_f64* s, hipStream_t strm, int min_status, int* idx,
+                        void** buf, size_t* buf_bytes);
 
 // warm_bars: warm_start 2 only (the fp64 continuation of rescue_f32), see ProblemArgsT;
 // iter_cap >= 0 (the f32_iters continuation): at most that many iterations, while the stat
@@ -461,8 +469,18 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
   srbd_qp_settings st64 = *st;
   st64.warm_start = cont ? 2 : 0;
   st64.f64_rescue = 0;
+  st64.f32_iters = 0;
   *rc = solve_impl<double>(h, R, &st64, &d64, &s64, strm, cont ? warm : nullptr);
   if (*rc) return hipSuccess;
+  // A QP the continuation leaves unsolved (an fp32 pass can end far off, with the barrier
+  // collapsed: t, lam -> 0 at a large stationarity residual, from where a warm-started IPM
+  // does not recover) is solved again cold in fp64 (its own list, buffer and idx slots:
+  // [capacity, 2 capacity) of resc_idx)
+  if (cont) {
+    *rc = fallback_f64(h, R, &st64, &d64, &s64, &s64, strm, 1, h->resc_idx + h->capacity, &h->resc2,
+                       &h->resc2_bytes);
+    if (*rc) return hipSuccess;
+  }
   hipSetDevice(h->device);
   for (const Out& f : outs)
     if (f.dst && e == hipSuccess) e = srbd::launch_scatter_narrow(*f.src, f.dst, idx, R, f.e, strm);
@@ -475,19 +493,20 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
 // ---------------------------------------------------------------------------
 // settings.f32_iters: mixed-precision IPM (fp32 iterations, then fp64 to the end)
 // ---------------------------------------------------------------------------
-// f32_iters: a QP the continuation leaves unsolved (status != Success) is solved again, cold,
-// in fp64 -- the mixed path never ends a QP worse than the fp64 path would
+// A QP a warm-started fp64 continuation ends with status >= min_status is solved again, cold,
+// in fp64 (compact batch in *buf, list in idx).  f32_iters: min_status 2 -- the mixed path
+// never ends a QP worse than the fp64 path would (numerical breakdowns: MinStepLengthReached,
+// NaNDetected; a MaxIterReached QP has spent the iteration budget, as the fp64 path would
+// have).  f64_rescue: min_status 1.
 static int fallback_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                         const srbd_qp_data_f64* d, const srbd_qp_solution_f64* sc,
-                        const srbd_qp_solution_f64* s, hipStream_t strm) {
+                        const srbd_qp_solution_f64* s, hipStream_t strm, int min_status, int* idx,
+                        void** buf, size_t* buf_bytes) {
   int prev = 0;
   hipGetDevice(&prev);
   hipSetDevice(h->device);
-  int* idx = h->resc_idx;
   int* count = h->resc_idx + 2 * (size_t)h->capacity;
-  // numerical breakdowns only (MinStepLengthReached, NaNDetected): a MaxIterReached QP has
-  // spent the iteration budget, as the fp64 path would have
-  hipError_t e = srbd::launch_select_unsolved(sc->status, batch, 2, idx, count, strm);
+  hipError_t e = srbd::launch_select_unsolved(sc->status, batch, min_status, idx, count, strm);
   if (e == hipSuccess) e = hipMemcpyAsync(h->resc_count_host, count, sizeof(int), hipMemcpyDeviceToHost, strm);
   if (e == hipSuccess) e = hipStreamSynchronize(strm);
   const int R = e == hipSuccess ? *h->resc_count_host : 0;
@@ -520,18 +539,18 @@ static int fallback_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   for (const In& f : ins) per_qp += f.src ? f.e : 0;
   for (const Out& f : outs) per_qp += f.dst ? f.e : 0;
   const size_t need = sizeof(double) * per_qp * (size_t)R + 2 * sizeof(int) * (size_t)R + 256;
-  if (need > h->resc_bytes) {
-    if (h->resc) hipFree(h->resc);
-    h->resc = nullptr;
-    h->resc_bytes = 0;
-    e = hipMalloc(&h->resc, need);
+  if (need > *buf_bytes) {
+    if (*buf) hipFree(*buf);
+    *buf = nullptr;
+    *buf_bytes = 0;
+    e = hipMalloc(buf, need);
     if (e != hipSuccess) {
       hipSetDevice(prev);
       return fail(SRBD_QP_ENOMEM, std::string("fallback batch: ") + hipGetErrorString(e));
     }
-    h->resc_bytes = need;
+    *buf_bytes = need;
   }
-  double* cur = reinterpret_cast<double*>(h->resc);
+  double* cur = reinterpret_cast<double*>(*buf);
   for (const In& f : ins) {
     if (!f.src || e != hipSuccess) continue;
     e = srbd::launch_gather_rows(f.src, cur, idx, R, f.e, strm);
@@ -649,7 +668,7 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   if (!sc.status) sc.status = h->resc_idx + h->capacity;
   rc = solve_impl<double>(h, batch, &st64, d, &sc, strm, warm, 0, st->iter_max - n32);
   if (rc) return rc;
-  return fallback_f64(h, batch, st, d, &sc, s, strm);
+  return fallback_f64(h, batch, st, d, &sc, s, strm, 2, h->resc_idx, &h->resc, &h->resc_bytes);
 }
 
 // ---------------------------------------------------------------------------

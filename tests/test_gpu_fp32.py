@@ -55,29 +55,32 @@ def test_friction_cone_fp32_vs_oracle(pkg, oracle):
     assert np.all(o32["res"][ok][:, 1:] <= 1e-3)
     # the fp32 KKT point at tol_stat 1e-2 differs from the fp64 one at 1e-4 by the
     # tolerance / curvature, not by rounding: bound the typical and the worst error
+    # (measured r03: median 2.9e-3 / max 1.2e-2 in u, 2.3e-3 / 1.5e-2 in x)
     ru = [np.linalg.norm(o32["u"][i] - ref["u"][i]) / np.linalg.norm(ref["u"][i])
           for i in np.nonzero(ok)[0]]
     rx = [np.linalg.norm(o32["x"][i] - ref["x"][i]) / np.linalg.norm(ref["x"][i])
           for i in np.nonzero(ok)[0]]
-    assert np.median(ru) <= 1e-2 and np.max(ru) <= 1e-1, (np.median(ru), np.max(ru))
-    assert np.median(rx) <= 1e-2 and np.max(rx) <= 1e-1, (np.median(rx), np.max(rx))
+    assert np.median(ru) <= 5e-3 and np.max(ru) <= 3e-2, (np.median(ru), np.max(ru))
+    assert np.median(rx) <= 5e-3 and np.max(rx) <= 3e-2, (np.median(rx), np.max(rx))
 
 
 def test_friction_cone_n40_fp32(pkg):
     """BASELINE config 5's problem class: N = 40, 24 friction-cone rows per stage;
-    status Success on >= 85 % of QPs at tol_stat 3e-2 (the rest stop at the
-    fp32 floor with MinStepLengthReached), fp64 reaches 1e-4 on all."""
+    status Success on >= 99 % of QPs at tol_stat 3e-2 with f64_rescue = 0 (the stage
+    factorization runs in fp64; before that 92.6 % here, the rest stopping
+    at the fp32 floor with MinStepLengthReached), fp64 reaches 1e-4 on all."""
     qp, x0 = pkg.srbd_model.generate_batch(256, N=40, seed=93, constraints="cone")
     st = dict(F32, tol_stat=3e-2)
     o32 = pkg.capi.solve(qp, x0, st, dtype=np.float32)
     o64 = pkg.capi.solve(qp, x0, NMPC)
     assert np.all(o64["status"] == 0)
-    assert np.mean(o32["status"] == 0) >= 0.85, np.bincount(o32["status"])
+    assert np.mean(o32["status"] == 0) >= 0.99, np.bincount(o32["status"])
     assert np.all(o32["status"] <= 2)  # no NaN at these settings
     ok = o32["status"] == 0
     ru = [np.linalg.norm(o32["u"][i] - o64["u"][i]) / np.linalg.norm(o64["u"][i])
           for i in np.nonzero(ok)[0]]
-    assert np.median(ru) <= 3e-2 and np.max(ru) <= 2e-1, (np.median(ru), np.max(ru))
+    # (measured r03: median 1.5e-3, max 7.2e-3)
+    assert np.median(ru) <= 3e-3 and np.max(ru) <= 2e-2, (np.median(ru), np.max(ru))
 
 
 def _rounded_to_f32(qp):
@@ -98,9 +101,12 @@ def test_f64_rescue_cone_n40(pkg, cap, stats, batch):
     the barrier state: HPIPM's warm_start = 2).  Every QP ends with status Success
     within the tolerances; the QPs fp32 solved keep their fp32 outputs bit for bit (an
     fp32 solve with iter_max = cap); the rescued ones land at the fp64 KKT point to the
-    accuracy the stationarity tolerance allows (the bound of test_friction_cone_n40_fp32)
-    in a few fp64 iterations.  batch 2500: the unsolved-QP list spans three ragged
-    1024-QP tiles of the selection kernel."""
+    accuracy the stationarity tolerance allows (the bound of test_friction_cone_n40_fp32),
+    each either continued in fewer fp64 iterations than its cold fp64 solve or -- when the
+    continuation does not converge (an fp32 pass can end with its barrier collapsed far
+    from the solution) -- solved again cold in fp64: then exactly the cold fp64 solve of
+    its fp32-rounded data.  batch 2500: the unsolved-QP list spans three ragged 1024-QP
+    tiles of the selection kernel."""
     qp, x0 = pkg.srbd_model.generate_batch(batch, N=40, seed=1005, constraints="cone")
     st = dict(F32, tol_stat=3e-2)
     plain = pkg.capi.solve(qp, x0, dict(st, iter_max=cap), dtype=np.float32, riccati=True,
@@ -120,9 +126,17 @@ def test_f64_rescue_cone_n40(pkg, cap, stats, batch):
     ru = [np.linalg.norm(resc["u"][i] - o64["u"][i]) / np.linalg.norm(o64["u"][i])
           for i in np.nonzero(bad)[0]]
     assert np.median(ru) <= 3e-2 and np.max(ru) <= 2e-1, (np.median(ru), np.max(ru))
-    # the continuation starts near the solution: far fewer iterations than a cold fp64 solve
-    assert resc["iter"][bad].mean() < 0.6 * o64["iter"][bad].mean(), (
-        resc["iter"][bad].mean(), o64["iter"][bad].mean())
+    # continued in fewer iterations than a cold fp64 solve, or re-solved cold
+    cold = pkg.capi.solve(_rounded_to_f32(qp), x0.astype(np.float32).astype(np.float64), st)
+    n_cont = 0
+    for i in np.nonzero(bad)[0]:
+        same = all(np.array_equal(resc[k][i], cold[k][i].astype(np.float32)) for k in ("x", "u", "pi"))
+        if not same:
+            assert resc["iter"][i] < o64["iter"][i], (i, resc["iter"][i], o64["iter"][i])
+            n_cont += 1
+        else:
+            assert resc["iter"][i] == cold["iter"][i], i
+    assert n_cont >= 1, "no rescued QP was continued"
 
 
 def test_f64_rescue_padded_is_a_cold_fp64_solve(pkg):

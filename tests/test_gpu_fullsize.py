@@ -214,7 +214,7 @@ def test_box_u_full_batch(pkg, oracle):
 
 def test_cone_n40_fp32_full_batch(pkg, oracle):
     """Config 5 (N = 40, friction-cone rows, fp32): the fp32 tolerances of DESIGN 4.5
-    are met by >= 90% of the batch, every solution is finite, satisfies the fp32
+    are met by >= 98.5% of the batch (99.1% measured, f64_rescue = 0), every solution is finite, satisfies the fp32
     dynamics to tol_eq and the cone rows to tol_ineq; windows stay within the fp32
     KKT tolerance of the fp64 oracle solution."""
     import torch
@@ -222,7 +222,7 @@ def test_cone_n40_fp32_full_batch(pkg, oracle):
     h, t = device_batch(pkg, N, "cone")
     s = solve_on_device(pkg, h, t, N, F32, dtype="f32")
     st = s["status"].cpu().numpy()
-    assert (st == 0).mean() >= 0.90, np.bincount(st)
+    assert (st == 0).mean() >= 0.985, np.bincount(st)
     assert set(np.unique(st)) <= {0, 1, 2}  # never NaNDetected
     for k in ("x", "u", "pi"):
         assert bool(torch.isfinite(s[k]).all()), k
@@ -244,7 +244,7 @@ def test_cone_n40_fp32_full_batch(pkg, oracle):
         ru += [np.linalg.norm(got[i] - ref["u"][i]) / np.linalg.norm(ref["u"][i])
                for i in np.nonzero(st[w] == 0)[0]]
     # the bound of tests/test_gpu_fp32.py (fp32 iterate at fp32 tolerances vs fp64 at 1e-4)
-    assert np.median(ru) <= 3e-2 and np.max(ru) <= 2e-1, (np.median(ru), np.max(ru))
+    assert np.median(ru) <= 3e-3 and np.max(ru) <= 2e-2, (np.median(ru), np.max(ru))
 
 
 def test_repeated_solves_bitwise_identical(pkg):
