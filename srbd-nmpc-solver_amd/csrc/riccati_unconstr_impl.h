@@ -5,7 +5,9 @@
 // blocks and forward records live:
 //   riccati_unconstr_kernel      (HbmSrc)  large batches: 16 lanes per QP, 16 QPs per
 //                                          workgroup; blocks streamed from HBM, records
-//                                          in the stage-major HBM workspace.
+//                                          in the stage-major HBM workspace (fp64: each
+//                                          wave writes its four records through an LDS
+//                                          image as whole 16-byte pieces).
 //   riccati_unconstr_lds_kernel  (LdsSrc)  small batches (the reference's one QP per
 //                                          solve() call): one QP per workgroup; the whole
 //                                          QP is first copied into an LDS image with
@@ -51,8 +53,15 @@ struct HbmSrc {
   __device__ const real* q(int k) const { return at(a.q, a.N + 1, 12, k); }
   __device__ const real* r(int k) const { return at(a.r, a.N, 12, k); }
   __device__ real* rec(int k) const { return a.ws + ((size_t)k * a.batch + qp) * kWsStage; }
+  // fp64 large-batch kernel: the wave's LDS image of its four QPs' records (null: plain
+  // stores)
+  real* img = nullptr;  // the wave's image base: group g's record at img + g * kWsStage
+  int gq = 0;           // QP group in the wave
+  template <class StoreRec>
+  __device__ void store_stage(int k, int lane, StoreRec&& store) const;
 };
 
+// forward declaration target; defined after store_rec below
 // LDS image of one QP: stage slot k (k = 0..N) holds the stage's blocks at the offsets
 // below (slot N: Q and q only); after the backward sweep has used slot k's blocks, the
 // stage's forward record (kernels.h kWs*, 402 reals) is written over them.
@@ -74,116 +83,93 @@ struct LdsSrc {
   __device__ real* rec(int k) const { return slot(k); }
 };
 
-// ---- the solve of one QP by its 16-lane group ----
-// SQRT: ric_alg = 1, the square-root recursion (riccati.h riccati_step_sqrt); the records
-// and outputs are the same (P_k = F - Y'Y of the stage, which Lx factors).
-template <bool SQRT, class Src>
-__device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src& src, const int qp,
-                                         const int lane) {
-  constexpr int nx = 12, nu = 12;
-  constexpr size_t nxx = 144, nxu = 144;
-  const int N = a.N;
+// ---- stage records ----
+// The terminal record (P_N, p_N) and, in solve_qp, every stage record by plain stores:
+// column owner j stores K[i][j] / Acl[i][j] at row i's slot j, the vector lane k[i] /
+// bcl[i] at slot 12 (kernels.h kWs*); P by packed columns (rows >= j), p on the vector lane.
+__device__ __forceinline__ void store_rec_P(real* rec, int lane, const real (&P)[12]) {
+  if (lane < kMaxDim) store_packed_col(rec + kWsP, lane, P);
+  if (lane == kVecLane) store12(rec + kWsp, P);
+}
+__device__ __forceinline__ void store_rec(real* rec, int lane, const real (&Kc)[12], const real (&Ac)[12],
+                                          const real (&P)[12]) {
   const bool isv = lane == kVecLane;
-  const bool own = lane < kMaxDim;  // lane owns a block column
-  const int col = own ? lane : kMaxDim - 1;
-  const real reg = a.reg;
-
-  // ---------------- terminal stage: P_N = Q_N, p_N = q_N ----------------
-  real P[12];
-  if (isv) {
-    load12(src.q(N), P);
-  } else {
-    load12(src.Q(N) + col * 12, P);
-  }
-  {
-    real* rec = src.rec(N);
-    if (own) store_packed_col(rec + kWsP, lane, P);
-    if (isv) store12(rec + kWsp, P);
-    if (a.P && own) store_n(a.P + ((size_t)qp * (N + 1) + N) * nxx + (size_t)lane * nx, nx, P);
-    if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + N) * nx, nx, P);
-  }
-  if constexpr (SQRT) sqrt_factor(P, lane);
-
-  // ---------------- backward sweep ----------------
-  real A_[12], B_[12];
-#pragma unroll 1
-  for (int k = N - 1; k >= 0; --k) {
-    // A, B (VL: b) of stage k, column-owned
-    if (isv) {
-      load12(src.b(k), A_);
-      sfor<0, 12>([&](auto i) { B_[decltype(i)::value] = real(0.0); });
-    } else {
-      load12(src.A(k) + col * 12, A_);
-      load12(src.B(k) + col * 12, B_);
-    }
-    auto loadR = [&](real (&Rc)[12]) {
-      if (isv) {
-        sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = real(0.0); });
-      } else {
-        load12(src.R(k) + col * 12, Rc);
-      }
-    };
-    auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
-      if (isv) {
-        load12(src.r(k), Sc);
-        load12(src.q(k), Qc);
-      } else {
-        load12(src.S(k) + col * 12, Sc);
-        load12(src.Q(k) + col * 12, Qc);
-      }
-    };
-    StageFactor<real> f;
-    if constexpr (SQRT) {
-      riccati_step_sqrt(P, A_, B_, loadR, loadSQ, lane, reg, f);
-    } else {
-      riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
-    }
-
-    real* rec = src.rec(k);
-    if (own) {
-      sfor<0, 12>([&](auto m) {
-        constexpr int M = decltype(m)::value;
-        rec[kWsK + M * 12 + lane] = f.Kc[M];
-        rec[kWsAcl + M * 12 + lane] = A_[M];
-      });
-      store_packed_col(rec + kWsP, lane, f.F);
-    }
-    if (isv) {
-      store12(rec + kWsk, f.Kc);
-      store12(rec + kWsbcl, A_);
-      store12(rec + kWsp, f.F);
-    }
-    if (a.P && own) store_n(a.P + ((size_t)qp * (N + 1) + k) * nxx + (size_t)lane * nx, nx, f.F);
-    if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + k) * nx, nx, f.F);
-    if (a.K && own) store_n(a.K + ((size_t)qp * N + k) * nxu + (size_t)lane * nu, nu, f.Kc);
-    if (a.k && isv) store_n(a.k + ((size_t)qp * N + k) * nu, nu, f.Kc);
-    sfor<0, 12>([&](auto i) {
-      constexpr int I = decltype(i)::value;
-      P[I] = f.F[I];
+  if (lane < kMaxDim || isv) {
+    const int c = isv ? kMaxDim : lane;
+    sfor<0, 12>([&](auto m) {
+      constexpr int M = decltype(m)::value;
+      rec[kWsK + M * kWsRow + c] = Kc[M];
+      rec[kWsAcl + M * kWsRow + c] = Ac[M];
     });
-    if constexpr (SQRT) sqrt_factor(P, lane);
   }
+  store_rec_P(rec, lane, P);
+}
 
-  // ---------------- forward sweep (row-owned) ----------------
-  // The record rows of stage k+1 are loaded while stage k computes (the loads
-  // do not depend on x), so each stage pays one memory latency less.
-  const int row = col;
+// A stage record by plain stores, or (img set) through the wave's LDS image: the four
+// groups write their records into the image, then the wave stores the four records, which
+// are contiguous in the stage-major workspace, as whole 16-byte pieces in lane order.
+template <class StoreRec>
+__device__ void HbmSrc::store_stage(int k, int lane, StoreRec&& store) const {
+  if (!img) {
+    store(rec(k));
+    return;
+  }
+  store(img + gq * kWsStage);
+  const int qp0 = qp - gq;
+  const int nq = a.batch - qp0 < 4 ? a.batch - qp0 : 4;  // live groups (the wave's first nq)
+  constexpr int kPiecesPerRec = kWsStage * (int)sizeof(real) / 16;
+  const int pieces = nq * kPiecesPerRec;
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const d2* src = reinterpret_cast<const d2*>(img);
+  d2* dst = reinterpret_cast<d2*>(a.ws + ((size_t)k * a.batch + qp0) * kWsStage);
+  for (int p = (int)(threadIdx.x & 63); p < pieces; p += 16 * nq) dst[p] = src[p];
+}
+
+// optional outputs of the backward sweep (hpipm-cpp getRiccati*): P_k, p_k, K_k, k_k
+__device__ __forceinline__ void store_riccati_out(const ProblemArgsT<real>& a, int qp, int k, int lane,
+                                                  const real (&F)[12], const real (&Kc)[12]) {
+  const int N = a.N;
+  const bool own = lane < kMaxDim, isv = lane == kVecLane;
+  if (a.P && own) store_n(a.P + ((size_t)qp * (N + 1) + k) * 144 + (size_t)lane * 12, 12, F);
+  if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + k) * 12, 12, F);
+  if (k < N) {
+    if (a.K && own) store_n(a.K + ((size_t)qp * N + k) * 144 + (size_t)lane * 12, 12, Kc);
+    if (a.k && isv) store_n(a.k + ((size_t)qp * N + k) * 12, 12, Kc);
+  }
+}
+
+// ---- forward sweep (row-owned), shared by every unconstrained kernel ----
+// u = K x + k, pi = P x + p, x+ = Acl x + bcl.  The record rows of stage k+1 are loaded
+// while stage k computes (the loads do not depend on x), so each stage pays one memory
+// latency less.
+template <class Src>
+__device__ __forceinline__ void fwd_sweep(const ProblemArgsT<real>& a, const Src& src, const int qp,
+                                          const int lane) {
+  constexpr int nx = 12, nu = 12;
+  const int N = a.N;
+  const bool own = lane < kMaxDim;
+  const int row = own ? lane : kMaxDim - 1;
   real xv = own ? a.x0[(size_t)qp * nx + lane] : real(0.0);
   bool bad = false;
   real* xo = a.x + (size_t)qp * (N + 1) * nx;
   real* uo = a.u + (size_t)qp * N * nu;
   real* po = a.pi + (size_t)qp * (N + 1) * nx;
   real Pr[12], Kr[12], Ar[12], pv, kv, bv;
-  auto load_rows = [&](int k, real (&P_)[12], real (&K_)[12], real (&A__)[12], real& p_,
-                       real& k_, real& b_) {
+  auto load_rows = [&](int k, real (&P_)[12], real (&K_)[12], real (&A__)[12], real& p_, real& k_,
+                       real& b_) {
     const real* rec = src.rec(k);
     load_packed_sym(rec + kWsP, row, P_);
     p_ = rec[kWsp + row];
     if (k < N) {
-      load12(rec + kWsK + row * 12, K_);
-      load12(rec + kWsAcl + row * 12, A__);
-      k_ = rec[kWsk + row];
-      b_ = rec[kWsbcl + row];
+      const real* kr = rec + kWsK + row * kWsRow;
+      const real* ar = rec + kWsAcl + row * kWsRow;
+      sfor<0, 12>([&](auto j) {
+        constexpr int J = decltype(j)::value;
+        K_[J] = kr[J];
+        A__[J] = ar[J];
+      });
+      k_ = kr[12];
+      b_ = ar[12];
     }
   };
   load_rows(0, Pr, Kr, Ar, pv, kv, bv);
@@ -236,14 +222,95 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
   }
 }
 
+// ---- the solve of one QP by its 16-lane group, blocks and records through `src` ----
+// SQRT: ric_alg = 1, the square-root recursion (riccati.h riccati_step_sqrt); the records
+// and outputs are the same (P_k = F - Y'Y of the stage, which Lx factors).
+template <bool SQRT, class Src>
+__device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src& src, const int qp,
+                                         const int lane) {
+  const int N = a.N;
+  const bool isv = lane == kVecLane;
+  const bool own = lane < kMaxDim;  // lane owns a block column
+  const int col = own ? lane : kMaxDim - 1;
+  const real reg = a.reg;
+
+  // ---------------- terminal stage: P_N = Q_N, p_N = q_N ----------------
+  real P[12];
+  if (isv) {
+    load12(src.q(N), P);
+  } else {
+    load12(src.Q(N) + col * 12, P);
+  }
+  store_rec_P(src.rec(N), lane, P);
+  store_riccati_out(a, qp, N, lane, P, P);
+  if constexpr (SQRT) sqrt_factor(P, lane);
+
+  // ---------------- backward sweep ----------------
+  real A_[12], B_[12];
+#pragma unroll 1
+  for (int k = N - 1; k >= 0; --k) {
+    // A, B (VL: b) of stage k, column-owned
+    if (isv) {
+      load12(src.b(k), A_);
+      sfor<0, 12>([&](auto i) { B_[decltype(i)::value] = real(0.0); });
+    } else {
+      load12(src.A(k) + col * 12, A_);
+      load12(src.B(k) + col * 12, B_);
+    }
+    auto loadR = [&](real (&Rc)[12]) {
+      if (isv) {
+        sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = real(0.0); });
+      } else {
+        load12(src.R(k) + col * 12, Rc);
+      }
+    };
+    auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
+      if (isv) {
+        load12(src.r(k), Sc);
+        load12(src.q(k), Qc);
+      } else {
+        load12(src.S(k) + col * 12, Sc);
+        load12(src.Q(k) + col * 12, Qc);
+      }
+    };
+    StageFactor<real> f;
+    if constexpr (SQRT) {
+      riccati_step_sqrt(P, A_, B_, loadR, loadSQ, lane, reg, f);
+    } else {
+      riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
+    }
+    if constexpr (std::is_same_v<Src, HbmSrc>) {
+      src.store_stage(k, lane, [&](real* r) { store_rec(r, lane, f.Kc, A_, f.F); });
+    } else {
+      store_rec(src.rec(k), lane, f.Kc, A_, f.F);
+    }
+    store_riccati_out(a, qp, k, lane, f.F, f.Kc);
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      P[I] = f.F[I];
+    });
+    if constexpr (SQRT) sqrt_factor(P, lane);
+  }
+  fwd_sweep(a, src, qp, lane);
+}
+
 // Large batches: 16 QPs per 256-thread workgroup, 2 workgroups per CU (the kernel needs
-// 217-223 VGPRs; memory-bound with the compute overlapped).
+// 217-224 VGPRs; memory-bound with the compute overlapped).  fp64: each
+// wave's stage records go out through its 12.6 KiB LDS image (HbmSrc::store_stage).
 template <bool SQRT>
 __global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<real> a) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int qp = gid >> 4;
   if (qp >= a.batch) return;
-  solve_qp<SQRT>(a, HbmSrc{a, qp}, qp, threadIdx.x & (kGroup - 1));
+  if constexpr (sizeof(real) == 8) {  // fp64 records are whole 16-byte pieces per QP
+    __shared__ __attribute__((aligned(16))) real rec_img[16 * kWsStage];
+    HbmSrc src{a, qp};
+    src.gq = (threadIdx.x >> 4) & 3;
+    src.img = rec_img + (threadIdx.x >> 6) * 4 * kWsStage;
+    solve_qp<SQRT>(a, src, qp, threadIdx.x & (kGroup - 1));
+  } else {
+    solve_qp<SQRT>(a, HbmSrc{a, qp}, qp, threadIdx.x & (kGroup - 1));
+  }
 }
 
 // Small batches: one QP per 64-thread workgroup.  All 64 lanes copy the QP into the LDS
