@@ -657,7 +657,9 @@ def roofline(constraints, achieved_gbs, traffic, kernel_ms, bytes_qp, flops_qp, 
     if constraints == "none":
         return {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "riccati_unconstr_kernel<true>", "kernel_avg_ms": kernel_ms,
+                # template argument = square-root Riccati (ric_alg; NMPC_solver.cpp:81 sets 0)
+                "kernel": "riccati_unconstr_kernel<%s>" % ("true" if NMPC_SETTINGS["ric_alg"] else "false"),
+                "kernel_avg_ms": kernel_ms,
                 "alg_bytes_per_qp": bytes_qp}
     it = max(float(np.mean(iters)), 1.0)
     gbs = achieved_gbs * it
