@@ -107,9 +107,31 @@ __device__ __forceinline__ Bar warm_bar(const real* p, const Side& s) {
 
 // The RB sweep's per-group LDS blocks (A, B, S: 3 x 144 reals per QP group).  One
 // function, so one allocation per kernel: the fused RB -> F1 kernel's F1 reuses them.
+// RB also stages each stage's factor record there (kRecSize reals) once the blocks are dead
+// (kRecImg: the box kernels; the general-row kernels' LDS and registers are at their limits
+// -- the fp32 ones' fp64 G scratch leaves no room for the larger block at 3 workgroups per
+// CU, the fp64 ones spill -- and they store the record directly).
+template <int GEN>
+constexpr bool kRecImg = GEN == 0;
+template <int GEN>
+constexpr int kGroupLds = kRecImg<GEN> && kRecSize > 3 * 144 ? kRecSize : 3 * 144;
+template <int GEN>
 __device__ __forceinline__ real* group_lds_blocks() {
-  __shared__ real blocks[(256 / kGroup) * 3 * 144];
-  return blocks + (threadIdx.x / kGroup) * 3 * 144;
+  __shared__ __attribute__((aligned(16))) real blocks[(256 / kGroup) * kGroupLds<GEN>];
+  return blocks + (threadIdx.x / kGroup) * kGroupLds<GEN>;
+}
+
+// A factor record from the group's LDS image to the workspace as whole 16-byte pieces
+// (16 lanes x 16 B per instruction; box-u 79.3 -> 76.5 ms same-box).  Plain stores: F1, B2
+// and F2 read the record again within the iteration (non-temporal stores of stages >= 4
+// measured the same).
+__device__ __forceinline__ void rec_copy(real* rec, const real* img, int lane) {
+  typedef real v4 __attribute__((ext_vector_type(16 / sizeof(real))));
+  constexpr int kPieces = kRecSize * (int)sizeof(real) / 16;
+  static_assert(kRecSize * sizeof(real) % 16 == 0, "whole pieces");
+  const v4* s = reinterpret_cast<const v4*>(img);
+  v4* d = reinterpret_cast<v4*>(rec);
+  for (int p = lane; p < kPieces; p += kGroup) d[p] = s[p];
 }
 
 template <bool FULL, int GEN>
@@ -884,7 +906,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     // or transposed) and a row-owned copy through LDS where they are not (A x, B u,
     // S x); S stays in LDS until the factorization's second phase asks for it.
     // LDS per QP group: A, B, S columns (3 x 144 reals).
-    real* const ldsA = group_lds_blocks();
+    real* const ldsA = group_lds_blocks<GEN>();
     real* const ldsB = ldsA + 144;
     real* const ldsS = ldsA + 288;
     // The sweep's six accumulators are live across the whole factorization, where the
@@ -1197,17 +1219,22 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         } else {
           riccati_step<1, true, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f);  // P_k symmetrized
         }
+        // The factor record goes through the group's LDS image (its A, B, S blocks are
+        // dead by now) and leaves as whole 16-byte pieces instead of ~40 scattered
+        // per-lane stores (the kRecP slot holds P, or its factor Lp for SQRT).
+        lds_wave_fence();
+        real* const img = kRecImg<GEN> ? ldsA : rec;
         if (lane < kMaxDim) {
-          store_packed_col(rec + kRecL, lane, f.Lc);
-          store12(rec + kRecK + lane * 12, f.Kc);
-          store12(rec + kRecAcl + lane * 12, A_);
-          if constexpr (!SQRT) store_packed_col(rec + kRecP, lane, f.F);
-          rec[kRecRs + lane] = f.rs;
+          store_packed_col(img + kRecL, lane, f.Lc);
+          store12(img + kRecK + lane * 12, f.Kc);
+          store12(img + kRecAcl + lane * 12, A_);
+          if constexpr (!SQRT) store_packed_col(img + kRecP, lane, f.F);
+          img[kRecRs + lane] = f.rs;
         }
         if (c.isv) {
-          store12(rec + kRecKv, f.Kc);
-          store12(rec + kRecBcl, A_);
-          store12(rec + kRecPv, f.F);
+          store12(img + kRecKv, f.Kc);
+          store12(img + kRecBcl, A_);
+          store12(img + kRecPv, f.F);
         }
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
@@ -1215,8 +1242,10 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         });
         if constexpr (SQRT) {
           sqrt_factor(P, lane);
-          if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
+          if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
         }
+        lds_wave_fence();
+        if constexpr (kRecImg<GEN>) rec_copy(rec, img, lane);
         // the next stage overwrites this group's LDS blocks: reads done first
         lds_wave_fence();
       }
@@ -1371,7 +1400,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   if constexpr (PH == kPhF1 || PH == kPhF2) {
     constexpr bool corr = PH == kPhF2;
     // F1 with C-free general rows: D'z goes through the group's first LDS block
-    real* const f1_lds_grp = group_lds_blocks();
+    real* const f1_lds_grp = group_lds_blocks<GEN>();
     real ap = real(1e30), ad = real(1e30);
     real s1 = real(0.0), s2 = real(0.0);  // predictor sums lam dt + t dlam, dlam dt (element-owned)
     bool bad = false;  // a non-finite component in the final step (fp32 breakdown)
