@@ -595,6 +595,11 @@ def call_pattern(pkg, seed, N=20, reps=20, oracle_reps=400):
                    "solve one SRBD QP (N=20) from host buffers, destroy; 15 per NMPC step")
     out["oracle_1_core_us"] = {"median": float(np.median(ts)) * 1e6, "min": float(np.min(ts)) * 1e6,
                                "kind": "port", "cores": 1}
+    # the fixed-size CPU port (oracle/fast_unconstr.c) on the same QP, one core
+    oracle.fast_unconstr_batch(qp, x0, 1)
+    ts = [oracle.fast_unconstr_batch(qp, x0, 1)[1] for _ in range(oracle_reps)]
+    out["cpu_port_1_core_us"] = {"median": float(np.median(ts)) * 1e6, "min": float(np.min(ts)) * 1e6,
+                                 "kind": "port", "cores": 1, "src": "oracle/fast_unconstr.c"}
     return out
 
 
@@ -677,10 +682,19 @@ def settings_dict(s):
 
 
 def cpu_baseline(pkg, qp, x0, settings, budget_s):
-    """The C oracle ('port': same algorithm, scalar C, -O3, x86-64-v3) on the host
-    cores over a bounded sample of the same workload."""
+    """A CPU port on the host cores over a bounded sample of the same workload: for
+    unconstrained 12 x 12 QPs the fixed-size vectorised port (oracle/fast_unconstr.c,
+    x, u, pi only, as the GPU line), otherwise the generic C oracle (same algorithm,
+    scalar C, -O3, x86-64-v3)."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle  # test infrastructure, used here only as the CPU baseline
+    fast = qp.ng == 0 and qp.nx == 12 and qp.nu == 12 and not _has_bounds(qp)
+    if fast:
+        run = lambda b, x, t: oracle.fast_unconstr_batch(b, x, t, settings.get("reg_prim", 1e-12))
+        src = "oracle/fast_unconstr.c: fixed 12 x 12 port, AVX2 + FMA"
+    else:
+        run = lambda b, x, t: oracle.solve_batch_threaded(b, settings, x, t)
+        src = "oracle/ocp_qp_oracle.c"
     # the GPU box's CPU share is OMP_NUM_THREADS (16 per GPU there); nproc shows
     # the whole machine
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
@@ -689,18 +703,21 @@ def cpu_baseline(pkg, qp, x0, settings, budget_s):
     # calibrate on a slice big enough that thread start-up does not dominate,
     # then repeat the slice until the budget is spent
     cal = qp.subset(slice(0, min(qp.batch, 64 * threads)))
-    _, dt = oracle.solve_batch_threaded(cal, settings, x0[:cal.batch], threads)
+    _, dt = run(cal, x0[:cal.batch], threads)
     rate = cal.batch / max(dt, 1e-9)
     n = int(min(qp.batch, max(cal.batch, rate * budget_s / 4)))
     sample = qp.subset(slice(0, n))
     t, reps = 0.0, 0
     while t < budget_s:
-        _, d = oracle.solve_batch_threaded(sample, settings, x0[:n], threads)
+        _, d = run(sample, x0[:n], threads)
         t += d
         reps += 1
     return {"value": n * reps / t, "unit": "QP solves/s", "cores": threads, "kind": "port",
-            "sample": f"{n} QPs x {reps} reps of the same workload ({t:.1f} s, {threads} threads, "
-                      f"oracle/ocp_qp_oracle.c)"}
+            "sample": f"{n} QPs x {reps} reps of the same workload ({t:.1f} s, {threads} threads, {src})"}
+
+
+def _has_bounds(qp):
+    return any(getattr(qp, k) is not None for k in ("lbu", "ubu", "lbx", "ubx"))
 
 
 def pmc_traffic(workload, batch):

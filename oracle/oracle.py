@@ -168,3 +168,39 @@ def solve_batch_threaded(batch, settings: Optional[Dict] = None, x0=None, thread
                              iters.ctypes.data_as(C.POINTER(C.c_int)), int(threads))
     dt = time.perf_counter() - t0
     return {"x": x, "u": u, "pi": pi, "status": status, "iter": iters}, dt
+
+
+# ---- the cpu_baseline port of the unconstrained solve (oracle/fast_unconstr.c) ----
+FAST_LIB_PATH = HERE / "build" / "libfast_unconstr.so"
+_fast = None
+
+
+def fast_lib():
+    global _fast
+    if _fast is None:
+        if not FAST_LIB_PATH.exists():
+            build()
+        _fast = C.CDLL(str(FAST_LIB_PATH))
+        _fast.fast_unconstr_solve_batch.restype = C.c_int
+    return _fast
+
+
+def fast_unconstr_batch(batch, x0, threads: int = 1, reg: float = 1e-12):
+    """x, u, pi of an unconstrained nx = nu = 12 batch by the fixed-size CPU port.
+    Returns (out, seconds)."""
+    p = batch.packed()
+    N, nb = batch.N, batch.batch
+    assert batch.nx == 12 and batch.nu == 12 and batch.ng == 0
+    arr = {k: np.ascontiguousarray(p[k], dtype=np.float64) for k in ("A", "B", "b", "Q", "S", "R", "q", "r")}
+    x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(nb, 12)
+    x = np.zeros((nb, N + 1, 12))
+    u = np.zeros((nb, N, 12))
+    pi = np.zeros((nb, N + 1, 12))
+    t0 = time.perf_counter()
+    rc = fast_lib().fast_unconstr_solve_batch(
+        int(nb), int(N), *(_ptr(arr[k]) for k in ("A", "B", "b", "Q", "S", "R", "q", "r")), _ptr(x0),
+        C.c_double(reg), _ptr(x), _ptr(u), _ptr(pi), int(threads))
+    dt = time.perf_counter() - t0
+    if rc != 0:
+        raise RuntimeError("fast_unconstr_solve_batch failed")
+    return {"x": x, "u": u, "pi": pi}, dt

@@ -96,3 +96,19 @@ def test_constrained_matches_unconstrained_when_inactive(OcpQpBatch, oracle):
     for i in range(2):
         assert helpers.is_approx(out["x"][i], ref["x"][i], 1e-8)
         assert helpers.is_approx(out["u"][i], ref["u"][i], 1e-8)
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_fast_unconstr_port_matches_oracle(pkg, oracle, threads):
+    """The cpu_baseline port (oracle/fast_unconstr.c, fixed 12 x 12) computes the oracle's
+    x, u, pi on SRBD QPs and on the reference test's random QPs (12 x 12)."""
+    qp, x0 = pkg.srbd_model.generate_batch(7, N=20, seed=1003)
+    ref = oracle.solve(qp, None, x0=x0)
+    out, _ = oracle.fast_unconstr_batch(qp, x0, threads=threads)
+    for key in ("x", "u", "pi"):
+        assert helpers.is_approx(out[key], ref[key], 1e-10), key
+    qp, x0 = helpers.random_unconstrained(5, 10, 12, 12, 77, pkg.OcpQpBatch)
+    ref = oracle.solve(qp, None, x0=x0)
+    out, _ = oracle.fast_unconstr_batch(qp, x0, threads=threads)
+    for key in ("x", "u", "pi"):
+        assert helpers.is_approx(out[key], ref[key], 1e-10), key
