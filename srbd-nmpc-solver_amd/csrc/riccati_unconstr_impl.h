@@ -57,11 +57,11 @@ struct HbmSrc {
   // stores)
   real* img = nullptr;  // the wave's image base: group g's record at img + g * kWsStage
   int gq = 0;           // QP group in the wave
+  // stage k's record, `store` writing it at a given base (defined after store_rec below)
   template <class StoreRec>
-  __device__ void store_stage(int k, int lane, StoreRec&& store) const;
+  __device__ void store_stage(int k, StoreRec&& store) const;
 };
 
-// forward declaration target; defined after store_rec below
 // LDS image of one QP: stage slot k (k = 0..N) holds the stage's blocks at the offsets
 // below (slot N: Q and q only); after the backward sweep has used slot k's blocks, the
 // stage's forward record (kernels.h kWs*, 402 reals) is written over them.
@@ -111,7 +111,7 @@ constexpr int kRecHotStages = 4;
 // groups write their records into the image, then the wave stores the four records, which
 // are contiguous in the stage-major workspace, as whole 16-byte pieces in lane order.
 template <class StoreRec>
-__device__ void HbmSrc::store_stage(int k, int lane, StoreRec&& store) const {
+__device__ void HbmSrc::store_stage(int k, StoreRec&& store) const {
   if (!img) {
     store(rec(k));
     return;
@@ -291,7 +291,7 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
       riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
     }
     if constexpr (std::is_same_v<Src, HbmSrc>) {
-      src.store_stage(k, lane, [&](real* r) { store_rec(r, lane, f.Kc, A_, f.F); });
+      src.store_stage(k, [&](real* r) { store_rec(r, lane, f.Kc, A_, f.F); });
     } else {
       store_rec(src.rec(k), lane, f.Kc, A_, f.F);
     }
