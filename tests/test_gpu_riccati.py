@@ -243,3 +243,22 @@ def test_latency_kernel_bit_identical(pkg, dtype, N, ric_alg):
         for key in ("x", "u", "pi", "P", "p", "K", "k", "status", "iter"):
             assert np.array_equal(small[key], big[key][idx]), (key, idx)
     assert np.all(big["status"] == 0)
+
+
+@pytest.mark.parametrize("ric_alg", [0, 1])
+def test_streaming_kernel_partial_waves(pkg, oracle, ric_alg):
+    """N = 30 (over the LDS image cap: the streaming kernel at every batch size) with
+    batches of 1, 2, 3, 5 and 37 QPs: the last wave holds fewer than four QP groups, and
+    its records still leave through the wave's LDS image in whole pieces.  Every QP's
+    outputs are bit-identical to the same QP inside a full batch, and match the oracle."""
+    qp, x0 = pkg.srbd_model.generate_batch(64, N=30, seed=91, constraints="none")
+    st = dict(ric_alg=ric_alg)
+    big = pkg.capi.solve(qp, x0, st, riccati=True)
+    ref = oracle.solve(qp.subset(slice(0, 5)), dict(ric_alg=ric_alg), x0=x0[:5])
+    for key in ("x", "u", "pi"):
+        assert helpers.is_approx(big[key][:5], ref[key], 1e-9), key
+    for nb in (1, 2, 3, 5, 37):
+        idx = slice(7, 7 + nb)
+        small = pkg.capi.solve(qp.subset(idx), x0[idx], st, riccati=True)
+        for key in ("x", "u", "pi", "P", "p", "K", "k", "status"):
+            assert np.array_equal(small[key], big[key][idx]), (key, nb)
