@@ -389,6 +389,10 @@ __device__ __forceinline__ void max_nan(real& m, real v) {
 __global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(ProblemArgsT<real> a) {
   const int qp = blockIdx.x;
   const int N = a.N, nx = a.nx, nu = a.nu;
+  if (a.stat) {  // the QP's stat table is cleared here (no separate memset), row 0 filled below
+    real* tab = a.stat + (size_t)qp * a.stat_rows * kStatCols;
+    for (int i = threadIdx.x; i < a.stat_rows * kStatCols; i += kResThreads) tab[i] = real(0);
+  }
   const bool smaj = a.layout == 1;
   auto at = [&](const real* base, int nstage, size_t blk, int k) -> const real* {
     return smaj ? base + ((size_t)k * a.batch + qp) * blk : base + ((size_t)qp * nstage + k) * blk;

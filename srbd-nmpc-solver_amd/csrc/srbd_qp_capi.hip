@@ -327,7 +327,8 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   a.tol_ineq = st->tol_ineq;
   a.tol_comp = st->tol_comp;
   hipError_t e = hipSuccess;
-  if (s->stat)
+  // (unconstrained with residuals: unconstr_residuals_kernel clears and fills the table)
+  if (s->stat && (constrained(h->dims) || !st->compute_residuals))
     e = hipMemsetAsync(s->stat, 0,
                        sizeof(T) * srbd::kStatCols * (size_t)(st->iter_max + 2) * (size_t)batch, strm);
   // nx < 12 or nu < 12: solve the problem embedded in 12 x 12 stages
