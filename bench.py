@@ -157,6 +157,66 @@ def gather_solutions(pkg, sol_t, world, rank, cpu_staged=False):
     return pkg.dist.gather_to_root(payload, world, rank)
 
 
+def baseline_config_name(workload, global_batch, world):
+    """Which BASELINE.json config a run measures (None if it is none of them)."""
+    if workload == "unconstr_n20" and global_batch == 262144 and world == 8:
+        return "config 4: batch 262144, N=20, sharded 8 x MI355X with RCCL gather"
+    if workload == "unconstr_n10_b4096" and global_batch == 4096:
+        return "config 2: batch 4096, N=10"
+    if workload == "box_u_n20" and global_batch == 65536:
+        return "config 3: batch 65536, N=20, box constraints on u"
+    if workload == "cone_n40_f32" and global_batch == 65536:
+        return "config 5: batch 65536, N=40, friction cone, fp32"
+    return None
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without an external launcher: start N rank processes
+    of this same script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their
+    environment, rendezvous on 127.0.0.1), wait for all of them and return the
+    worst exit code.  Called before this process touches the GPU; the ranks are
+    children, this process is not replaced.  Only rank 0 prints the JSON line."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:],
+                                      env=env))
+    log(f"[launcher] {n} ranks started (pids {[p.pid for p in procs]}, port {port})")
+    rc, kill_at = 0, None
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                # one rank failed: the others would wait in a collective forever
+                for q in pending:
+                    q.terminate()
+                kill_at = time.monotonic() + 15.0
+        if kill_at is not None and time.monotonic() > kill_at:
+            for q in pending:
+                q.kill()
+            kill_at = None
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -187,19 +247,49 @@ def main():
     ap.add_argument("--f32-iters", type=int, default=0,
                     help="fp64 IPM workloads: settings.f32_iters = n (mixed precision: the first n "
                          "IPM iterations in fp32, then fp64 to the fp64 tolerances)")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process-group backend for N > 1: nccl (= RCCL over xGMI, one GPU per "
+                         "rank) or gloo (host-staged gather; ranks may share a GPU, for tests)")
+    ap.add_argument("--print-ranks", action="store_true",
+                    help="print each rank's RANK / WORLD_SIZE / MASTER_* and exit (launcher check)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
 
-    import torch
-    import torch.distributed as dist
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks ourselves, before anything touches the GPU
+        sys.exit(launch_ranks(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report "
+                         f"a {world}-rank measurement as {args.gpus} GPUs")
+    if args.print_ranks:  # launcher check: report this rank's environment, touch nothing
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world": world,
+                          "master": [os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")]}),
+              flush=True)
+        return
+
+    import torch
+    import torch.distributed as dist
+
     distributed = world > 1
+    gloo = args.dist_backend == "gloo"
+    ndev = torch.cuda.device_count()  # counting devices does not initialise the GPU
+    if distributed and not gloo and ndev < world:
+        raise SystemExit(f"bench.py: {world} nccl ranks need {world} GPUs, {ndev} visible")
+    dev_index = local_rank % max(ndev, 1) if gloo else local_rank
     if distributed:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+    device = torch.device("cuda", dev_index)
+    # the time reduction runs on the backend's own device type
+    red_device = torch.device("cpu") if gloo else device
     pkg = import_pkg()
     capi = pkg.capi
 
@@ -218,7 +308,7 @@ def main():
     if stage_major and constraints != "none":
         raise SystemExit("--layout stage: unconstrained workloads only")
     ng = 24 if constraints == "cone" else 0
-    h = capi.Handle(N, 12, 12, ng, constraints == "box_u", False, capacity=batch, device=local_rank,
+    h = capi.Handle(N, 12, 12, ng, constraints == "box_u", False, capacity=batch, device=dev_index,
                     layout=1 if stage_major else 0)
     dt, xs_np, us_np, x0_np = device_shard(pkg, h, N, constraints, batch, rank, args.seed, device,
                                            np_dtype, stage_major)
@@ -252,7 +342,11 @@ def main():
         dist.barrier()
     t_wall = time.perf_counter() - t_start
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    t_max = pkg.dist.max_over_ranks(t_wall, device)
+    t_max = pkg.dist.max_over_ranks(t_wall, red_device)
+    rank_walls = [t_wall]
+    if distributed:
+        rank_walls = [None] * world
+        dist.all_gather_object(rank_walls, t_wall)
     status = sol_t["status"].cpu().numpy()
     iters = sol_t["iter"].cpu().numpy()
     n_ok = int((status == 0).sum())
@@ -282,9 +376,9 @@ def main():
         tg = time.perf_counter()
         reps = 5
         for _ in range(reps):
-            gather_solutions(pkg, sol_t, world, rank)
+            gather_solutions(pkg, sol_t, world, rank, cpu_staged=gloo)
         torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - tg) / reps * 1e3
+        gather_ms = pkg.dist.max_over_ranks((time.perf_counter() - tg) / reps, red_device) * 1e3
 
     if rank != 0:
         if distributed:
@@ -342,6 +436,9 @@ def main():
         "config": {"workload": args.workload, "description": desc, "batch_per_gpu": batch,
                    "global_batch": total_qps, "N": N, "nx": 12, "nu": 12, "constraints": constraints,
                    "parallelism": f"dp{world} (independent QP shards)",
+                   "baseline_config": baseline_config_name(args.workload, total_qps, world),
+                   "dist_backend": (args.dist_backend if distributed else None),
+                   "rank_ms_per_step": [w / args.steps * 1e3 for w in rank_walls],
                    "input_layout": "stage-major" if stage_major else "qp-major",
                    "settings": ("NMPC_solver.cpp:70-82 (Speed, iter_max 30, split_step) with fp32 "
                                 "tolerances stat 3e-2 / 1e-3" if dtype == "f32" else
@@ -363,7 +460,11 @@ def main():
     if pattern is not None:
         line["reference_call_pattern"] = pattern
     if gather_ms is not None:
-        line["gather"] = {"ms": gather_ms, "bytes_per_rank": batch * (2 * (N + 1) * 12 + N * 12) * 8,
+        elem = 4 if dtype == "f32" else 8
+        line["gather"] = {"what": "x, u, pi of every rank to rank 0 (dist.gather, one message per rank"
+                                  + (", host-staged over gloo)" if gloo else ", RCCL over xGMI)"),
+                          "ms": gather_ms, "bytes_per_rank": batch * (2 * (N + 1) * 12 + N * 12) * elem,
+                          "value_kernel_only": value,
                           "value_with_gather": total_qps / (t_max / args.steps + gather_ms * 1e-3)}
     print(json.dumps(line), flush=True)
     if distributed:

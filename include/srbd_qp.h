@@ -76,7 +76,7 @@
 extern "C" {
 #endif
 
-#define SRBD_QP_ABI_VERSION 8
+#define SRBD_QP_ABI_VERSION 9
 #define SRBD_QP_MAX_NX 12
 #define SRBD_QP_MAX_NU 12
 #define SRBD_QP_MAX_NG 64
@@ -158,15 +158,16 @@ typedef struct srbd_qp_settings {
                      * iter_max - 1) iterations run in fp32 (half the bytes per
                      * sweep), and the fp64 IPM continues from that iterate (x,
                      * u, pi, lam, t) on the caller's fp64 data to the fp64
-                     * tolerances for at most iter_max - m iterations, so the
-                     * iteration budget stays iter_max; iter and stat count the
-                     * fp64 iterations.  A QP the continuation ends with
-                     * MinStepLengthReached or NaNDetected (a numerical
-                     * breakdown) is solved again cold in fp64, iter_max
-                     * iterations, and then carries the fp64 path's outputs; the
-                     * call waits once to count them.  Worst case per QP: iter_max
-                     * iterations (m fp32) plus, for a breakdown only, iter_max
-                     * fp64 ones.                                           */
+                     * tolerances for at most iter_max - m iterations; iter and
+                     * stat count the fp64 iterations.  Contract: the mixed path
+                     * never ends a QP worse than the fp64 path.  Every QP the
+                     * continuation does not end with Success is solved again
+                     * in fp64 exactly as the plain fp64 call would solve it
+                     * (iter_max iterations, from the caller's x / u when
+                     * warm_start is set, cold otherwise) and then carries that
+                     * solve's outputs, bit for bit; the call waits once to
+                     * count them.  Worst case per QP: iter_max iterations (m of
+                     * them fp32) plus iter_max fp64 ones.                  */
 } srbd_qp_settings;
 
 typedef struct srbd_qp_data_f64 {
@@ -328,6 +329,14 @@ void* srbd_qp_stream(srbd_qp_handle h);
 
 /* Device workspace bytes the handle holds.                                */
 size_t srbd_qp_workspace_bytes(srbd_qp_handle h);
+
+/* Every byte the handle holds right now: the workspace plus the buffers it
+ * allocates on first use (host-solve staging and its pinned host mirror, the
+ * 12 x 12 embedding, the NMPC loop state, the f64_rescue / f32_iters
+ * batches).  A pool of handles (hpipm-cpp's, which re-implements the
+ * reference's construct-per-solve pattern, NMPC_solver.cpp:318-319) sizes
+ * itself by this.  (ABI 9)                                                  */
+size_t srbd_qp_memory_bytes(srbd_qp_handle h);
 
 void srbd_qp_destroy(srbd_qp_handle h);
 

@@ -125,6 +125,11 @@ def lib():
         L.srbd_qp_stream.restype = C.c_void_p
         L.srbd_qp_workspace_bytes.argtypes = [C.c_void_p]
         L.srbd_qp_workspace_bytes.restype = C.c_size_t
+        try:  # ABI >= 9 (older builds are still loaded by A/B scripts)
+            L.srbd_qp_memory_bytes.argtypes = [C.c_void_p]
+            L.srbd_qp_memory_bytes.restype = C.c_size_t
+        except AttributeError:
+            pass
         L.srbd_qp_default_settings.argtypes = [C.POINTER(Settings)]
         L.srbd_qp_default_settings.restype = None
         L.srbd_qp_check_settings.argtypes = [C.POINTER(Settings)]
@@ -207,6 +212,10 @@ class Handle:
 
     def workspace_bytes(self) -> int:
         return int(lib().srbd_qp_workspace_bytes(self._h))
+
+    def memory_bytes(self) -> int:
+        """Everything the handle holds (workspace + first-use buffers)."""
+        return int(lib().srbd_qp_memory_bytes(self._h))
 
     def synchronize(self) -> None:
         check(lib().srbd_qp_synchronize(self._h), "srbd_qp_synchronize")

@@ -335,13 +335,7 @@ __device__ __forceinline__ void lds_get_row(const real* blk, int r, real (&v)[12
     v[J] = blk[J * 12 + r];
   });
 }
-// the group's lanes exchange data through LDS inside one wave: LDS executes a
-// wave's instructions in order, so only the compiler must not move the reads
-// above the writes (a compiler-only barrier: no wait on outstanding global loads)
-__device__ __forceinline__ void lds_wave_fence() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
+// (lds_wave_fence: qp_group.h)
 
 // general-constraint chunk state (see kGenChunk)
 __device__ __forceinline__ Bar load_gbar(const real* g, int i) {
@@ -1576,9 +1570,38 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 template <int GEN>
 constexpr int kIpmMinBlocks = sizeof(real) == 4 && GEN < 2 ? 3 : 2;
 
+// Live-QP report after an RB sweep (ProblemArgsT::ctl): one count per workgroup with a QP
+// still running, and the workgroup that finishes last hands the verdict to the host.  Every
+// thread of the workgroup reaches this (the phase functions return, the kernels do not).
+__device__ __forceinline__ void report_running(const ProblemArgsT<real>& a) {
+  if (!a.ctl) return;
+  const int qp = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4);
+  bool run = false;
+  if ((threadIdx.x & (kGroup - 1)) == 0 && qp < a.batch)  // the lane that wrote the status
+    run = a.ws[(size_t)qp * a.ws_qp + kQsStatus] < real(0.0);
+  const int any = __syncthreads_or(run);
+  if (threadIdx.x == 0) {
+    int* cnt = a.ctl + 2 * a.launch_it;
+    if (any) atomicAdd(cnt, 1);
+    __threadfence();
+    if (atomicAdd(cnt + 1, 1) == (int)gridDim.x - 1) {
+      __threadfence();
+      const int live = atomicAdd(cnt, 0);
+      __hip_atomic_store(a.ctl_host + a.launch_it, (a.ctl_tag << 1) | (live > 0 ? 1 : 0), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 template <bool FULL, int GEN, int PH, bool SQRT = false>
 __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase_kernel(ProblemArgsT<real> a) {
+  if constexpr (PH == kPhInit) {  // this solve's live-QP counters start at 0
+    if (a.ctl)
+      for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * a.ctl_cap; i += gridDim.x * blockDim.x)
+        a.ctl[i] = 0;
+  }
   ipm_phase<FULL, GEN, PH, SQRT>(a);
+  if constexpr (PH == kPhRB) report_running(a);
 }
 
 // Two consecutive sweeps of one iteration in one launch (RB -> F1, B2 -> F2):
@@ -1591,6 +1614,7 @@ __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase2
   ipm_phase<FULL, GEN, PH1, SQRT>(a);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   ipm_phase<FULL, GEN, PH2, SQRT>(a);
+  if constexpr (PH1 == kPhRB) report_running(a);
 }
 
 template <bool FULL, int GEN, bool SQRT>
@@ -1602,19 +1626,38 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
   // the registers (and occupancy) of its own phase; QPs that have exited return
   // at the top of every later launch.  iter_max + 1 factorization sweeps at
   // most: the last one always decides (converged or MaxIterReached).
-  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhInit>), grid, block, 0, stream, a);
+  // Live-QP control (ProblemArgsT::ctl): the host runs one iteration ahead of the verdict
+  // of RB(it - 1) and stops launching once it says every QP has exited, so a solve costs
+  // the launches of the iterations its slowest QP takes (+ one), not 2 iter_max + 3.
+  const bool ctl = a.ctl && a.ctl_host && a.ctl_ev[0] && a.ctl_ev[1] && a.iter_max < a.ctl_cap;
+  ProblemArgsT<real> b = a;
+  if (!ctl) b.ctl = nullptr;
+  b.launch_it = 0;
+  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhInit>), grid, block, 0, stream, b);
   // (SQRT changes RB and how B2, F1, F2 and the outputs apply the record's P)
   for (int it = 0;; ++it) {
+    b.launch_it = it;
     if (it >= a.iter_max) {
       if (!a.skip_last_rb)
-        hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT>), grid, block, 0, stream, a);
+        hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT>), grid, block, 0, stream, b);
       break;
     }
-    hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT>), grid, block, 0, stream, b);
+    hipEvent_t ev = ctl ? reinterpret_cast<hipEvent_t>(a.ctl_ev[it & 1]) : nullptr;
+    if (ctl) {
+      hipError_t e = hipEventRecord(ev, stream);
+      if (e != hipSuccess) return e;
+    }
     if (a.pred_corr)
-      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhB2, kPhF2, SQRT>), grid, block, 0, stream, a);
+      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhB2, kPhF2, SQRT>), grid, block, 0, stream, b);
+    if (ctl && it >= 1) {
+      hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(a.ctl_ev[(it - 1) & 1]));
+      if (e != hipSuccess) return e;
+      const int v = __atomic_load_n(a.ctl_host + (it - 1), __ATOMIC_ACQUIRE);
+      if (v == (a.ctl_tag << 1)) break;  // this solve's RB(it - 1): no QP left running
+    }
   }
-  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut, SQRT>), grid, block, 0, stream, a);
+  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut, SQRT>), grid, block, 0, stream, b);
   return hipGetLastError();
 }
 

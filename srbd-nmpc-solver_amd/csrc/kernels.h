@@ -53,7 +53,19 @@ struct ProblemArgsT {
   // step without the sweep that would apply it; the step is handed to the fp64 continuation
   int skip_last_rb;
   T alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp;
+  // Live-QP control of the host-driven IPM loop (the handle's; ctl NULL = off).  After the
+  // RB sweep of launch iteration it, ctl[2 it] counts the workgroups with a QP still
+  // running and ctl[2 it + 1] the workgroups done; the last one writes ctl_host[it] =
+  // (ctl_tag << 1) | any-running into pinned host memory.  The host waits on ctl_ev (one
+  // iteration behind the launches) and stops launching once every QP has exited.
+  int* ctl;
+  int* ctl_host;
+  int ctl_tag, ctl_cap;  // ctl_cap: iterations the arrays hold
+  int launch_it;         // set per launch
+  void* ctl_ev[2];       // hipEvent_t (host side only)
 };
+// iterations of the live-QP control arrays (iter_max >= this runs without the control)
+constexpr int kCtlCap = 257;
 using ProblemArgs = ProblemArgsT<double>;
 
 constexpr int kStatCols = 18;  // HPIPM ws->stat row width
@@ -95,6 +107,9 @@ size_t ws_doubles_unconstr(int N);
 
 template <typename T>
 hipError_t launch_riccati_unconstr(const ProblemArgsT<T>& a, hipStream_t stream);
+// per-device launch attributes of the unconstrained kernels, on the current device
+// (srbd_qp_create, after selecting the handle's device)
+hipError_t prepare_riccati_device();
 // KKT residual norms / objective of an unconstrained solution into a.res / a.obj
 template <typename T>
 hipError_t launch_unconstr_residuals(const ProblemArgsT<T>& a, hipStream_t stream);

@@ -63,6 +63,14 @@ __device__ __forceinline__ float bc(float v) {
       float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x150 + SRC, 0xf, 0xf, true));
 }
 
+// The group's lanes exchange data through LDS inside one wave: LDS executes a
+// wave's instructions in order, so only the compiler must not move the reads
+// above the writes (a compiler-only barrier: no wait on outstanding global loads).
+__device__ __forceinline__ void lds_wave_fence() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // Opaque copy: the compiler can no longer prove the values equal to the
 // originals, so broadcasts of the laundered array are not CSE'd with earlier
 // broadcasts of the same registers (which would keep 144 broadcast values

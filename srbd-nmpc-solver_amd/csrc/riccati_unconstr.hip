@@ -35,6 +35,11 @@ namespace srbd {
 
 size_t ws_doubles_unconstr(int N) { return (size_t)(N + 1) * kWsStage; }
 
+hipError_t prepare_riccati_device() {
+  hipError_t e = ric_f64::prepare_device();
+  return e == hipSuccess ? ric_f32::prepare_device() : e;
+}
+
 template <>
 hipError_t launch_riccati_unconstr<double>(const ProblemArgsT<double>& a, hipStream_t stream) {
   return ric_f64::launch(a, stream);

@@ -117,6 +117,9 @@ __device__ void HbmSrc::store_stage(int k, StoreRec&& store) const {
     return;
   }
   store(img + gq * kWsStage);
+  // the copy below reads other groups' parts of the image: LDS executes the wave's
+  // instructions in order, so only the compiler must not move accesses across this point
+  lds_wave_fence();
   const int qp0 = qp - gq;
   const int nq = a.batch - qp0 < 4 ? a.batch - qp0 : 4;  // live groups (the wave's first nq)
   constexpr int kPiecesPerRec = kWsStage * (int)sizeof(real) / 16;
@@ -134,6 +137,7 @@ __device__ void HbmSrc::store_stage(int k, StoreRec&& store) const {
   } else {
     for (int p = l; p < pieces; p += 16 * nq) dst[p] = src[p];
   }
+  lds_wave_fence();  // the next stage's writes into the image stay after these reads
 }
 
 // optional outputs of the backward sweep (hpipm-cpp getRiccati*): P_k, p_k, K_k, k_k
@@ -505,14 +509,9 @@ bool use_lds_kernel(const ProblemArgsT<real>& a) {
 template <bool SQRT>
 static hipError_t launch_alg(const ProblemArgsT<real>& a, hipStream_t stream) {
   if (use_lds_kernel(a)) {
+    // (the > 64 KiB dynamic-LDS attribute is set on the handle's device by srbd_qp_create:
+    // prepare_device below)
     const size_t bytes = lds_image_bytes(a.N);
-    static bool attr_set = false;  // (same value for every N: the LDS cap)
-    if (!attr_set) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_unconstr_lds_kernel<SQRT>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytesMax);
-      if (e != hipSuccess) return e;
-      attr_set = true;
-    }
     hipLaunchKernelGGL(riccati_unconstr_lds_kernel<SQRT>, dim3((unsigned)a.batch), dim3(64), bytes, stream, a);
     return hipGetLastError();
   }
@@ -521,6 +520,18 @@ static hipError_t launch_alg(const ProblemArgsT<real>& a, hipStream_t stream) {
   const int blocks = (int)((lanes + threads - 1) / threads);
   hipLaunchKernelGGL(riccati_unconstr_kernel<SQRT>, dim3(blocks), dim3(threads), 0, stream, a);
   return hipGetLastError();
+}
+
+// Per-device launch attributes, set on the current device (srbd_qp_create calls this
+// after selecting the handle's device; hipFuncSetAttribute is per device, and every
+// handle sets it, so concurrent handles on any device need no shared flag).
+hipError_t prepare_device() {
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_unconstr_lds_kernel<false>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytesMax);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_unconstr_lds_kernel<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytesMax);
+  return e;
 }
 
 hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {

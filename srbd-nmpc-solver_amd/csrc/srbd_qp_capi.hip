@@ -65,6 +65,12 @@ struct srbd_qp_handle_s {
   // settings.f32_iters: fp32 copy of the data, fp32 iterate, barrier state (first use)
   void* mixed = nullptr;
   size_t mixed_bytes = 0;
+  // live-QP control of the IPM launch loop (ProblemArgsT::ctl): device counters, the pinned
+  // verdicts the last workgroup writes, two events, and the solve tag
+  int* ctl = nullptr;
+  int* ctl_host = nullptr;
+  hipEvent_t ctl_ev[2] = {nullptr, nullptr};
+  int ctl_tag = 0;
 };
 
 extern "C" {
@@ -180,7 +186,13 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srb
   h->ws_qp = ws_doubles_per_qp(*dims);
   h->ws_bytes = h->ws_qp * sizeof(double) * (size_t)batch_capacity;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = srbd::prepare_riccati_device();  // per-device kernel attributes
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&h->ws), h->ws_bytes);
+  if (e == hipSuccess && constrained(*dims)) {
+    e = hipMalloc(reinterpret_cast<void**>(&h->ctl), sizeof(int) * 2 * srbd::kCtlCap);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&h->ctl_host), sizeof(int) * srbd::kCtlCap);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&h->ctl_ev[i], hipEventDisableTiming);
+  }
   hipSetDevice(prev);
   if (e != hipSuccess) {
     srbd_qp_destroy(h);
@@ -208,6 +220,10 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   if (h->resc2) hipFree(h->resc2);
   if (h->mixed) hipFree(h->mixed);
   if (h->resc_count_host) hipHostFree(h->resc_count_host);
+  if (h->ctl) hipFree(h->ctl);
+  if (h->ctl_host) hipHostFree(h->ctl_host);
+  for (hipEvent_t ev : h->ctl_ev)
+    if (ev) hipEventDestroy(ev);
   if (h->stream) hipStreamDestroy(h->stream);
   hipSetDevice(prev);
   delete h;
@@ -216,6 +232,14 @@ void srbd_qp_destroy(srbd_qp_handle h) {
 void* srbd_qp_stream(srbd_qp_handle h) { return h ? reinterpret_cast<void*>(h->stream) : nullptr; }
 
 size_t srbd_qp_workspace_bytes(srbd_qp_handle h) { return h ? h->ws_bytes : 0; }
+
+size_t srbd_qp_memory_bytes(srbd_qp_handle h) {
+  if (!h) return 0;
+  return h->ws_bytes + h->stage_bytes + h->pinned_bytes + h->pad_bytes + h->nmpc_bytes +
+         (h->ctl ? sizeof(int) * 3 * srbd::kCtlCap : 0) +
+         h->resc_bytes + h->resc2_bytes + h->mixed_bytes +
+         (h->resc_idx ? sizeof(int) * (2 * (size_t)h->capacity + 1) : 0);
+}
 
 int srbd_qp_synchronize(srbd_qp_handle h) {
   if (!h) return fail(SRBD_QP_EINVAL, "handle is NULL");
@@ -256,7 +280,8 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
 static int fallback_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                         const srbd_qp_data_f64* d, const srbd_qp_solution_f64* sc,
                         const srbd_qp_solution_f64* s, hipStream_t strm, int min_status, int* idx,
-                        void** buf, size_t* buf_bytes);
+                        void** buf, size_t* buf_bytes, const double* warm_x = nullptr,
+                        const double* warm_u = nullptr);
 
 // warm_bars: warm_start 2 only (the fp64 continuation of rescue_f32), see ProblemArgsT;
 // iter_cap >= 0 (the f32_iters continuation): at most that many iterations, while the stat
@@ -326,6 +351,14 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   a.tol_eq = st->tol_eq;
   a.tol_ineq = st->tol_ineq;
   a.tol_comp = st->tol_comp;
+  if (h->ctl) {
+    a.ctl = h->ctl;
+    a.ctl_host = h->ctl_host;
+    a.ctl_cap = srbd::kCtlCap;
+    a.ctl_tag = h->ctl_tag = (h->ctl_tag + 1) & 0x3fffffff;
+    a.ctl_ev[0] = h->ctl_ev[0];
+    a.ctl_ev[1] = h->ctl_ev[1];
+  }
   hipError_t e = hipSuccess;
   // (unconstrained with residuals: unconstr_residuals_kernel clears and fills the table)
   if (s->stat && (constrained(h->dims) || !st->compute_residuals))
@@ -494,15 +527,15 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
 // ---------------------------------------------------------------------------
 // settings.f32_iters: mixed-precision IPM (fp32 iterations, then fp64 to the end)
 // ---------------------------------------------------------------------------
-// A QP a warm-started fp64 continuation ends with status >= min_status is solved again, cold,
-// in fp64 (compact batch in *buf, list in idx).  f32_iters: min_status 2 -- the mixed path
-// never ends a QP worse than the fp64 path would (numerical breakdowns: MinStepLengthReached,
-// NaNDetected; a MaxIterReached QP has spent the iteration budget, as the fp64 path would
-// have).  f64_rescue: min_status 1.
+// A QP a warm-started fp64 continuation ends with status >= min_status is solved again in
+// fp64 (compact batch in *buf, list in idx) exactly as the plain fp64 call solves it: the
+// caller's iter_max, and its x / u warm start when warm_x / warm_u are given (the caller's
+// buffers as they were on entry), cold otherwise.  Both users pass min_status 1, so neither
+// the mixed path (f32_iters) nor the rescue (f64_rescue) ends a QP worse than fp64 does.
 static int fallback_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                         const srbd_qp_data_f64* d, const srbd_qp_solution_f64* sc,
                         const srbd_qp_solution_f64* s, hipStream_t strm, int min_status, int* idx,
-                        void** buf, size_t* buf_bytes) {
+                        void** buf, size_t* buf_bytes, const double* warm_x, const double* warm_u) {
   int prev = 0;
   hipGetDevice(&prev);
   hipSetDevice(h->device);
@@ -565,10 +598,13 @@ static int fallback_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   }
   s2.status = reinterpret_cast<int*>(cur);
   s2.iter = s2.status + R;
+  const bool warm = warm_x && warm_u && st->warm_start;
+  if (warm && e == hipSuccess) e = srbd::launch_gather_rows(warm_x, s2.x, idx, R, (N + 1) * nx, strm);
+  if (warm && e == hipSuccess) e = srbd::launch_gather_rows(warm_u, s2.u, idx, R, N * nu, strm);
   hipSetDevice(prev);
   if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("fallback: ") + hipGetErrorString(e));
   srbd_qp_settings st2 = *st;
-  st2.warm_start = 0;
+  st2.warm_start = warm ? st->warm_start : 0;
   st2.f32_iters = 0;
   int rc = solve_impl<double>(h, R, &st2, &d2, &s2, strm);
   if (rc) return rc;
@@ -603,7 +639,9 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   const size_t warm_e = (N + 1) * (96 + (size_t)((m.ng + 11) / 12) * 48);
   size_t floats = 2 * ex + eu;  // per QP: x, u, pi
   for (const F& f : ins) floats += f.src ? f.e : 0;
-  const size_t need = B * (floats * sizeof(float) + warm_e * sizeof(double)) + 512;
+  // warm_start: the caller's x / u as they are on entry (the fp64 fallback starts from them)
+  const size_t keep_e = st->warm_start ? ex + eu : 0;
+  const size_t need = B * (floats * sizeof(float) + (warm_e + keep_e) * sizeof(double)) + 512;
   int prev = 0;
   hipGetDevice(&prev);
   hipSetDevice(h->device);
@@ -620,7 +658,13 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
     h->mixed_bytes = need;
   }
   double* warm = reinterpret_cast<double*>(h->mixed);
-  float* cur = reinterpret_cast<float*>(warm + B * warm_e);
+  double* keep_x = keep_e ? warm + B * warm_e : nullptr;
+  double* keep_u = keep_e ? keep_x + B * ex : nullptr;
+  float* cur = reinterpret_cast<float*>(warm + B * (warm_e + keep_e));
+  if (keep_e) {
+    e = hipMemcpyAsync(keep_x, s->x, sizeof(double) * B * ex, hipMemcpyDeviceToDevice, strm);
+    if (e == hipSuccess) e = hipMemcpyAsync(keep_u, s->u, sizeof(double) * B * eu, hipMemcpyDeviceToDevice, strm);
+  }
   for (const F& f : ins) {
     if (!f.src || e != hipSuccess) continue;
     e = srbd::launch_narrow(f.src, cur, f.e * B, strm);
@@ -669,7 +713,8 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   if (!sc.status) sc.status = h->resc_idx + h->capacity;
   rc = solve_impl<double>(h, batch, &st64, d, &sc, strm, warm, 0, st->iter_max - n32);
   if (rc) return rc;
-  return fallback_f64(h, batch, st, d, &sc, s, strm, 2, h->resc_idx, &h->resc, &h->resc_bytes);
+  return fallback_f64(h, batch, st, d, &sc, s, strm, 1, h->resc_idx, &h->resc, &h->resc_bytes, keep_x,
+                      keep_u);
 }
 
 // ---------------------------------------------------------------------------
@@ -807,7 +852,12 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
   ss.stat = dp(ostat);
   hipSetDevice(prev);
   rc = solve_impl<T>(h, batch, st, &dd, &ss, nullptr);
-  if (rc) return rc;
+  if (rc) {
+    // copies from the pinned buffer may still be queued: the next call must not
+    // overwrite (or free) it under a pending DMA
+    hipStreamSynchronize(h->stream);
+    return rc;
+  }
   hipSetDevice(h->device);
   if (small) {
     if (e == hipSuccess && in_end < off)

@@ -121,6 +121,7 @@ class HandlePool {
       if (best != free_.size()) {
         Entry e = free_[best];
         free_.erase(free_.begin() + static_cast<long>(best));
+        parked_bytes_ -= e.bytes;
         *capacity = e.capacity;
         return e.h;
       }
@@ -133,11 +134,15 @@ class HandlePool {
   }
   void release(int device, const Shape& s, int capacity, srbd_qp_handle h) {
     if (!h) return;
-    // big workspaces (batched solves) are freed, not parked
-    if (srbd_qp_workspace_bytes(h) <= kMaxPooledBytes) {
+    // big handles (batched solves) are freed, not parked; the count covers everything a
+    // handle holds (workspace, staging, pinned mirror, padding / rescue buffers), and the
+    // parked handles together stay under kMaxPooledBytes
+    const size_t bytes = srbd_qp_memory_bytes(h);
+    {
       std::lock_guard<std::mutex> lk(m_);
-      if (free_.size() < kMaxPooled) {
-        free_.push_back(Entry{device, s, capacity, h});
+      if (free_.size() < kMaxPooled && parked_bytes_ + bytes <= kMaxPooledBytes) {
+        free_.push_back(Entry{device, s, capacity, h, bytes});
+        parked_bytes_ += bytes;
         return;
       }
     }
@@ -150,11 +155,13 @@ class HandlePool {
     Shape shape;
     int capacity;
     srbd_qp_handle h;
+    size_t bytes;  // srbd_qp_memory_bytes when parked
   };
   static constexpr size_t kMaxPooled = 16;
-  static constexpr size_t kMaxPooledBytes = size_t(256) << 20;
+  static constexpr size_t kMaxPooledBytes = size_t(256) << 20;  // all parked handles together
   std::mutex m_;
   std::vector<Entry> free_;
+  size_t parked_bytes_ = 0;
 };
 
 }  // namespace

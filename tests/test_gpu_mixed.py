@@ -71,20 +71,46 @@ def test_mixed_ignored_when_padded_or_unconstrained(pkg):
 
 def test_mixed_iter_max_bounds_the_fp32_pass(pkg):
     """f32_iters >= iter_max: the fp32 pass runs iter_max - 1 iterations and the fp64
-    continuation the one left of the budget; warm-started calls narrow the caller's
-    x / u for the fp32 pass."""
+    continuation the one left of the budget; a QP that one step does not finish is solved
+    again by the plain fp64 path (never worse than fp64: ADVICE r02).  Warm-started calls
+    narrow the caller's x / u for the fp32 pass."""
     qp, x0 = pkg.srbd_model.generate_batch(32, N=20, seed=9, constraints="box_u")
     o64 = pkg.capi.solve(qp, x0, NMPC)
-    mix = pkg.capi.solve(qp, x0, dict(NMPC, iter_max=8, f32_iters=50))
-    assert np.all(mix["iter"] == 1), mix["iter"]
-    assert np.all(mix["status"] <= 1), mix["status"]
-    assert np.all(mix["res"][mix["status"] == 0] <= 1e-4)
+    plain8 = pkg.capi.solve(qp, x0, dict(NMPC, iter_max=8), stats=True)
+    mix = pkg.capi.solve(qp, x0, dict(NMPC, iter_max=8, f32_iters=50), stats=True)
+    assert np.all(mix["status"] <= plain8["status"]), (mix["status"], plain8["status"])
+    cont = mix["iter"] == 1  # finished by the one fp64 step of the continuation
+    assert np.all(mix["status"][cont] == 0) and np.all(mix["res"][cont] <= 1e-4)
+    for key in ("x", "u", "pi", "status", "iter", "res", "obj", "stat"):
+        assert np.array_equal(mix[key][~cont], plain8[key][~cont]), key
+    # the fp64 path converges at iter_max = 30: so does the mixed path with f32_iters >= iter_max
+    assert np.all(o64["status"] == 0)
+    mix30 = pkg.capi.solve(qp, x0, dict(NMPC, f32_iters=50))
+    assert np.all(mix30["status"] == 0), mix30["status"]
+    assert np.all(mix30["res"] <= 1e-4)
     warm = pkg.capi.solve(qp, x0, dict(NMPC, warm_start=1, f32_iters=4),
                           x_init=o64["x"], u_init=o64["u"])
     assert np.all(warm["status"] == 0), warm["status"]
     assert np.all(warm["res"] <= 1e-4)
     # (a different tol-1e-4 KKT point than the cold solve's: the warm start re-centres
     # lam = mu0 / t, and the SRBD R has 1e-4 curvature directions, so no closeness bound)
+
+
+def test_mixed_fallback_keeps_the_callers_warm_start(pkg):
+    """warm_start = 1: a QP the continuation leaves unsolved is solved again by the fp64
+    path from the caller's own x / u (kept on entry), so it ends bit for bit as the plain
+    warm-started fp64 call ends it."""
+    qp, x0 = pkg.srbd_model.generate_batch(200, N=20, seed=29, constraints="box_u")
+    o64 = pkg.capi.solve(qp, x0, NMPC)
+    xi = o64["x"] + 0.01 * np.sin(np.arange(o64["x"].size)).reshape(o64["x"].shape)
+    ui = o64["u"] + 0.5 * np.cos(np.arange(o64["u"].size)).reshape(o64["u"].shape)
+    st = dict(NMPC, iter_max=3, warm_start=1)
+    plain = pkg.capi.solve(qp, x0, st, x_init=xi, u_init=ui, stats=True)
+    mix = pkg.capi.solve(qp, x0, dict(st, f32_iters=2), x_init=xi, u_init=ui, stats=True)
+    bad = mix["status"] != 0
+    assert bad.sum() > 10, np.bincount(mix["status"])
+    for key in ("x", "u", "pi", "status", "iter", "res", "obj", "stat"):
+        assert np.array_equal(mix[key][bad], plain[key][bad]), key
 
 
 def test_mixed_host_entry_point_matches_device(pkg):
@@ -129,14 +155,19 @@ def test_mixed_fallback_is_the_fp64_solve(pkg):
 def test_mixed_iteration_budget(pkg, f32_iters):
     """The fp32 iterations count against iter_max: m = min(f32_iters, iter_max - 1) fp32
     iterations, then at most iter_max - m fp64 ones (reported in iter).  At iter_max = 3
-    most QPs end MaxIterReached and are returned as they are, not solved again."""
+    most QPs are not finished there; each of those is solved again by the fp64 path and
+    returns exactly its result (here MaxIterReached after 3 fp64 iterations)."""
     qp, x0 = pkg.srbd_model.generate_batch(300, N=20, seed=23, constraints="box_u")
     st = dict(NMPC, iter_max=3)
+    plain = pkg.capi.solve(qp, x0, st, stats=True)
     mix = pkg.capi.solve(qp, x0, dict(st, f32_iters=f32_iters), stats=True)
     m = min(f32_iters, 2)
-    assert np.all(mix["iter"] <= 3 - m) and np.all(mix["iter"] >= 1)
-    assert np.all(mix["status"] <= 1), np.bincount(mix["status"])
-    assert (mix["status"] == 1).sum() > 100, np.bincount(mix["status"])
+    ok = mix["status"] == 0
+    assert np.all(mix["iter"][ok] <= 3 - m) and np.all(mix["iter"] >= 1)
+    assert (~ok).sum() > 100, np.bincount(mix["status"])
+    for key in ("x", "u", "pi", "status", "iter", "res", "obj", "stat"):
+        assert np.array_equal(mix[key][~ok], plain[key][~ok]), key
+    assert np.all(mix["status"] <= plain["status"])
     # the stat table keeps the caller's iter_max + 2 rows; rows past the last fp64 one are 0
     assert mix["stat"].shape[1] == 5
     for i in range(qp.batch):
