@@ -415,6 +415,7 @@ def main():
                                                                   args.seed, rescue=RESCUE_CAP)
         secondary["nmpc_step_config1"] = nmpc_config1(pkg, capi, device, args.seed,
                                                       with_cpu=not args.no_cpu_baseline)
+        secondary["unconstr_n20_full_outputs"] = full_outputs_line(pkg, capi, device, args.seed)
 
     traffic = pmc_traffic(args.workload, batch)
     line = {
@@ -562,6 +563,55 @@ def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=
     del h
     torch.cuda.empty_cache()
     return out
+
+
+def full_outputs_line(pkg, capi, device, seed, batch=65536, N=20, steps=5, warmup=1):
+    """The headline workload with everything hpipm-cpp's solve() returns
+    (ocp_qp_ipm_solver.cpp:337-403): x, u, pi plus the Riccati matrices P, p, K, k of
+    every stage and the KKT residual norms / objective (stat row 0 too), i.e. the
+    solve kernel writing P, p, K, k beside its records and the residual kernel's
+    extra pass over the QP data.  Same timing as the main line (HIP events on the
+    handle's stream)."""
+    import torch
+    h = capi.Handle(N, 12, 12, 0, False, False, capacity=batch, device=device.index or 0)
+    dt, _, _, _ = device_shard(pkg, h, N, "none", batch, 0, seed, device)
+    f = dict(dtype=torch.float64, device=device)
+    s = {"x": torch.zeros(batch, N + 1, 12, **f), "u": torch.zeros(batch, N, 12, **f),
+         "pi": torch.zeros(batch, N + 1, 12, **f),
+         "P": torch.zeros(batch, N + 1, 12, 12, **f), "p": torch.zeros(batch, N + 1, 12, **f),
+         "K": torch.zeros(batch, N, 12, 12, **f), "k": torch.zeros(batch, N, 12, **f),
+         "status": torch.zeros(batch, dtype=torch.int32, device=device),
+         "iter": torch.zeros(batch, dtype=torch.int32, device=device),
+         "res": torch.zeros(batch, 4, **f), "obj": torch.zeros(batch, **f)}
+    data = capi.Data(**{k: (None if dt.get(k) is None else dt[k].data_ptr()) for k in capi.DATA_FIELDS})
+    sol = capi.Solution(**{k: (s[k].data_ptr() if k in s else None) for k in capi.SOL_FIELDS})
+    st = capi.settings_struct(NMPC_SETTINGS)
+    ext = torch.cuda.ExternalStream(h.stream(), device=device)
+    for _ in range(warmup):
+        h.solve_device(batch, st, data, sol)
+    h.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(ext)
+    for _ in range(steps):
+        h.solve_device(batch, st, data, sol)
+    ev1.record(ext)
+    h.synchronize()
+    t_wall = time.perf_counter() - t0
+    ms = ev0.elapsed_time(ev1) / steps
+    out_b = 8 * ((N + 1) * (144 + 12) + N * (144 + 12) + 4 + 1)  # P, p, K, k, res, obj
+    res = s["res"].cpu().numpy()
+    line = {"description": "unconstr_n20 with the whole hpipm-cpp output set: x, u, pi, P, p, K, k, "
+                           "res (4 norms), obj; solve kernel + residual kernel",
+            "batch": batch, "N": N, "steps": steps, "value": batch * steps / t_wall, "unit": "QP solves/s",
+            "kernel_ms": ms, "success_rate": float((s["status"] == 0).float().mean()),
+            "bytes_per_qp": {"algorithmic_x_u_pi": alg_bytes_per_qp(N), "extra_outputs": out_b,
+                             "residual_pass_reads": alg_bytes_per_qp(N) - 8 * ((N + 1) * 12 + N * 12 + (N + 1) * 12)},
+            "max_res_stat": float(res[:, 0].max()), "max_res_eq": float(res[:, 1].max())}
+    log(f"[secondary] full outputs: kernel {ms:.2f} ms, {line['value']:.4g} QP/s")
+    del h, dt, s
+    torch.cuda.empty_cache()
+    return line
 
 
 def nmpc_config1(pkg, capi, device, seed, batch=65536, N=20, sqp_max_loop=15, reps=3,

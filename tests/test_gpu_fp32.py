@@ -30,7 +30,8 @@ def test_box_u_fp32_vs_fp64(pkg):
     o32 = pkg.capi.solve(qp, x0, NMPC, dtype=np.float32)
     o64 = pkg.capi.solve(qp, x0, NMPC)
     assert np.all(o64["status"] == 0)
-    assert np.mean(o32["status"] == 0) >= 0.95, o32["status"]
+    # (measured r03: 64 / 64 Success, u within 8.9e-4 and x within 6.6e-4 of fp64)
+    assert np.all(o32["status"] == 0), o32["status"]
     ok = o32["status"] == 0
     assert np.all(o32["res"][ok] <= 1e-4)
     for i in np.nonzero(ok)[0]:
@@ -49,7 +50,8 @@ def test_friction_cone_fp32_vs_oracle(pkg, oracle):
     o32 = pkg.capi.solve(qp, x0, F32, dtype=np.float32)
     ref = oracle.solve(qp, NMPC, x0=x0)
     assert np.all(ref["status"] == 0)
-    assert np.mean(o32["status"] == 0) >= 0.95, o32["status"]
+    # (measured r03: 63 / 64 Success, one MinStepLengthReached at the fp32 floor)
+    assert (o32["status"] == 0).sum() >= 63, np.bincount(o32["status"])
     ok = o32["status"] == 0
     assert np.all(o32["res"][ok][:, 0] <= F32["tol_stat"])
     assert np.all(o32["res"][ok][:, 1:] <= 1e-3)
@@ -125,7 +127,8 @@ def test_f64_rescue_cone_n40(pkg, cap, stats, batch):
     assert np.all(resc["res"][bad][:, 1:] <= 1e-3)
     ru = [np.linalg.norm(resc["u"][i] - o64["u"][i]) / np.linalg.norm(o64["u"][i])
           for i in np.nonzero(bad)[0]]
-    assert np.median(ru) <= 3e-2 and np.max(ru) <= 2e-1, (np.median(ru), np.max(ru))
+    # (measured r03: median 5e-5..1.9e-4, max 6.6e-4 at cap 12 and 2.0e-3 at cap 30)
+    assert np.median(ru) <= 1e-3 and np.max(ru) <= 5e-3, (np.median(ru), np.max(ru))
     # continued in fewer iterations than a cold fp64 solve, or re-solved cold
     cold = pkg.capi.solve(_rounded_to_f32(qp), x0.astype(np.float32).astype(np.float64), st)
     n_cont = 0

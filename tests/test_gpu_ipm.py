@@ -82,9 +82,15 @@ def test_constrained_vs_oracle(pkg, oracle, dims, ric_alg):
         eps = np.finfo(float).eps
         scale = (np.linalg.norm(A0) * np.linalg.norm(x0[i]) + np.linalg.norm(B0) *
                  np.linalg.norm(out["u"][i, 0]) + np.linalg.norm(b0) + np.linalg.norm(out["x"][i, 1]))
-        bound = 1e-6 * np.linalg.norm(pi0) + 64 * eps * np.linalg.norm(A0) * np.linalg.norm(out["P"][i, 1]) * scale
-        assert np.linalg.norm(out["pi"][i, 0] - pi0) <= bound, ("pi0", i)
-        assert helpers.is_approx(out["pi"][i, 0], ref["pi"][i, 0], 1e-3), ("pi0 vs oracle", i)
+        cond = 64 * eps * np.linalg.norm(A0) * np.linalg.norm(out["P"][i, 1]) * scale
+        assert np.linalg.norm(out["pi"][i, 0] - pi0) <= 1e-6 * np.linalg.norm(pi0) + cond, ("pi0", i)
+        # the oracle's pi_0 in the same stationarity form, from its own u0, x1, pi1, P1:
+        # 1e-7 (the x / u bar) plus the same rounding term of res_b0 (measured r03: ric_alg 1
+        # 1e-12..5e-9 relative; ric_alg 0 up to 3e-5 at 5 x 3, where |P_1| res_b0 dominates)
+        rb0r = A0 @ x0[i] + B0 @ ref["u"][i, 0] + b0 - ref["x"][i, 1]
+        pi0r = (qp.Q[i, 0] @ x0[i] + qp.S[i, 0].T @ ref["u"][i, 0] + qp.q[i, 0]
+                + A0.T @ (ref["pi"][i, 1] + ref["P"][i, 1] @ rb0r))
+        assert np.linalg.norm(pi0 - pi0r) <= 1e-7 * np.linalg.norm(pi0r) + cond, ("pi0 vs oracle", i)
         assert np.all(out["res"][i] <= 1e-8)
 
 
