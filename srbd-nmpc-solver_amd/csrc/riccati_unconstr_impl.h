@@ -23,14 +23,6 @@ namespace SRBD_NS {
 
 using real = SRBD_REAL;
 
-// out[i] = v[i] for i < n (static register indices, predicated stores)
-__device__ __forceinline__ void store_n(real* out, int n, const real (&v)[12]) {
-  sfor<0, 12>([&](auto i) {
-    constexpr int I = decltype(i)::value;
-    if (I < n) out[I] = v[I];
-  });
-}
-
 // ---- where a QP's blocks and records are ----
 
 // HBM, the C-ABI layout: QP-major ([batch][stage][blk], Eigen order) or stage-major
@@ -155,11 +147,12 @@ __device__ __forceinline__ void store_riccati_out(const ProblemArgsT<real>& a, i
                                                   const real (&F)[12], const real (&Kc)[12]) {
   const int N = a.N;
   const bool own = lane < kMaxDim, isv = lane == kVecLane;
-  if (a.P && own) store_n(a.P + ((size_t)qp * (N + 1) + k) * 144 + (size_t)lane * 12, 12, F);
-  if (a.p && isv) store_n(a.p + ((size_t)qp * (N + 1) + k) * 12, 12, F);
+  // (vector stores: the C-ABI requires 16-byte aligned base pointers, include/srbd_qp.h)
+  if (a.P && own) store12(a.P + ((size_t)qp * (N + 1) + k) * 144 + (size_t)lane * 12, F);
+  if (a.p && isv) store12(a.p + ((size_t)qp * (N + 1) + k) * 12, F);
   if (k < N) {
-    if (a.K && own) store_n(a.K + ((size_t)qp * N + k) * 144 + (size_t)lane * 12, 12, Kc);
-    if (a.k && isv) store_n(a.k + ((size_t)qp * N + k) * 12, 12, Kc);
+    if (a.K && own) store12(a.K + ((size_t)qp * N + k) * 144 + (size_t)lane * 12, Kc);
+    if (a.k && isv) store12(a.k + ((size_t)qp * N + k) * 12, Kc);
   }
 }
 
@@ -511,9 +504,143 @@ __global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(Problem
   }
 }
 
+// The same residuals for large batches, on the solve's layout: one 16-lane group per QP
+// (16 QPs per workgroup), lane j < 12 owning column j of every stage block (16-byte column
+// loads, as the solve reads them), the QP's stages in order.  The column-shaped products
+// (A'pi, B'pi, S'u) are DPP dot products; the row-shaped ones (A x + B u, R u + S x, Q x)
+// are formed column by column and summed across the group through its 12 x 12 LDS block.
+// The objective uses u'Sx = x'(S'u) and takes u'(Ru + Sx) from the row sums: the same
+// quantities as the oracle's, summed in another order.  FULL: nx = nu = 12.
+template <bool FULL>
+__global__ void __launch_bounds__(256) unconstr_residuals_group_kernel(ProblemArgsT<real> a) {
+  __shared__ __attribute__((aligned(16))) real tb_all[(256 / kGroup) * 144];
+  const int qp = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4);
+  const int lane = threadIdx.x & (kGroup - 1);
+  if (qp >= a.batch) return;
+  real* const tb = tb_all + (threadIdx.x >> 4) * 144;
+  const int N = a.N, nx = FULL ? 12 : a.nx, nu = FULL ? 12 : a.nu;
+  if (a.stat) {  // the QP's stat table is cleared here, row 0 filled below
+    real* tab = a.stat + (size_t)qp * a.stat_rows * kStatCols;
+    for (int i = lane; i < a.stat_rows * kStatCols; i += kGroup) tab[i] = real(0);
+  }
+  const bool smaj = a.layout == 1;
+  auto at = [&](const real* base, int nstage, size_t blk, int k) -> const real* {
+    return smaj ? base + ((size_t)k * a.batch + qp) * blk : base + ((size_t)qp * nstage + k) * blk;
+  };
+  const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu, nuu = (size_t)nu * nu;
+  const real* x = a.x + (size_t)qp * (N + 1) * nx;
+  const real* u = a.u + (size_t)qp * N * nu;
+  const real* pi = a.pi + (size_t)qp * (N + 1) * nx;
+  const int li = lane < kMaxDim ? lane : 0;
+  const bool xl = lane < nx, ul = lane < nu;
+  // column j (= lane) of a rows x cols column-major block, zero past the block
+  auto colv = [&](const real* blk, int rows, int cols, real (&v)[12]) {
+    if constexpr (FULL) {
+      load12(blk + li * 12, v);
+    } else {
+      load_col_pad(blk + (size_t)li * rows, rows, lane < cols, v);
+    }
+  };
+  // lane i <- sum over columns j of T_j[i] (lane j holds T_j)
+  auto row_sum = [&](const real (&T)[12]) -> real {
+    lds_wave_fence();  // the previous sum's reads are done
+    if (lane < kMaxDim) store12(tb + lane * 12, T);
+    lds_wave_fence();
+    real s = real(0);
+    sfor<0, 12>([&](auto j) { s += tb[decltype(j)::value * 12 + li]; });
+    return s;
+  };
+  real mg = real(0), mb = real(0), ob = real(0);
+#pragma unroll 1
+  for (int k = 0; k <= N; ++k) {
+    const real xk = xl ? x[(size_t)k * nx + lane] : real(0);
+    real T[12];
+    real gx = real(0);  // x-row stationarity residual (k >= 1)
+    if (k > 0) {
+      real Qc[12];
+      colv(at(a.Q, N + 1, nxx, k), nx, nx, Qc);
+      sfor<0, 12>([&](auto i) { T[decltype(i)::value] = Qc[decltype(i)::value] * xk; });
+      const real qx = row_sum(T);  // (Q x)_i
+      const real qk = xl ? at(a.q, N + 1, nx, k)[lane] : real(0);
+      gx = qx + qk - (xl ? pi[(size_t)k * nx + lane] : real(0));
+      if (xl) ob += xk * (real(0.5) * qx + qk);
+    }
+    if (k < N) {
+      const real uk = ul ? u[(size_t)k * nu + lane] : real(0);
+      const real xn = xl ? x[(size_t)(k + 1) * nx + lane] : real(0);
+      const real pin = xl ? pi[(size_t)(k + 1) * nx + lane] : real(0);
+      real Ac[12], Bc[12];
+      colv(at(a.A, N, nxx, k), nx, nx, Ac);
+      colv(at(a.B, N, nxu, k), nx, nu, Bc);
+      const real atp = dot_bcast(Ac, pin, real(0));  // (A'pi_{k+1})_j
+      const real btp = dot_bcast(Bc, pin, real(0));  // (B'pi_{k+1})_j
+      sfor<0, 12>([&](auto i) {
+        constexpr int I = decltype(i)::value;
+        T[I] = fmadd(Ac[I], xk, Bc[I] * uk);
+      });
+      const real axbu = row_sum(T);  // (A x + B u)_i
+      if (xl) max_nan(mb, axbu + at(a.b, N, nx, k)[lane] - xn);
+      real Sc[12], Rc[12];
+      colv(at(a.S, N, nxu, k), nu, nx, Sc);
+      colv(at(a.R, N, nuu, k), nu, nu, Rc);
+      const real stu = dot_bcast(Sc, uk, real(0));  // (S'u)_j
+      sfor<0, 12>([&](auto i) {
+        constexpr int I = decltype(i)::value;
+        T[I] = fmadd(Rc[I], uk, Sc[I] * xk);
+      });
+      const real rusx = row_sum(T);  // (R u + S x)_i
+      const real rk = ul ? at(a.r, N, nu, k)[lane] : real(0);
+      if (ul) {
+        max_nan(mg, rusx + rk + btp);
+        ob += uk * (real(0.5) * rusx + rk);
+      }
+      if (xl) ob += real(0.5) * xk * stu;
+      gx += stu + atp;
+    }
+    if (k > 0 && xl) max_nan(mg, gx);
+  }
+  // group reduction: NaN-propagating max of mg, mb; sum of ob (lanes >= 12 hold 0)
+  sfor<0, 4>([&](auto s) {
+    constexpr int M = 8 >> decltype(s)::value;
+    const real og = __shfl_xor(mg, M, kGroup), obb = __shfl_xor(mb, M, kGroup);
+    if (og > mg || og != og) mg = og;
+    if (obb > mb || obb != obb) mb = obb;
+    ob += __shfl_xor(ob, M, kGroup);
+  });
+  if (lane == 0) {
+    if (a.res) {
+      a.res[(size_t)qp * 4 + 0] = mg;
+      a.res[(size_t)qp * 4 + 1] = mb;
+      a.res[(size_t)qp * 4 + 2] = real(0);
+      a.res[(size_t)qp * 4 + 3] = real(0);
+    }
+    if (a.obj) a.obj[qp] = ob;
+    if (a.stat) {
+      real* row = a.stat + (size_t)qp * a.stat_rows * kStatCols;
+      row[6] = mg;
+      row[7] = mb;
+      row[10] = ob;
+    }
+    if (a.status && (mg != mg || mb != mb)) a.status[qp] = 3;  // NaNDetected
+  }
+}
+
+// small batches (the reference's one QP per call): the stage-parallel kernel above, whose
+// latency is a few memory round trips; large ones: the group kernel (one pass over the data)
+constexpr int kResGroupMin = 256;
+
 hipError_t launch_residuals(const ProblemArgsT<real>& a, hipStream_t stream) {
   if (a.batch <= 0) return hipSuccess;
-  hipLaunchKernelGGL(unconstr_residuals_kernel, dim3((unsigned)a.batch), dim3(kResThreads), 0, stream, a);
+  if (a.batch <= kResGroupMin) {
+    hipLaunchKernelGGL(unconstr_residuals_kernel, dim3((unsigned)a.batch), dim3(kResThreads), 0, stream, a);
+    return hipGetLastError();
+  }
+  const unsigned blocks = (unsigned)(((long long)a.batch * kGroup + 255) / 256);
+  if (a.nx == 12 && a.nu == 12) {
+    hipLaunchKernelGGL(unconstr_residuals_group_kernel<true>, dim3(blocks), dim3(256), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(unconstr_residuals_group_kernel<false>, dim3(blocks), dim3(256), 0, stream, a);
+  }
   return hipGetLastError();
 }
 

@@ -228,6 +228,62 @@ def test_unconstrained_residuals_and_objective(pkg, oracle, case):
     assert np.all(zero["res"] == 0) and np.all(zero["obj"] == 0)
 
 
+@pytest.mark.parametrize("case", ["srbd", "padded", "stage_major", "nan"])
+def test_residuals_large_batch_group_kernel(pkg, oracle, case):
+    """Batches over 256 QPs take the group-mapped residual kernel (one 16-lane group per
+    QP, the solve's column-owned loads): obj against the oracle's compute_residuals at
+    1e-10, res at rounding level of the terms, NaN data -> NaNDetected, and on the same
+    QPs the small-batch (stage-parallel) kernel's obj to 1e-12."""
+    import torch
+    B, N = 300, 12
+    if case == "padded":
+        qp, x0 = helpers.random_unconstrained(B, N, 7, 5, 611, pkg.OcpQpBatch)
+        rho = np.max(np.abs(np.linalg.eigvals(qp.A)), axis=-1)
+        qp.A = qp.A / rho[..., None, None]
+    else:
+        qp, x0 = pkg.srbd_model.generate_batch(B, N=N, seed=612, constraints="none")
+    if case == "nan":
+        qp.R[7, 3, 2, 2] = np.nan
+    if case == "stage_major":
+        h = pkg.capi.Handle(N, 12, 12, 0, False, False, capacity=B, layout=1)
+        p = qp.packed()
+        p["x0"] = np.ascontiguousarray(x0)
+        dev = {k: (torch.from_numpy(v).cuda().transpose(0, 1).contiguous() if k != "x0"
+                   else torch.from_numpy(v).cuda()) for k, v in p.items() if v is not None}
+        f64 = dict(dtype=torch.float64, device="cuda")
+        sol = {"x": torch.zeros(B, N + 1, 12, **f64), "u": torch.zeros(B, N, 12, **f64),
+               "pi": torch.zeros(B, N + 1, 12, **f64), "res": torch.zeros(B, 4, **f64),
+               "obj": torch.zeros(B, **f64), "status": torch.zeros(B, dtype=torch.int32, device="cuda")}
+        data = pkg.capi.Data(**{k: (dev[k].data_ptr() if k in dev else None) for k in pkg.capi.DATA_FIELDS})
+        S = pkg.capi.Solution(**{k: (sol[k].data_ptr() if k in sol else None) for k in pkg.capi.SOL_FIELDS})
+        h.solve_device(B, pkg.capi.settings_struct(dict(iter_max=30)), data, S)
+        h.synchronize()
+        out = {k: v.cpu().numpy() for k, v in sol.items()}
+    else:
+        out = pkg.capi.solve(qp, x0, dict(iter_max=30), stats=True)
+    if case == "nan":
+        assert out["status"][7] == 3 and np.isnan(out["res"][7, 0])
+        ok = np.arange(B) != 7
+        assert np.all(out["status"][ok] == 0)
+        return
+    ref = oracle.solve(qp, dict(iter_max=30), x0=x0)
+    scale = max(1.0, float(np.abs(ref["obj"]).max()))
+    np.testing.assert_allclose(out["obj"], ref["obj"], rtol=1e-10, atol=1e-12 * scale)
+    # rounding-level numbers (both solutions differ at ~1e-15): over 300 QPs the worst one
+    # reaches 1.0e-12 of the terms' magnitude, so the bar is 4e-12 here, for the oracle too
+    mag = np.array([max(np.abs(out[k][i]).max() for k in ("x", "u", "pi")) for i in range(B)])
+    for j in (0, 1):
+        assert np.all(out["res"][:, j] <= 4e-12 * mag), (j, np.max(out["res"][:, j] / mag))
+        assert np.all(ref["res"][:, j] <= 4e-12 * mag), (j, np.max(ref["res"][:, j] / mag))
+    assert np.all(out["res"][:, 2:] == 0)
+    if case != "stage_major":
+        assert np.array_equal(out["stat"][:, 0, 6], out["res"][:, 0])
+        assert np.array_equal(out["stat"][:, 0, 10], out["obj"])
+        assert np.all(out["stat"][:, 1:] == 0)
+        small = pkg.capi.solve(qp.subset(slice(0, 200)), x0[:200], dict(iter_max=30))
+        np.testing.assert_allclose(out["obj"][:200], small["obj"], rtol=1e-12, atol=1e-13 * scale)
+
+
 @pytest.mark.parametrize("ric_alg", [0, 1])
 @pytest.mark.parametrize("dtype,N", [(np.float64, 20), (np.float64, 26), (np.float32, 40)])
 def test_latency_kernel_bit_identical(pkg, dtype, N, ric_alg):
