@@ -18,12 +18,20 @@ __global__ void write_k(d2* p, size_t n, double v, int nt) {
   }
 }
 
+// 8 independent 16-byte loads in flight per lane per step (whole 1 KiB per wave-instruction)
 template <int NT>
 __global__ void read_k(const d2* p, size_t n, double* sink) {
   d2 acc = {0.0, 0.0};
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    if constexpr (NT) acc += __builtin_nontemporal_load(p + i);
-    else acc += p[i];
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i + 7 * stride < n; i += 8 * stride) {
+    d2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if constexpr (NT) v[u] = __builtin_nontemporal_load(p + i + u * stride);
+      else v[u] = p[i + u * stride];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
   }
   if (acc.x == -1.2345) sink[0] = acc.y;  // never: keeps the loads
 }
@@ -37,7 +45,7 @@ int main(int argc, char** argv) {
   hipMalloc(&rec, nr * 16);
   hipMalloc(&in, ni * 16);
   hipMalloc(&sink, 8);
-  const dim3 g(256 * 16), b(256);
+  const dim3 g(256 * 8), b(256);
   hipLaunchKernelGGL(write_k, g, b, 0, 0, in, ni, 1.0, 0);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);

@@ -1617,6 +1617,12 @@ __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase2
   if constexpr (PH1 == kPhRB) report_running(a);
 }
 
+// diagnostic builds (-DSRBD_IPM_SPLIT=1, profiling only): every sweep its own launch
+#ifndef SRBD_IPM_SPLIT
+#define SRBD_IPM_SPLIT 0
+#endif
+constexpr bool kIpmSplit = SRBD_IPM_SPLIT != 0;
+
 template <bool FULL, int GEN, bool SQRT>
 static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream) {
   const int threads = 256;
@@ -1642,14 +1648,23 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
         hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT>), grid, block, 0, stream, b);
       break;
     }
-    hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT>), grid, block, 0, stream, b);
+    if (kIpmSplit) {  // diagnostic schedule: one launch per sweep
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT>), grid, block, 0, stream, b);
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF1, SQRT>), grid, block, 0, stream, b);
+    } else {
+      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT>), grid, block, 0, stream, b);
+    }
     hipEvent_t ev = ctl ? reinterpret_cast<hipEvent_t>(a.ctl_ev[it & 1]) : nullptr;
     if (ctl) {
       hipError_t e = hipEventRecord(ev, stream);
       if (e != hipSuccess) return e;
     }
-    if (a.pred_corr)
+    if (a.pred_corr && kIpmSplit) {
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhB2, SQRT>), grid, block, 0, stream, b);
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF2, SQRT>), grid, block, 0, stream, b);
+    } else if (a.pred_corr) {
       hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhB2, kPhF2, SQRT>), grid, block, 0, stream, b);
+    }
     if (ctl && it >= 1) {
       hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(a.ctl_ev[(it - 1) & 1]));
       if (e != hipSuccess) return e;
