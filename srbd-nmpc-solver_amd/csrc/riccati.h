@@ -39,6 +39,32 @@
 
 namespace srbd {
 
+// Diagnostic phase timestamps (builds with -DSRBD_TSTAMP=1 only, read back by
+// srbd_qp_diag_tstamps in such a build): lane 0 of workgroup 0 appends (id, cycle counter)
+// at the phase boundaries of a stage -- the critical path of a single-QP solve.
+#ifndef SRBD_TSTAMP
+#define SRBD_TSTAMP 0
+#endif
+constexpr int kTstampCap = 4096;
+#if SRBD_TSTAMP
+static __device__ unsigned long long g_tstamp[2 * kTstampCap];
+static __device__ unsigned int g_tstamp_n;
+#endif
+__device__ __forceinline__ void tstamp(int id) {
+#if SRBD_TSTAMP
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const unsigned i = g_tstamp_n;
+    if (i < kTstampCap) {
+      g_tstamp[2 * i] = (unsigned long long)id;
+      g_tstamp[2 * i + 1] = __builtin_readcyclecounter();
+      g_tstamp_n = i + 1;
+    }
+  }
+#else
+  (void)id;
+#endif
+}
+
 // C[:,l] += P M[:,l]: P symmetric & column-owned, M column-owned (fused
 // v_fmac_*_dpp blocks of qp_group.h: the broadcast rides on the FMA).
 template <typename T>
@@ -204,9 +230,11 @@ __device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], const int
   // ---- Y = L^-1 H, K = -L^-T Y
   trsv_lower(o.Lc, o.rs, o.H);
   SRBD_PHASE_FENCE();
+  tstamp(7);
   launder(o.Lc);
   trsv_upper_t_neg_axpy(o.Lc, o.rs, o.H, o.Kc);
   SRBD_PHASE_FENCE();
+  tstamp(8);
   if constexpr (MidAt == 2) {
     mid();
     SRBD_PHASE_FENCE();
@@ -218,9 +246,12 @@ __device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], const int
     tmul_acc(o.H, Hn, o.F);
   }
   SRBD_PHASE_FENCE();
+  tstamp(9);
   // ---- Acl = A + B K (VL: bcl = b + B k)
   launder(B_);
   sym_mul_col(B_, o.Kc, A_);  // A[i][l] += B[i][m] K[m][l]: bc<m>(B_[i]) * Kc[m]
+  SRBD_PHASE_FENCE();
+  tstamp(10);
   if constexpr (SYMP) {
     SRBD_PHASE_FENCE();
     symmetrize_lower(o.F, lane);  // (B dead here: fewer live registers)
@@ -247,13 +278,16 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
     sfor<0, 12>([&](auto i) { WB[decltype(i)::value] = T(0); });
     sym_mul_col(P, B_, WB);
     SRBD_PHASE_FENCE();
+    tstamp(1);
     TG G[12];
     loadR(G);
     tmul_acc_g(B_, WB, G);
     SRBD_PHASE_FENCE();
+    tstamp(2);
     chol_g(G, lane, reg, o);
   }
   SRBD_PHASE_FENCE();
+  tstamp(3);
   // ---- W = P [A | b] (+ p on VL); H = S + B'W; F = Q + A'W
   {
     T Pl[12], Bl[12];
@@ -271,12 +305,15 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
     });
     sym_mul_col(Pl, A_, W);
     SRBD_PHASE_FENCE();
+    tstamp(4);
     loadSQ(o.H, o.F);
     tmul_acc(Bl, W, o.H);
     SRBD_PHASE_FENCE();
+    tstamp(5);
     tmul_acc(A_, W, o.F);
   }
   SRBD_PHASE_FENCE();
+  tstamp(6);
   riccati_tail<MidAt, SYMP>(A_, B_, lane, o, mid);
 }
 

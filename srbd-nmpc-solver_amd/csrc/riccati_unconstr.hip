@@ -58,3 +58,20 @@ hipError_t launch_unconstr_residuals<float>(const ProblemArgsT<float>& a, hipStr
 }
 
 }  // namespace srbd
+
+#if SRBD_TSTAMP
+// Diagnostic builds only (not part of include/srbd_qp.h): copy the (id, cycle) pairs the
+// last launches appended (this translation unit's buffer: the unconstrained kernels) and
+// reset the buffer; returns the number of pairs.
+extern "C" int srbd_qp_diag_tstamps(unsigned long long* out, int cap) {
+  unsigned n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(srbd::g_tstamp_n), sizeof n) != hipSuccess) return -1;
+  if (n > (unsigned)srbd::kTstampCap) n = srbd::kTstampCap;
+  if ((int)n > cap) n = (unsigned)cap;
+  if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(srbd::g_tstamp), 2 * sizeof(unsigned long long) * n) != hipSuccess)
+    return -1;
+  const unsigned zero = 0;
+  hipMemcpyToSymbol(HIP_SYMBOL(srbd::g_tstamp_n), &zero, sizeof zero);
+  return (int)n;
+}
+#endif

@@ -302,6 +302,7 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
       }
     };
     StageFactor<real> f;
+    tstamp(0);
     if constexpr (SQRT) {
       riccati_step_sqrt(P, A_, B_, loadR, loadSQ, lane, reg, f);
     } else {
@@ -312,6 +313,7 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
     } else {
       store_rec(src.rec(k), lane, f.Kc, A_, f.F);
     }
+    tstamp(11);
     store_riccati_out(a, qp, k, lane, f.F, f.Kc);
     sfor<0, 12>([&](auto i) {
       constexpr int I = decltype(i)::value;
@@ -319,7 +321,9 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
     });
     if constexpr (SQRT) sqrt_factor(P, lane);
   }
+  tstamp(12);
   fwd_sweep(a, src, qp, lane);
+  tstamp(13);
 }
 
 // Large batches: 16 QPs per 256-thread workgroup, 2 workgroups per CU (the kernel needs
@@ -341,10 +345,13 @@ __global__ void __launch_bounds__(256, 2) riccati_unconstr_kernel(ProblemArgsT<r
   }
 }
 
-// Small batches: one QP per 64-thread workgroup.  All 64 lanes copy the QP into the LDS
-// image with 16-byte global->LDS DMA (one wave-instruction fills 1 KiB of the image; each
-// lane gathers its own 16 bytes from the QP-major buffers), then lanes 0-15 solve.
+// Small batches: one QP per workgroup.  kLdsCopyThreads lanes (8 waves) copy the QP into the
+// LDS image with 16-byte global->LDS DMA (one wave-instruction fills 1 KiB of the image; each
+// lane gathers its own 16 bytes from the QP-major buffers), then lanes 0-15 solve.  One wave
+// issuing the whole copy took ~40 us of the ~160 us single-QP solve (the DMA issue rate of a
+// wave, scripts/dev/latency_breakdown.py); eight issue it in parallel.
 constexpr int kRealsPerDma = 16 / (int)sizeof(real);
+constexpr int kLdsCopyThreads = 512;
 
 __device__ __forceinline__ const real* img_source(const ProblemArgsT<real>& a, int qp, int e) {
   const int N = a.N;
@@ -362,21 +369,26 @@ __device__ __forceinline__ const real* img_source(const ProblemArgsT<real>& a, i
 }
 
 template <bool SQRT>
-__global__ void __launch_bounds__(64, 1) riccati_unconstr_lds_kernel(ProblemArgsT<real> a) {
+__global__ void __launch_bounds__(kLdsCopyThreads, 1) riccati_unconstr_lds_kernel(ProblemArgsT<real> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   real* img = reinterpret_cast<real*>(lds_raw);
   const int qp = blockIdx.x;
   const int lane = threadIdx.x;
+  tstamp(16);
   const int total = (a.N + 1) * kImgStage;
-  for (int c0 = 0; c0 < total; c0 += 64 * kRealsPerDma) {
+  const int wave_off = (lane >> 6) * 64 * kRealsPerDma;  // this wave's 1 KiB of each round
+  for (int c0 = 0; c0 < total; c0 += kLdsCopyThreads * kRealsPerDma) {
     const int e = c0 + lane * kRealsPerDma;
     const real* g = e < total ? img_source(a, qp, e) : nullptr;
     if (g)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                       (__attribute__((address_space(3))) void*)(img + c0), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)(img + c0 + wave_off), 16,
+                                       0, 0);
   }
+  tstamp(14);  // (kernel entry is the first stamp of a launch: the copy into LDS ends here)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  tstamp(15);
   if (lane >= kGroup) return;
   solve_qp<SQRT>(a, LdsSrc{img}, qp, lane);
 }
@@ -659,7 +671,8 @@ static hipError_t launch_alg(const ProblemArgsT<real>& a, hipStream_t stream) {
     // (the > 64 KiB dynamic-LDS attribute is set on the handle's device by srbd_qp_create:
     // prepare_device below)
     const size_t bytes = lds_image_bytes(a.N);
-    hipLaunchKernelGGL(riccati_unconstr_lds_kernel<SQRT>, dim3((unsigned)a.batch), dim3(64), bytes, stream, a);
+    hipLaunchKernelGGL(riccati_unconstr_lds_kernel<SQRT>, dim3((unsigned)a.batch), dim3(kLdsCopyThreads), bytes,
+                       stream, a);
     return hipGetLastError();
   }
   const int threads = 256;
