@@ -97,17 +97,7 @@ __device__ __forceinline__ void store_rec(real* rec, int lane, const real (&Kc)[
   store_rec_P(rec, lane, P);
 }
 
-#ifndef SRBD_UNC_REC_HOT
-#define SRBD_UNC_REC_HOT 4
-#endif
-#ifndef SRBD_UNC_NT_IN
-#define SRBD_UNC_NT_IN 0
-#endif
-#ifndef SRBD_UNC_LDS_PAD
-#define SRBD_UNC_LDS_PAD 0
-#endif
-constexpr int kRecHotStages = SRBD_UNC_REC_HOT;
-constexpr bool kNtIn = SRBD_UNC_NT_IN != 0;
+constexpr int kRecHotStages = 4;
 
 // A stage record by plain stores, or (img set) through the wave's LDS image: the four
 // groups write their records into the image, then the wave stores the four records, which
@@ -243,16 +233,6 @@ __device__ __forceinline__ void fwd_sweep(const ProblemArgsT<real>& a, const Src
 // ---- the solve of one QP by its 16-lane group, blocks and records through `src` ----
 // SQRT: ric_alg = 1, the square-root recursion (riccati.h riccati_step_sqrt); the records
 // and outputs are the same (P_k = F - Y'Y of the stage, which Lx factors).
-// stage blocks: HBM sources may stream them past the caches (kNtIn), LDS images not
-template <class Src>
-__device__ __forceinline__ void ld12(const real* p, real (&v)[12]) {
-  if constexpr (std::is_same_v<Src, HbmSrc> && kNtIn) {
-    load12_nt(p, v);
-  } else {
-    load12(p, v);
-  }
-}
-
 template <bool SQRT, class Src>
 __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src& src, const int qp,
                                          const int lane) {
@@ -265,9 +245,9 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
   // ---------------- terminal stage: P_N = Q_N, p_N = q_N ----------------
   real P[12];
   if (isv) {
-    ld12<Src>(src.q(N), P);
+    load12(src.q(N), P);
   } else {
-    ld12<Src>(src.Q(N) + col * 12, P);
+    load12(src.Q(N) + col * 12, P);
   }
   store_rec_P(src.rec(N), lane, P);
   store_riccati_out(a, qp, N, lane, P, P);
@@ -279,26 +259,26 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
   for (int k = N - 1; k >= 0; --k) {
     // A, B (VL: b) of stage k, column-owned
     if (isv) {
-      ld12<Src>(src.b(k), A_);
+      load12(src.b(k), A_);
       sfor<0, 12>([&](auto i) { B_[decltype(i)::value] = real(0.0); });
     } else {
-      ld12<Src>(src.A(k) + col * 12, A_);
-      ld12<Src>(src.B(k) + col * 12, B_);
+      load12(src.A(k) + col * 12, A_);
+      load12(src.B(k) + col * 12, B_);
     }
     auto loadR = [&](real (&Rc)[12]) {
       if (isv) {
         sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = real(0.0); });
       } else {
-        ld12<Src>(src.R(k) + col * 12, Rc);
+        load12(src.R(k) + col * 12, Rc);
       }
     };
     auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
       if (isv) {
-        ld12<Src>(src.r(k), Sc);
-        ld12<Src>(src.q(k), Qc);
+        load12(src.r(k), Sc);
+        load12(src.q(k), Qc);
       } else {
-        ld12<Src>(src.S(k) + col * 12, Sc);
-        ld12<Src>(src.Q(k) + col * 12, Qc);
+        load12(src.S(k) + col * 12, Sc);
+        load12(src.Q(k) + col * 12, Qc);
       }
     };
     StageFactor<real> f;
@@ -678,7 +658,7 @@ static hipError_t launch_alg(const ProblemArgsT<real>& a, hipStream_t stream) {
   const int threads = 256;
   const long long lanes = (long long)a.batch * kGroup;
   const int blocks = (int)((lanes + threads - 1) / threads);
-  hipLaunchKernelGGL(riccati_unconstr_kernel<SQRT>, dim3(blocks), dim3(threads), SRBD_UNC_LDS_PAD, stream, a);
+  hipLaunchKernelGGL(riccati_unconstr_kernel<SQRT>, dim3(blocks), dim3(threads), 0, stream, a);
   return hipGetLastError();
 }
 
