@@ -9,18 +9,18 @@
 namespace srbd {
 
 // Forward-pass record of one stage, written by the backward sweep and read
-// back (row-owned) by the forward sweep.  [K | k] and [Acl | bcl] are 12 rows of
-// 13: row i = (K[i][0..11], k[i]), so the backward sweep's column owners (lane j)
-// and its vector lane (k, bcl: "column 12") store element (i, j) at one common
-// stride per row i, and lane i of the forward pass loads row i and its affine term
-// as 13 contiguous values.  The symmetric P is packed (lower triangle by columns,
-// 78 values: qp_group.h packed_col), followed by p.
-constexpr int kWsRow = 13;   // [K | k] / [Acl | bcl] row length
+// back (row-owned) by the forward sweep.  [K | k] is 12 rows of 13: row i =
+// (K[i][0..11], k[i]), so the backward sweep's column owners (lane j) and its
+// vector lane (k: "column 12") store element (i, j) at one common stride per
+// row i, and lane i of the forward pass loads row i and its affine term as 13
+// contiguous values.  The symmetric P is packed (lower triangle by columns, 78
+// values: qp_group.h packed_col), followed by p.  The forward sweep takes
+// x+ = A x + B u + b from the QP data itself (no closed-loop Acl in the record).
+constexpr int kWsRow = 13;   // [K | k] row length
 constexpr int kWsK = 0;      // [K | k]     [12][13]
-constexpr int kWsAcl = 156;  // [Acl | bcl] [12][13]
-constexpr int kWsP = 312;    // P   packed lower triangle, 78
-constexpr int kWsp = 390;    // p   [12]
-constexpr int kWsStage = 402;  // doubles per stage record (16-byte multiple)
+constexpr int kWsP = 156;    // P   packed lower triangle, 78
+constexpr int kWsp = 234;    // p   [12]
+constexpr int kWsStage = 246;  // doubles per stage record (16-byte multiple)
 
 // Arguments of every launch; T = double (srbd_qp_solve_f64) or float
 // (srbd_qp_solve_f32).  Workspace offsets below count elements of T.

@@ -220,7 +220,8 @@ __device__ __forceinline__ void symmetrize_lower(T (&M)[12], const int lane) {
 // then solve systems that differ far above the factorization's own error, which stalled
 // degenerate endgames.  (The square-root step needs no such step: its
 // Hessian terms are sums of squares, symmetric by construction.)
-template <int MidAt, bool SYMP, typename T, typename Mid>
+// ACL = false (the unconstrained solve, whose forward sweep uses A, B, b themselves): no Acl.
+template <int MidAt, bool SYMP, bool ACL, typename T, typename Mid>
 __device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], const int lane, StageFactor<T>& o,
                                              Mid&& mid) {
   if constexpr (MidAt == 1) {
@@ -248,9 +249,11 @@ __device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], const int
   SRBD_PHASE_FENCE();
   tstamp(9);
   // ---- Acl = A + B K (VL: bcl = b + B k)
-  launder(B_);
-  sym_mul_col(B_, o.Kc, A_);  // A[i][l] += B[i][m] K[m][l]: bc<m>(B_[i]) * Kc[m]
-  SRBD_PHASE_FENCE();
+  if constexpr (ACL) {
+    launder(B_);
+    sym_mul_col(B_, o.Kc, A_);  // A[i][l] += B[i][m] K[m][l]: bc<m>(B_[i]) * Kc[m]
+    SRBD_PHASE_FENCE();
+  }
   tstamp(10);
   if constexpr (SYMP) {
     SRBD_PHASE_FENCE();
@@ -265,8 +268,8 @@ __device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], const int
 // `mid` runs between the products and the triangular solves (MidAt = 1: P is
 // dead there) or after the solves (MidAt = 2: L is dead too): the caller may
 // issue the next stage's loads into registers of its own.
-template <int MidAt = 1, bool SYMP = false, typename TGin = void, typename T, typename LoadR,
-          typename LoadSQ, typename Mid = NoMid>
+template <int MidAt = 1, bool SYMP = false, typename TGin = void, bool ACL = true, typename T,
+          typename LoadR, typename LoadSQ, typename Mid = NoMid>
 __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&B_)[12],
                                              LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
                                              const T reg, StageFactor<T>& o, Mid&& mid = Mid{}) {
@@ -314,7 +317,7 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
   }
   SRBD_PHASE_FENCE();
   tstamp(6);
-  riccati_tail<MidAt, SYMP>(A_, B_, lane, o, mid);
+  riccati_tail<MidAt, SYMP, ACL>(A_, B_, lane, o, mid);
 }
 
 // Square-root step (ric_alg = 1).  `Lp` holds the factor of P_{k+1} (lane l: column l,
@@ -323,8 +326,8 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
 //   G = R + MB'MB,  H = S + MB'MA,  F = Q + MA'MA,  g = r + MB'm,  f = q + MA'm
 // -- in exact arithmetic the classical B'PB, B'PA, A'PA, B'(Pb + p), A'(Pb + p) --
 // then the common tail.  The caller continues the recursion with sqrt_factor(P_k).
-template <int MidAt = 1, bool SYMP = false, typename TGin = void, typename T, typename LoadR,
-          typename LoadSQ, typename Mid = NoMid>
+template <int MidAt = 1, bool SYMP = false, typename TGin = void, bool ACL = true, typename T,
+          typename LoadR, typename LoadSQ, typename Mid = NoMid>
 __device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12], T (&B_)[12],
                                                   LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
                                                   const T reg, StageFactor<T>& o,
@@ -359,7 +362,7 @@ __device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12]
     tmul_acc(MA, MA, o.F);
   }
   SRBD_PHASE_FENCE();
-  riccati_tail<MidAt, SYMP>(A_, B_, lane, o, mid);
+  riccati_tail<MidAt, SYMP, ACL>(A_, B_, lane, o, mid);
 }
 
 // P (lane l: column l of P_k; VL: p_k) -> its square-root form for the next

@@ -55,11 +55,12 @@ struct HbmSrc {
 };
 
 // LDS image of one QP: stage slot k (k = 0..N) holds the stage's blocks at the offsets
-// below (slot N: Q and q only); after the backward sweep has used slot k's blocks, the
-// stage's forward record (kernels.h kWs*, 402 reals) is written over them.
+// below (slot N: Q and q only); after the backward sweep has used slot k's Q, S, R, the
+// stage's forward record (kernels.h kWs*, 246 reals) is written over them (A, B, b stay
+// for the forward sweep's x+ = A x + B u + b).
 constexpr int kImgA = 0, kImgB = 144, kImgb = 288, kImgQ = 300, kImgS = 444, kImgR = 588,
-              kImgq = 732, kImgr = 744, kImgStage = 756;
-static_assert(kWsStage <= kImgStage, "a record fits its stage slot");
+              kImgq = 732, kImgr = 744, kImgStage = 756, kImgRec = kImgQ;
+static_assert(kImgRec + kWsStage <= kImgStage, "a record fits its stage slot past A, B, b");
 
 struct LdsSrc {
   real* img;
@@ -72,32 +73,33 @@ struct LdsSrc {
   __device__ const real* R(int k) const { return slot(k) + kImgR; }
   __device__ const real* q(int k) const { return slot(k) + kImgq; }
   __device__ const real* r(int k) const { return slot(k) + kImgr; }
-  __device__ real* rec(int k) const { return slot(k); }
+  __device__ real* rec(int k) const { return slot(k) + kImgRec; }
 };
 
 // ---- stage records ----
 // The terminal record (P_N, p_N) and, in solve_qp, every stage record by plain stores:
-// column owner j stores K[i][j] / Acl[i][j] at row i's slot j, the vector lane k[i] /
-// bcl[i] at slot 12 (kernels.h kWs*); P by packed columns (rows >= j), p on the vector lane.
+// column owner j stores K[i][j] at row i's slot j, the vector lane k[i] at slot 12
+// (kernels.h kWs*); P by packed columns (rows >= j), p on the vector lane.
 __device__ __forceinline__ void store_rec_P(real* rec, int lane, const real (&P)[12]) {
   if (lane < kMaxDim) store_packed_col(rec + kWsP, lane, P);
   if (lane == kVecLane) store12(rec + kWsp, P);
 }
-__device__ __forceinline__ void store_rec(real* rec, int lane, const real (&Kc)[12], const real (&Ac)[12],
-                                          const real (&P)[12]) {
+__device__ __forceinline__ void store_rec(real* rec, int lane, const real (&Kc)[12], const real (&P)[12]) {
   const bool isv = lane == kVecLane;
   if (lane < kMaxDim || isv) {
     const int c = isv ? kMaxDim : lane;
     sfor<0, 12>([&](auto m) {
       constexpr int M = decltype(m)::value;
       rec[kWsK + M * kWsRow + c] = Kc[M];
-      rec[kWsAcl + M * kWsRow + c] = Ac[M];
     });
   }
   store_rec_P(rec, lane, P);
 }
 
-constexpr int kRecHotStages = 4;
+#ifndef SRBD_UNC_REC_HOT
+#define SRBD_UNC_REC_HOT 4
+#endif
+constexpr int kRecHotStages = SRBD_UNC_REC_HOT;
 
 // A stage record by plain stores, or (img set) through the wave's LDS image: the four
 // groups write their records into the image, then the wave stores the four records, which
@@ -147,7 +149,9 @@ __device__ __forceinline__ void store_riccati_out(const ProblemArgsT<real>& a, i
 }
 
 // ---- forward sweep (row-owned), shared by every unconstrained kernel ----
-// u = K x + k, pi = P x + p, x+ = Acl x + bcl.  The record rows of stage k+1 are loaded
+// u = K x + k, pi = P x + p, x+ = A x + B u + b (A, B, b row-owned from the QP data: the
+// closed-loop Acl = A + B K is not formed in the backward sweep, which saves it 12 FMA blocks
+// per stage and the record 156 reals).  The record and data rows of stage k+1 are loaded
 // while stage k computes (the loads do not depend on x), so each stage pays one memory
 // latency less.
 template <class Src>
@@ -170,19 +174,25 @@ __device__ __forceinline__ void fwd_sweep(const ProblemArgsT<real>& a, const Src
     p_ = rec[kWsp + row];
     if (k < N) {
       const real* kr = rec + kWsK + row * kWsRow;
-      const real* ar = rec + kWsAcl + row * kWsRow;
+      const real* Ab = src.A(k);
       sfor<0, 12>([&](auto j) {
         constexpr int J = decltype(j)::value;
         K_[J] = kr[J];
-        A__[J] = ar[J];
+        A__[J] = Ab[J * 12 + row];  // column-major block: row `row` at stride 12
       });
       k_ = kr[12];
-      b_ = ar[12];
+      b_ = src.b(k)[row];
     }
   };
   load_rows(0, Pr, Kr, Ar, pv, kv, bv);
 #pragma unroll 1
   for (int k = 0; k <= N; ++k) {
+    // this stage's B row (used last: its load overlaps P x, K x, A x), then stage k+1's rows
+    real Br[12];
+    if (k < N) {
+      const real* Bb = src.B(k);
+      sfor<0, 12>([&](auto j) { Br[decltype(j)::value] = Bb[decltype(j)::value * 12 + row]; });
+    }
     real Pn[12], Kn[12], An[12], pvn = real(0.0), kvn = real(0.0), bvn = real(0.0);
     if (k < N) load_rows(k + 1, Pn, Kn, An, pvn, kvn, bvn);
     real bx[12];
@@ -207,6 +217,7 @@ __device__ __forceinline__ void fwd_sweep(const ProblemArgsT<real>& a, const Src
       xn = fmadd(Ar[J], bx[J], xn);
     });
     if (own) uo[(size_t)k * nu + lane] = uu;
+    xn = dot_bcast(Br, uu, xn);  // + B u (u element-owned, broadcast inside the FMAs)
     bad |= own && (!(uu == uu) || !(xn == xn));
     xv = xn;
     sfor<0, 12>([&](auto j) {
@@ -284,14 +295,14 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
     StageFactor<real> f;
     tstamp(0);
     if constexpr (SQRT) {
-      riccati_step_sqrt(P, A_, B_, loadR, loadSQ, lane, reg, f);
+      riccati_step_sqrt<1, false, void, false>(P, A_, B_, loadR, loadSQ, lane, reg, f);
     } else {
-      riccati_step(P, A_, B_, loadR, loadSQ, lane, reg, f);
+      riccati_step<1, false, void, false>(P, A_, B_, loadR, loadSQ, lane, reg, f);
     }
     if constexpr (std::is_same_v<Src, HbmSrc>) {
-      src.store_stage(k, [&](real* r) { store_rec(r, lane, f.Kc, A_, f.F); });
+      src.store_stage(k, [&](real* r) { store_rec(r, lane, f.Kc, f.F); });
     } else {
-      store_rec(src.rec(k), lane, f.Kc, A_, f.F);
+      store_rec(src.rec(k), lane, f.Kc, f.F);
     }
     tstamp(11);
     store_riccati_out(a, qp, k, lane, f.F, f.Kc);
