@@ -1570,6 +1570,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 template <int GEN>
 constexpr int kIpmMinBlocks = sizeof(real) == 4 && GEN < 2 ? 3 : 2;
 
+// the host verdict word of an RB sweep: the solve's tag (16 bits) and its live-workgroup count
+__host__ __device__ constexpr int ctl_word(int tag, int live) {
+  return ((tag & 0x7fff) << 16) | (live < 0xffff ? live : 0xffff);
+}
+
 // Live-QP report after an RB sweep (ProblemArgsT::ctl): one count per workgroup with a QP
 // still running, and the workgroup that finishes last hands the verdict to the host.  Every
 // thread of the workgroup reaches this (the phase functions return, the kernels do not).
@@ -1586,8 +1591,8 @@ __device__ __forceinline__ void report_running(const ProblemArgsT<real>& a) {
     __threadfence();
     if (atomicAdd(cnt + 1, 1) == (int)gridDim.x - 1) {
       __threadfence();
-      const int live = atomicAdd(cnt, 0);
-      __hip_atomic_store(a.ctl_host + a.launch_it, (a.ctl_tag << 1) | (live > 0 ? 1 : 0), __ATOMIC_RELAXED,
+      const int live = atomicAdd(cnt, 0);  // workgroups with a QP still running
+      __hip_atomic_store(a.ctl_host + a.launch_it, ctl_word(a.ctl_tag, live), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
@@ -1636,6 +1641,7 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
   // of RB(it - 1) and stops launching once it says every QP has exited, so a solve costs
   // the launches of the iterations its slowest QP takes (+ one), not 2 iter_max + 3.
   const bool ctl = a.ctl && a.ctl_host && a.ctl_ev[0] && a.ctl_ev[1] && a.iter_max < a.ctl_cap;
+
   ProblemArgsT<real> b = a;
   if (!ctl) b.ctl = nullptr;
   b.launch_it = 0;
@@ -1669,7 +1675,9 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
       hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(a.ctl_ev[(it - 1) & 1]));
       if (e != hipSuccess) return e;
       const int v = __atomic_load_n(a.ctl_host + (it - 1), __ATOMIC_ACQUIRE);
-      if (v == (a.ctl_tag << 1)) break;  // this solve's RB(it - 1): no QP left running
+      if ((v >> 16) == (a.ctl_tag & 0x7fff)) {  // this solve's RB(it - 1)
+        if ((v & 0xffff) == 0) break;  // no QP left running
+      }
     }
   }
   hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut, SQRT>), grid, block, 0, stream, b);

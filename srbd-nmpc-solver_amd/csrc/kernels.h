@@ -56,8 +56,9 @@ struct ProblemArgsT {
   // Live-QP control of the host-driven IPM loop (the handle's; ctl NULL = off).  After the
   // RB sweep of launch iteration it, ctl[2 it] counts the workgroups with a QP still
   // running and ctl[2 it + 1] the workgroups done; the last one writes ctl_host[it] =
-  // (ctl_tag << 1) | any-running into pinned host memory.  The host waits on ctl_ev (one
-  // iteration behind the launches) and stops launching once every QP has exited.
+  // (tag, number of workgroups with a live QP) into pinned host memory (ipm_box_impl.h
+  // ctl_word).  The host waits on ctl_ev (one iteration behind the launches) and stops
+  // launching once every QP has exited.
   int* ctl;
   int* ctl_host;
   int ctl_tag, ctl_cap;  // ctl_cap: iterations the arrays hold

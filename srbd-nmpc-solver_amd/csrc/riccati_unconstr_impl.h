@@ -96,10 +96,7 @@ __device__ __forceinline__ void store_rec(real* rec, int lane, const real (&Kc)[
   store_rec_P(rec, lane, P);
 }
 
-#ifndef SRBD_UNC_REC_HOT
-#define SRBD_UNC_REC_HOT 4
-#endif
-constexpr int kRecHotStages = SRBD_UNC_REC_HOT;
+constexpr int kRecHotStages = 4;
 
 // A stage record by plain stores, or (img set) through the wave's LDS image: the four
 // groups write their records into the image, then the wave stores the four records, which
