@@ -436,12 +436,19 @@ __device__ __forceinline__ void gather12(real v, real (&out)[12]) {
 // same 78 reals) and every sweep applies P as Lp (Lp' v): the solves use exactly the P the
 // next stage's factorization used (ric_alg 0 gets the same consistency by symmetrizing its
 // register P_k, riccati.h SYMP).
+// QP of this thread's group: the grid position, or (ProblemArgsT::qp_list) the position's
+// entry of the active-QP list; -1 past the batch / the list
+__device__ __forceinline__ int group_qp(const ProblemArgsT<real>& a) {
+  const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4);
+  if (a.qp_list) return g < a.qp_list[a.batch] ? a.qp_list[g] : -1;
+  return g < a.batch ? g : -1;
+}
+
 template <bool FULL, int GEN, int PH, bool SQRT = false>
 __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int qp = gid >> 4;
+  const int qp = group_qp(a);
   const int lane = threadIdx.x & (kGroup - 1);
-  if (qp >= a.batch) return;
+  if (qp < 0) return;
   const int N = a.N;
   const int nx = FULL ? 12 : a.nx;
   const int nu = FULL ? 12 : a.nu;
@@ -1296,7 +1303,93 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   }
   const real mu = qs[kQsMu], musum_all = qs[kQsMuSum];
   real sigma_mu = qs[kQsSigmaMu];
-  if constexpr (PH == kPhB2) {
+#ifndef SRBD_IPM_B2_DELTA
+#define SRBD_IPM_B2_DELTA 0
+#endif
+  if constexpr (PH == kPhB2 && GEN < 2 && (SRBD_IPM_B2_DELTA == 1 || (SRBD_IPM_B2_DELTA == 2 && sizeof(real) == 8))) {
+        // ---- B2 (boxes, C-free rows): the corrector's vectors as the predictor's plus the
+        // solve of the change of right-hand side.  The factorization is shared and every step
+        // of the vector recursion is linear in the right-hand side: gamma_corr - gamma_pred =
+        // (dlam_aff dt_aff - sigma mu) / t per active side (C-free rows: sigma mu D'e + D'z,
+        // stored by RB and F1), b~ is unchanged, so the change (dr, dq) runs through
+        //   dg = dr + B'dp_{k+1},  dp_k = dq + A'dp_{k+1} + K'dg,  dk = -L^-T L^-1 dg,  dbcl = B dk
+        // and k, bcl, p of the record (RB's predictor values) each get their change added.
+        // It reads neither P, the residuals, x, u, the multipliers nor the bound values.
+        // (Rows with C keep the direct recursion below: on a near-degenerate endgame with
+        // barrier Hessians of ~1e13 the sum drifted far enough to stop one QP at min step.)
+        auto dgam = [&](const Side& sd, const Bar& b, const BarStep& d) -> real {
+          real g = real(0.0);
+          if (sd.ml != real(0.0)) g += (d.dll * d.dtl - sigma_mu) / b.tl;
+          if (sd.mu != real(0.0)) g -= (d.dlu * d.dtu - sigma_mu) / b.tu;
+          return g;
+        };
+        real pnext = real(0.0);  // dp_{k+1}, element-owned
+        {
+          real* stN = c.st(N);
+          real dq = real(0.0);
+          if (lane < kMaxDim && xel) dq = dgam(c.side_x(N, lane), c.bar(stN, 1, lane), c.bstep(stN, 1, lane));
+          pnext = dq;
+          if (lane < kMaxDim) stN[par * kRecSize + kRecPv + lane] += dq;
+        }
+        for (int k = N - 1; k >= 0; --k) {
+          real* stk = c.st(k);
+          real* rec = stk + par * kRecSize;
+          real dr = real(0.0), dq = real(0.0);
+          if (lane < kMaxDim) {
+            if (uel) dr = dgam(c.side_u(k, lane), c.bar(stk, 0, lane), c.bstep(stk, 0, lane));
+            if (xel) dq = dgam(c.side_x(k, lane), c.bar(stk, 1, lane), c.bstep(stk, 1, lane));
+          }
+          if constexpr (GEN == 1) {
+            // D'gamma_corr - D'gamma_pred = sigma mu D'e + D'z (RB's D'e, F1's D'z)
+            if (lane < kMaxDim && uel) {
+              const real* v = c.gv(k);
+              dr += v[24 + lane] + sigma_mu * v[12 + lane];
+            }
+          }
+          // dg = dr + B'dp_{k+1} ; df = dq + A'dp_{k+1}
+          real Bc[12], Ac[12];
+          c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, Bc);
+          c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, Ac);
+          real g = dr, f = dq;
+          dot_bcast2(Bc, Ac, pnext, g, f);
+          if (lane >= kMaxDim) g = real(0.0);
+          // dp = df + K'dg  (K column-owned: lane j holds K[:, j])
+          real Kc[12];
+          load12(rec + kRecK + col * 12, Kc);
+          const real pv = dot_bcast(Kc, g, f);
+          // y = L^-1 dg (row-owned L), then z = L^-T y (column-owned L), dk = -z
+          real Lr[12], Lc[12];
+          load_packed_lrow(rec + kRecL, li, Lr);
+          load_packed_lcol(rec + kRecL, col, Lc);
+          const real rs = rec[kRecRs + li];
+          real y = g;
+          sfor<0, 12>([&](auto kk) {
+            constexpr int K = decltype(kk)::value;
+            const real yk = bc<K>(y * rs);
+            if (lane == K) y = yk;
+            if (lane > K) y = fmadd(-Lr[K], yk, y);
+          });
+          sfor_down<0, 12>([&](auto kk) {
+            constexpr int K = decltype(kk)::value;
+            const real zk = bc<K>(y * rs);
+            if (lane == K) y = zk;
+            if (lane < K) y = fmadd(-Lc[K], zk, y);
+          });
+          const real kv = lane < kMaxDim && uel ? -y : real(0.0);
+          // dbcl = B dk (row-owned B)
+          real Br[12];
+          c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
+          const real bcl = dot_bcast(Br, kv, real(0.0));
+          if (lane < kMaxDim) {
+            rec[kRecKv + lane] += kv;
+            rec[kRecBcl + lane] += xel ? bcl : real(0.0);
+            rec[kRecPv + lane] += xel ? pv : real(0.0);
+          }
+          pnext = xel ? pv : real(0.0);
+        }
+    return;
+  }
+  if constexpr (PH == kPhB2) {  // rows with C: the direct recursion
         // ---- B2: corrector vectors (element-owned recursion) ----
         real pnext = real(0.0);  // p_{k+1}, element-owned
         {
@@ -1580,9 +1673,9 @@ __host__ __device__ constexpr int ctl_word(int tag, int live) {
 // thread of the workgroup reaches this (the phase functions return, the kernels do not).
 __device__ __forceinline__ void report_running(const ProblemArgsT<real>& a) {
   if (!a.ctl) return;
-  const int qp = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4);
+  const int qp = group_qp(a);
   bool run = false;
-  if ((threadIdx.x & (kGroup - 1)) == 0 && qp < a.batch)  // the lane that wrote the status
+  if ((threadIdx.x & (kGroup - 1)) == 0 && qp >= 0)  // the lane that wrote the status
     run = a.ws[(size_t)qp * a.ws_qp + kQsStatus] < real(0.0);
   const int any = __syncthreads_or(run);
   if (threadIdx.x == 0) {
@@ -1622,6 +1715,22 @@ __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase2
   if constexpr (PH1 == kPhRB) report_running(a);
 }
 
+// The active-QP list: every QP whose status is still "running", in no particular order (a
+// QP's arithmetic does not depend on its place in the grid), the count at buf[batch].  One
+// atomic add per wave.  buf[batch] must be 0 on entry (zero_count_kernel).
+__global__ void __launch_bounds__(256) zero_count_kernel(int* buf, int batch) { buf[batch] = 0; }
+__global__ void __launch_bounds__(256) compact_running_kernel(const real* __restrict__ ws, size_t ws_qp,
+                                                              int batch, int* __restrict__ buf) {
+  const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const bool run = q < batch && ws[(size_t)q * ws_qp + kQsStatus] < real(0.0);
+  const unsigned long long m = __ballot(run);
+  const int lane = (int)(threadIdx.x & 63);
+  int base = 0;
+  if (lane == 0 && m) base = atomicAdd(buf + batch, __popcll(m));
+  base = __shfl(base, 0);
+  if (run) buf[base + __popcll(m & ((1ull << lane) - 1))] = q;
+}
+
 // diagnostic builds (-DSRBD_IPM_SPLIT=1, profiling only): every sweep its own launch
 #ifndef SRBD_IPM_SPLIT
 #define SRBD_IPM_SPLIT 0
@@ -1632,7 +1741,8 @@ template <bool FULL, int GEN, bool SQRT>
 static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream) {
   const int threads = 256;
   const long long lanes = (long long)a.batch * kGroup;
-  const dim3 grid((unsigned)((lanes + threads - 1) / threads)), block(threads);
+  const dim3 full_grid((unsigned)((lanes + threads - 1) / threads)), block(threads);
+  dim3 grid = full_grid;
   // Host-driven iteration: each sweep is its own launch, so every kernel gets
   // the registers (and occupancy) of its own phase; QPs that have exited return
   // at the top of every later launch.  iter_max + 1 factorization sweeps at
@@ -1645,7 +1755,15 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
   ProblemArgsT<real> b = a;
   if (!ctl) b.ctl = nullptr;
   b.launch_it = 0;
+  b.qp_list = nullptr;
   hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhInit>), grid, block, 0, stream, b);
+  // Active-QP compaction: once the verdict one iteration back says the workgroups with a live
+  // QP are at most 3/4 of the grid, the next sweeps run on a list of the running QPs (built
+  // after the last enqueued sweep, so it is exact for them; QPs exiting later return at the
+  // top as before) on a grid of (live workgroups of the verdict) x 16 QPs, an upper bound.
+  // A wave then carries four live QPs instead of the one or two a thinned-out batch leaves it.
+  const bool compact = ctl && a.qp_buf;
+  long long grid_wg = full_grid.x;
   // (SQRT changes RB and how B2, F1, F2 and the outputs apply the record's P)
   for (int it = 0;; ++it) {
     b.launch_it = it;
@@ -1676,11 +1794,23 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
       if (e != hipSuccess) return e;
       const int v = __atomic_load_n(a.ctl_host + (it - 1), __ATOMIC_ACQUIRE);
       if ((v >> 16) == (a.ctl_tag & 0x7fff)) {  // this solve's RB(it - 1)
-        if ((v & 0xffff) == 0) break;  // no QP left running
+        const long long live_wg = v & 0xffff;
+        if (live_wg == 0) break;  // no QP left running
+        if (compact && live_wg < 0xffff && 4 * live_wg <= 3 * grid_wg) {
+          long long qps = live_wg * 16;
+          if (qps > a.batch) qps = a.batch;
+          hipLaunchKernelGGL(zero_count_kernel, dim3(1), dim3(1), 0, stream, a.qp_buf, a.batch);
+          hipLaunchKernelGGL(compact_running_kernel, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, stream,
+                             a.ws, a.ws_qp, a.batch, a.qp_buf);
+          b.qp_list = a.qp_buf;
+          grid_wg = (qps * kGroup + threads - 1) / threads;
+          grid = dim3((unsigned)grid_wg);
+        }
       }
     }
   }
-  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut, SQRT>), grid, block, 0, stream, b);
+  b.qp_list = nullptr;  // outputs for every QP
+  hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut, SQRT>), full_grid, block, 0, stream, b);
   return hipGetLastError();
 }
 

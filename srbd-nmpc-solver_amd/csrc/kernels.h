@@ -64,6 +64,10 @@ struct ProblemArgsT {
   int ctl_tag, ctl_cap;  // ctl_cap: iterations the arrays hold
   int launch_it;         // set per launch
   void* ctl_ev[2];       // hipEvent_t (host side only)
+  // Active-QP list of the IPM sweeps (the handle's; capacity + 1 ints, the count last).
+  // qp_list set for a launch: QP group g of the grid works on QP qp_list[g] if g < count.
+  int* qp_buf;
+  const int* qp_list;
 };
 // iterations of the live-QP control arrays (iter_max >= this runs without the control)
 constexpr int kCtlCap = 257;

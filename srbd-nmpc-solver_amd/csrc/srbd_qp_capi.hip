@@ -71,6 +71,7 @@ struct srbd_qp_handle_s {
   int* ctl_host = nullptr;
   hipEvent_t ctl_ev[2] = {nullptr, nullptr};
   int ctl_tag = 0;
+  int* qp_buf = nullptr;  // active-QP list of the IPM sweeps: capacity + 1 ints
 };
 
 extern "C" {
@@ -192,6 +193,7 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srb
     e = hipMalloc(reinterpret_cast<void**>(&h->ctl), sizeof(int) * 2 * srbd::kCtlCap);
     if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&h->ctl_host), sizeof(int) * srbd::kCtlCap);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&h->ctl_ev[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&h->qp_buf), sizeof(int) * ((size_t)batch_capacity + 1));
   }
   hipSetDevice(prev);
   if (e != hipSuccess) {
@@ -221,6 +223,7 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   if (h->mixed) hipFree(h->mixed);
   if (h->resc_count_host) hipHostFree(h->resc_count_host);
   if (h->ctl) hipFree(h->ctl);
+  if (h->qp_buf) hipFree(h->qp_buf);
   if (h->ctl_host) hipHostFree(h->ctl_host);
   for (hipEvent_t ev : h->ctl_ev)
     if (ev) hipEventDestroy(ev);
@@ -237,6 +240,7 @@ size_t srbd_qp_memory_bytes(srbd_qp_handle h) {
   if (!h) return 0;
   return h->ws_bytes + h->stage_bytes + h->pinned_bytes + h->pad_bytes + h->nmpc_bytes +
          (h->ctl ? sizeof(int) * 3 * srbd::kCtlCap : 0) +
+         (h->qp_buf ? sizeof(int) * ((size_t)h->capacity + 1) : 0) +
          h->resc_bytes + h->resc2_bytes + h->mixed_bytes +
          (h->resc_idx ? sizeof(int) * (2 * (size_t)h->capacity + 1) : 0);
 }
@@ -358,6 +362,7 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
     a.ctl_tag = h->ctl_tag = (h->ctl_tag + 1) & 0x3fffffff;
     a.ctl_ev[0] = h->ctl_ev[0];
     a.ctl_ev[1] = h->ctl_ev[1];
+    a.qp_buf = h->qp_buf;
   }
   hipError_t e = hipSuccess;
   // (unconstrained with residuals: unconstr_residuals_kernel clears and fills the table)
