@@ -811,8 +811,10 @@ def roofline(constraints, achieved_gbs, traffic, kernel_ms, bytes_qp, flops_qp, 
     iterations taken / kernel time, against the same 8 TB/s peak (no MFMA is used:
     the 12 x 12 blocks run on the FP vector pipe)."""
     if constraints == "none":
+        prof, prof_ns = pmc_profile("unconstr_n20" if batch == 65536 else "", batch)
         return {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_profile": prof, "profile_kernel_avg_ms": None if prof_ns is None else prof_ns * 1e-6,
                 # template argument = square-root Riccati (ric_alg; NMPC_solver.cpp:81 sets 0)
                 "kernel": "riccati_unconstr_kernel<%s>" % ("true" if NMPC_SETTINGS["ric_alg"] else "false"),
                 "kernel_avg_ms": kernel_ms,
@@ -869,6 +871,18 @@ def cpu_baseline(pkg, qp, x0, settings, budget_s):
 
 def _has_bounds(qp):
     return any(getattr(qp, k) is not None for k in ("lbu", "ubu", "lbx", "ubx"))
+
+
+def pmc_profile(workload, batch):
+    """(profile summary file, its kernel's average ns) behind pmc_traffic, if any."""
+    f = REPO / "profiles" / "pmc_traffic.json"
+    try:
+        e = json.loads(f.read_text()).get(workload)
+        if e and int(e.get("batch", -1)) == batch:
+            return e.get("profile"), e.get("avg_ns")
+    except Exception:
+        pass
+    return None, None
 
 
 def pmc_traffic(workload, batch):

@@ -61,7 +61,8 @@ tot_ns = sum(e.get("total_ns", 0.0) for e in per.values())
 tot_b = sum(e.get("hbm_bytes_per_launch", 0.0) * e.get("calls", 0) for e in per.values())
 kname = stats[0]["Name"] if stats else None
 dom = per.get(kname, {})
-summary = {"workload": workload, "batch": batch, "kernel": kname, "avg_ns": dom.get("avg_ns"),
+summary = {"workload": workload, "batch": batch, "profile": f"profiles/{tag}/{workload}_summary.json",
+           "kernel": kname, "avg_ns": dom.get("avg_ns"),
            "launches_traced": len(trace),
            "fetch_bytes_per_launch": dom.get("fetch_size_bytes_per_launch"),
            "write_bytes_per_launch": dom.get("write_size_bytes_per_launch"),
