@@ -1303,93 +1303,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   }
   const real mu = qs[kQsMu], musum_all = qs[kQsMuSum];
   real sigma_mu = qs[kQsSigmaMu];
-#ifndef SRBD_IPM_B2_DELTA
-#define SRBD_IPM_B2_DELTA 0
-#endif
-  if constexpr (PH == kPhB2 && GEN < 2 && (SRBD_IPM_B2_DELTA == 1 || (SRBD_IPM_B2_DELTA == 2 && sizeof(real) == 8))) {
-        // ---- B2 (boxes, C-free rows): the corrector's vectors as the predictor's plus the
-        // solve of the change of right-hand side.  The factorization is shared and every step
-        // of the vector recursion is linear in the right-hand side: gamma_corr - gamma_pred =
-        // (dlam_aff dt_aff - sigma mu) / t per active side (C-free rows: sigma mu D'e + D'z,
-        // stored by RB and F1), b~ is unchanged, so the change (dr, dq) runs through
-        //   dg = dr + B'dp_{k+1},  dp_k = dq + A'dp_{k+1} + K'dg,  dk = -L^-T L^-1 dg,  dbcl = B dk
-        // and k, bcl, p of the record (RB's predictor values) each get their change added.
-        // It reads neither P, the residuals, x, u, the multipliers nor the bound values.
-        // (Rows with C keep the direct recursion below: on a near-degenerate endgame with
-        // barrier Hessians of ~1e13 the sum drifted far enough to stop one QP at min step.)
-        auto dgam = [&](const Side& sd, const Bar& b, const BarStep& d) -> real {
-          real g = real(0.0);
-          if (sd.ml != real(0.0)) g += (d.dll * d.dtl - sigma_mu) / b.tl;
-          if (sd.mu != real(0.0)) g -= (d.dlu * d.dtu - sigma_mu) / b.tu;
-          return g;
-        };
-        real pnext = real(0.0);  // dp_{k+1}, element-owned
-        {
-          real* stN = c.st(N);
-          real dq = real(0.0);
-          if (lane < kMaxDim && xel) dq = dgam(c.side_x(N, lane), c.bar(stN, 1, lane), c.bstep(stN, 1, lane));
-          pnext = dq;
-          if (lane < kMaxDim) stN[par * kRecSize + kRecPv + lane] += dq;
-        }
-        for (int k = N - 1; k >= 0; --k) {
-          real* stk = c.st(k);
-          real* rec = stk + par * kRecSize;
-          real dr = real(0.0), dq = real(0.0);
-          if (lane < kMaxDim) {
-            if (uel) dr = dgam(c.side_u(k, lane), c.bar(stk, 0, lane), c.bstep(stk, 0, lane));
-            if (xel) dq = dgam(c.side_x(k, lane), c.bar(stk, 1, lane), c.bstep(stk, 1, lane));
-          }
-          if constexpr (GEN == 1) {
-            // D'gamma_corr - D'gamma_pred = sigma mu D'e + D'z (RB's D'e, F1's D'z)
-            if (lane < kMaxDim && uel) {
-              const real* v = c.gv(k);
-              dr += v[24 + lane] + sigma_mu * v[12 + lane];
-            }
-          }
-          // dg = dr + B'dp_{k+1} ; df = dq + A'dp_{k+1}
-          real Bc[12], Ac[12];
-          c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, Bc);
-          c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, Ac);
-          real g = dr, f = dq;
-          dot_bcast2(Bc, Ac, pnext, g, f);
-          if (lane >= kMaxDim) g = real(0.0);
-          // dp = df + K'dg  (K column-owned: lane j holds K[:, j])
-          real Kc[12];
-          load12(rec + kRecK + col * 12, Kc);
-          const real pv = dot_bcast(Kc, g, f);
-          // y = L^-1 dg (row-owned L), then z = L^-T y (column-owned L), dk = -z
-          real Lr[12], Lc[12];
-          load_packed_lrow(rec + kRecL, li, Lr);
-          load_packed_lcol(rec + kRecL, col, Lc);
-          const real rs = rec[kRecRs + li];
-          real y = g;
-          sfor<0, 12>([&](auto kk) {
-            constexpr int K = decltype(kk)::value;
-            const real yk = bc<K>(y * rs);
-            if (lane == K) y = yk;
-            if (lane > K) y = fmadd(-Lr[K], yk, y);
-          });
-          sfor_down<0, 12>([&](auto kk) {
-            constexpr int K = decltype(kk)::value;
-            const real zk = bc<K>(y * rs);
-            if (lane == K) y = zk;
-            if (lane < K) y = fmadd(-Lc[K], zk, y);
-          });
-          const real kv = lane < kMaxDim && uel ? -y : real(0.0);
-          // dbcl = B dk (row-owned B)
-          real Br[12];
-          c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
-          const real bcl = dot_bcast(Br, kv, real(0.0));
-          if (lane < kMaxDim) {
-            rec[kRecKv + lane] += kv;
-            rec[kRecBcl + lane] += xel ? bcl : real(0.0);
-            rec[kRecPv + lane] += xel ? pv : real(0.0);
-          }
-          pnext = xel ? pv : real(0.0);
-        }
-    return;
-  }
-  if constexpr (PH == kPhB2) {  // rows with C: the direct recursion
+  if constexpr (PH == kPhB2) {
         // ---- B2: corrector vectors (element-owned recursion) ----
         real pnext = real(0.0);  // p_{k+1}, element-owned
         {
