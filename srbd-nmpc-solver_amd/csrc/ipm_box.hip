@@ -16,7 +16,7 @@
 //   RB  k = N..0  apply the previous step to stage k, its residuals res_g /
 //                 res_b / res_d / res_m (norms, mu, obj), Gamma / gamma, and the
 //                 barrier-augmented factorization (riccati_step) writing the
-//                 stage record {L, K, Acl, P, 1/diag L, k, bcl, p}.  Every QP
+//                 stage record {L, K, P, 1/diag L, k, p}.  Every QP
 //                 block is read from global memory once per iteration; the
 //                 row-owned residual products go through LDS.  After the sweep:
 //                 exit test (NaN, converged, iter_max, min step).
@@ -166,3 +166,19 @@ hipError_t launch_ipm_box<float>(const ProblemArgsT<float>& a, hipStream_t strea
 }
 
 }  // namespace srbd
+
+#if SRBD_TSTAMP
+// Diagnostic builds only: this translation unit's stamp buffer (the IPM kernels), as
+// srbd_qp_diag_tstamps does for the unconstrained ones.
+extern "C" int srbd_qp_diag_tstamps_ipm(unsigned long long* out, int cap) {
+  unsigned n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(srbd::g_tstamp_n), sizeof n) != hipSuccess) return -1;
+  if (n > (unsigned)srbd::kTstampCap) n = srbd::kTstampCap;
+  if ((int)n > cap) n = (unsigned)cap;
+  if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(srbd::g_tstamp), 2 * sizeof(unsigned long long) * n) != hipSuccess)
+    return -1;
+  const unsigned zero = 0;
+  hipMemcpyToSymbol(HIP_SYMBOL(srbd::g_tstamp_n), &zero, sizeof zero);
+  return (int)n;
+}
+#endif

@@ -927,6 +927,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     real xn = real(0.0), pin = real(0.0);  // updated x_{k+1}, pi_{k+1} (element-owned), from stage k+1
     real P[12];
     for (int k = N; k >= 0; --k) {
+      tstamp(20);
       real* stk = c.st(k);
       real* rec = stk + par * kRecSize;
       // ---- apply the previous step to stage k ----
@@ -1123,6 +1124,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         return rb_;
       };
       SRBD_PHASE_FENCE();
+      tstamp(21);
       if (k == N) {
         // terminal stage: P_N = Q_N + diag(Gamma_x) (+ C'Gamma C), p_N = q~_N
         c.col(c.Q() + (size_t)N * c.nxx(), nx, col, xel, P);
@@ -1214,6 +1216,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             }
           });
         };
+        tstamp(22);
         StageFactor<real> f;
         if constexpr (SQRT) {
           riccati_step_sqrt<1, false, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f);
@@ -1228,13 +1231,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         if (lane < kMaxDim) {
           store_packed_col(img + kRecL, lane, f.Lc);
           store12(img + kRecK + lane * 12, f.Kc);
-          store12(img + kRecAcl + lane * 12, A_);
           if constexpr (!SQRT) store_packed_col(img + kRecP, lane, f.F);
           img[kRecRs + lane] = f.rs;
         }
         if (c.isv) {
           store12(img + kRecKv, f.Kc);
-          store12(img + kRecBcl, A_);
           store12(img + kRecPv, f.F);
         }
         sfor<0, 12>([&](auto i) {
@@ -1249,6 +1250,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         if constexpr (kRecImg<GEN>) rec_copy(rec, img, lane);
         // the next stage overwrites this group's LDS blocks: reads done first
         lds_wave_fence();
+        tstamp(23);
       }
       xn = xk;
       pin = pik;
@@ -1325,6 +1327,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           if (lane < kMaxDim) stN[par * kRecSize + kRecPv + lane] = pnext;
         }
         for (int k = N - 1; k >= 0; --k) {
+          tstamp(40);
           real* stk = c.st(k);
           real* rec = stk + par * kRecSize;
           const real* recn = c.st(k + 1) + par * kRecSize;
@@ -1385,13 +1388,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             if (lane < K) y = fmadd(-Lc[K], zk, y);
           });
           const real kv = lane < kMaxDim && uel ? -y : real(0.0);
-          // bcl = b~ + B k (row-owned B)
-          real Br[12];
-          c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
-          const real bcl = dot_bcast(Br, kv, bt);
           if (lane < kMaxDim) {
             rec[kRecKv + lane] = kv;
-            rec[kRecBcl + lane] = xel ? bcl : real(0.0);
             rec[kRecPv + lane] = xel ? pv : real(0.0);
           }
           pnext = xel ? pv : real(0.0);
@@ -1409,17 +1407,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       ap = real(1e30);
       ad = real(1e30);
       real dxk = real(0.0);  // dx_0 = 0 (x0 fixed)
-      auto load_rows = [&](int k, real (&Kr)[12], real (&Ar)[12], real& kv, real& bv) {
-        const real* rk = c.st(k) + par * kRecSize;
-        sfor<0, 12>([&](auto j) {
-          constexpr int J = decltype(j)::value;
-          Kr[J] = rk[kRecK + J * 12 + li];
-          Ar[J] = rk[kRecAcl + J * 12 + li];
-        });
-        kv = rk[kRecKv + li];
-        bv = rk[kRecBcl + li];
-      };
       for (int k = 0; k <= N; ++k) {
+        tstamp(corr ? 31 : 30);
         real* stk = c.st(k);
         const real* rec = stk + par * kRecSize;
         // dpi = P dx + p is part of the final step only (F2, or F1 without corrector)
@@ -1427,9 +1416,21 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         if (corr || !a.pred_corr) dpi = rec_P_mul(rec, dxk, rec[kRecPv + li]);
         real du = real(0.0), dxn = real(0.0);
         if (k < N) {
+          // du = K dx + k, dx+ = A dx + B du + b~ (open loop: the QP's own A, B; b~ = res_b,
+          // unchanged between predictor and corrector)
           real Kr[12], Ar[12];
-          load_rows(k, Kr, Ar, du, dxn);
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            Kr[J] = rec[kRecK + J * 12 + li];
+          });
+          c.row(c.A() + (size_t)k * c.nxx(), nx, nx, li, xel, Ar);
+          du = rec[kRecKv + li];
+          dxn = stk[kStRes + 24 + li];
           dot_bcast2(Kr, Ar, dxk, du, dxn);
+          if (!uel) du = real(0.0);
+          real Br[12];
+          c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
+          dxn = dot_bcast(Br, du, dxn);
         }
         if (!uel || k == N) du = real(0.0);
         if (!xel) {

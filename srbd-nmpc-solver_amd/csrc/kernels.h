@@ -79,15 +79,15 @@ constexpr int kStatCols = 18;  // HPIPM ws->stat row width
 // records per stage (ping-pong by iteration parity: the iteration that exits
 // still reports the previous iteration's Riccati factors, like HPIPM's
 // getters), then the iterate's barrier state.
-constexpr int kRecL = 0;      // L packed lower triangle (78)
-constexpr int kRecK = 78;     // K [12][12], column j contiguous
-constexpr int kRecAcl = 222;  // Acl [12][12], column j contiguous
-constexpr int kRecP = 366;    // P packed lower triangle (78)
-constexpr int kRecRs = 444;   // 1 / diag(L)
-constexpr int kRecKv = 456;   // k
-constexpr int kRecBcl = 468;  // bcl
-constexpr int kRecPv = 480;   // p
-constexpr int kRecSize = 492;
+// The forward sweeps step x+ = A x + B u + b~ with the QP's own A, B (open loop), so the
+// record holds no closed-loop Acl = A + B K.
+constexpr int kRecL = 0;     // L packed lower triangle (78)
+constexpr int kRecK = 78;    // K [12][12], column j contiguous
+constexpr int kRecP = 222;   // P packed lower triangle (78)
+constexpr int kRecRs = 300;  // 1 / diag(L)
+constexpr int kRecKv = 312;  // k
+constexpr int kRecPv = 324;  // p
+constexpr int kRecSize = 336;
 constexpr int kStLam = 2 * kRecSize;  // 8 x 12: lam_l,u / lam_u,u / t_l,u / t_u,u / same for x
 constexpr int kStRes = kStLam + 96;   // 3 x 12: res_g,u / res_g,x / res_b
 constexpr int kStStep = kStRes + 36;  // 3 x 12: du / dx / dpi

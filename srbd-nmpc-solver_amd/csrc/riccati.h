@@ -7,7 +7,7 @@
 //   H  = S + B'W_A,  g = r + B'w,  F = Q + A'W_A,  f = q + A'w
 //   Y  = L^-1 H,  y = L^-1 g,  K = -L^-T Y,  k = -L^-T y
 //   P- = F - Y'Y,  p- = f - Y'y
-//   Acl = A + B K,  bcl = b + B k           (closed loop, for the forward pass)
+// (the forward passes step x+ = A x + B u + b with the QP's own blocks)
 // This is HPIPM's d_ocp_qp_fact_solve_kkt_unconstr (hpipm_d_ocp_qp_kkt.h:54)
 // i.e. the BLASFEO dgemm_nt / dsyrk_ln / dpotrf_l / dtrsv chain, re-blocked
 // for one-column-per-lane.  A non-positive pivot zeroes its direction like
@@ -211,7 +211,7 @@ __device__ __forceinline__ void symmetrize_lower(T (&M)[12], const int lane) {
 
 // The common tail of both step variants: given L = chol(G) and the column-owned
 // H (VL: g) and F (VL: f) of the stage,
-//   Y = L^-1 H, K = -L^-T Y, P_k = F - Y'Y (VL: p_k = f - Y'y), Acl = A + B K.
+//   Y = L^-1 H, K = -L^-T Y, P_k = F - Y'Y (VL: p_k = f - Y'y).
 // `mid` runs before the triangular solves (MidAt = 1) or after them (MidAt = 2).
 // SYMP: P_k is made exactly symmetric from its lower triangle before it continues the
 // recursion.  The column-wise products leave rounding-level asymmetry in F - Y'Y, while
@@ -220,10 +220,8 @@ __device__ __forceinline__ void symmetrize_lower(T (&M)[12], const int lane) {
 // then solve systems that differ far above the factorization's own error, which stalled
 // degenerate endgames.  (The square-root step needs no such step: its
 // Hessian terms are sums of squares, symmetric by construction.)
-// ACL = false (the unconstrained solve, whose forward sweep uses A, B, b themselves): no Acl.
-template <int MidAt, bool SYMP, bool ACL, typename T, typename Mid>
-__device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], const int lane, StageFactor<T>& o,
-                                             Mid&& mid) {
+template <int MidAt, bool SYMP, typename T, typename Mid>
+__device__ __forceinline__ void riccati_tail(const int lane, StageFactor<T>& o, Mid&& mid) {
   if constexpr (MidAt == 1) {
     mid();
     SRBD_PHASE_FENCE();
@@ -248,12 +246,6 @@ __device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], const int
   }
   SRBD_PHASE_FENCE();
   tstamp(9);
-  // ---- Acl = A + B K (VL: bcl = b + B k)
-  if constexpr (ACL) {
-    launder(B_);
-    sym_mul_col(B_, o.Kc, A_);  // A[i][l] += B[i][m] K[m][l]: bc<m>(B_[i]) * Kc[m]
-    SRBD_PHASE_FENCE();
-  }
   tstamp(10);
   if constexpr (SYMP) {
     SRBD_PHASE_FENCE();
@@ -262,14 +254,13 @@ __device__ __forceinline__ void riccati_tail(T (&A_)[12], T (&B_)[12], const int
 }
 
 // One backward Riccati step.  `P` holds P_{k+1} (VL: p_{k+1}) on entry.
-// A_ is overwritten with the closed-loop column Acl (VL: bcl) on exit.
 // The S/Q/R columns are fetched through the callables so that their loads
 // are issued late (short live ranges).
 // `mid` runs between the products and the triangular solves (MidAt = 1: P is
 // dead there) or after the solves (MidAt = 2: L is dead too): the caller may
 // issue the next stage's loads into registers of its own.
-template <int MidAt = 1, bool SYMP = false, typename TGin = void, bool ACL = true, typename T,
-          typename LoadR, typename LoadSQ, typename Mid = NoMid>
+template <int MidAt = 1, bool SYMP = false, typename TGin = void, typename T, typename LoadR,
+          typename LoadSQ, typename Mid = NoMid>
 __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&B_)[12],
                                              LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
                                              const T reg, StageFactor<T>& o, Mid&& mid = Mid{}) {
@@ -317,7 +308,7 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
   }
   SRBD_PHASE_FENCE();
   tstamp(6);
-  riccati_tail<MidAt, SYMP, ACL>(A_, B_, lane, o, mid);
+  riccati_tail<MidAt, SYMP>(lane, o, mid);
 }
 
 // Square-root step (ric_alg = 1).  `Lp` holds the factor of P_{k+1} (lane l: column l,
@@ -326,8 +317,8 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
 //   G = R + MB'MB,  H = S + MB'MA,  F = Q + MA'MA,  g = r + MB'm,  f = q + MA'm
 // -- in exact arithmetic the classical B'PB, B'PA, A'PA, B'(Pb + p), A'(Pb + p) --
 // then the common tail.  The caller continues the recursion with sqrt_factor(P_k).
-template <int MidAt = 1, bool SYMP = false, typename TGin = void, bool ACL = true, typename T,
-          typename LoadR, typename LoadSQ, typename Mid = NoMid>
+template <int MidAt = 1, bool SYMP = false, typename TGin = void, typename T, typename LoadR,
+          typename LoadSQ, typename Mid = NoMid>
 __device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12], T (&B_)[12],
                                                   LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
                                                   const T reg, StageFactor<T>& o,
@@ -362,7 +353,7 @@ __device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12]
     tmul_acc(MA, MA, o.F);
   }
   SRBD_PHASE_FENCE();
-  riccati_tail<MidAt, SYMP, ACL>(A_, B_, lane, o, mid);
+  riccati_tail<MidAt, SYMP>(lane, o, mid);
 }
 
 // P (lane l: column l of P_k; VL: p_k) -> its square-root form for the next

@@ -7,10 +7,10 @@
 //
 // One kernel, two sweeps per QP group (see qp_group.h):
 //   backward k = N-1..0 : riccati_step on the stage's column-owned blocks,
-//                         then write the forward record {K, Acl, P, k, bcl, p}
-//                         (row-major, kernels.h) to the per-QP workspace;
+//                         then write the forward record {K, P, k, p} to the
+//                         per-QP workspace;
 //   forward  k = 0..N   : row-owned u = K x + k, pi = P x + p,
-//                         x+ = Acl x + bcl, with x broadcast by DPP.
+//                         x+ = A x + B u + b, with x, u broadcast by DPP.
 // The forward sweep reads the records in LIFO order (stage 0 was written
 // last), so the most recent records are still in L2 / Infinity Cache.
 //

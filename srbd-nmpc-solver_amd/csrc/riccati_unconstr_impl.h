@@ -292,9 +292,9 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
     StageFactor<real> f;
     tstamp(0);
     if constexpr (SQRT) {
-      riccati_step_sqrt<1, false, void, false>(P, A_, B_, loadR, loadSQ, lane, reg, f);
+      riccati_step_sqrt<1, false>(P, A_, B_, loadR, loadSQ, lane, reg, f);
     } else {
-      riccati_step<1, false, void, false>(P, A_, B_, loadR, loadSQ, lane, reg, f);
+      riccati_step<1, false>(P, A_, B_, loadR, loadSQ, lane, reg, f);
     }
     if constexpr (std::is_same_v<Src, HbmSrc>) {
       src.store_stage(k, [&](real* r) { store_rec(r, lane, f.Kc, f.F); });
