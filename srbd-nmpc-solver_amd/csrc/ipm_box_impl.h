@@ -151,7 +151,7 @@ struct Ctx {
 
   __device__ size_t oq() const {
     int v = qp;
-    asm volatile("" : "+v"(v));
+    asm("" : "+v"(v));
     return (size_t)v;
   }
   __device__ size_t iq() const { return oq(); }  // input QP index
@@ -198,17 +198,22 @@ struct Ctx {
   // per-stage general-row vectors (kGenVec) after the chunks
   __device__ real* gv(int k) const { return st(k) + kIpmStage + nch * kGenChunk; }
   // row i of chunk ch (element-owned): lg <= v <= ug
+  // (The side loaders read a valid address on every lane and mask the result with selects:
+  // a load under a branch is waited for inside that branch, one memory round trip each.
+  // The optional mask arrays are chosen by their wave-uniform base pointers.)
+  __device__ static Side side_at(const real* lb, const real* ub, const real* lm, const real* um, size_t o,
+                                 bool ok) {
+    const real l = lb[o], u = ub[o];
+    const real ml = (lm ? lm : lb)[o], mu = (um ? um : ub)[o];
+    const bool al = (ml != real(0.0)) | (lm == nullptr), au = (mu != real(0.0)) | (um == nullptr);
+    return Side{ok ? l : real(0.0), ok ? u : real(0.0), ok && al ? real(1.0) : real(0.0),
+                ok && au ? real(1.0) : real(0.0)};
+  }
   __device__ Side side_g(int k, int ch, int i) const {
-    Side s{real(0.0), real(0.0), real(0.0), real(0.0)};
     const int r = ch * kMaxDim + i;
-    if (i < kMaxDim && r < ng) {
-      const size_t o = (size_t)k * ng + r;
-      s.lb = lg()[o];
-      s.ub = ug()[o];
-      s.ml = lgm() ? (lgm()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
-      s.mu = ugm() ? (ugm()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
-    }
-    return s;
+    const bool ok = i < kMaxDim && r < ng;
+    const size_t o = (sN1() + k) * ng + (ok ? r : 0);
+    return side_at(blg, bug, blgm, bugm, o, ok);
   }
   // row-owned C / D rows of chunk ch (lane i = row); C_0 dropped like the
   // reference's x0 embedding (nx[0] = 0), D_N absent
@@ -299,26 +304,16 @@ struct Ctx {
     if (has_bars(which)) store_bstep(stk, which, i, d);
   }
   __device__ Side side_u(int k, int i) const {
-    Side s{real(0.0), real(0.0), real(0.0), real(0.0)};
-    if (blbu && i < nu && k < N) {
-      const size_t o = (size_t)k * nu + i;
-      s.lb = lbu()[o];
-      s.ub = ubu()[o];
-      s.ml = lbum() ? (lbum()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
-      s.mu = ubum() ? (ubum()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
-    }
-    return s;
+    if (!blbu) return Side{real(0.0), real(0.0), real(0.0), real(0.0)};
+    const bool ok = i < nu && k < N;
+    const size_t o = (sN() + (k < N ? k : N - 1)) * nu + (ok ? i : 0);
+    return side_at(blbu, bubu, blbum, bubum, o, ok);
   }
   __device__ Side side_x(int k, int i) const {
-    Side s{real(0.0), real(0.0), real(0.0), real(0.0)};
-    if (blbx && i < nx && k > 0) {  // stage-0 x bounds dropped (x0 embedding)
-      const size_t o = (size_t)k * nx + i;
-      s.lb = lbx()[o];
-      s.ub = ubx()[o];
-      s.ml = lbxm() ? (lbxm()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
-      s.mu = ubxm() ? (ubxm()[o] != real(0.0) ? real(1.0) : real(0.0)) : real(1.0);
-    }
-    return s;
+    if (!blbx) return Side{real(0.0), real(0.0), real(0.0), real(0.0)};
+    const bool ok = i < nx && k > 0;  // stage-0 x bounds dropped (x0 embedding)
+    const size_t o = (sN1() + k) * nx + (ok ? i : 0);
+    return side_at(blbx, bubx, blbxm, bubxm, o, ok);
   }
 };
 
@@ -930,28 +925,44 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       tstamp(20);
       real* stk = c.st(k);
       real* rec = stk + par * kRecSize;
+      // ---- the stage's loads that wait for none of its arithmetic, issued ahead of its
+      // first store: the memory counter retires in issue order, so every load issued behind
+      // a store waits for that store too, and the stage would pay one memory round trip per
+      // load-after-store group.  (Addresses are valid on every lane; the values are masked
+      // where the old conditional loads did not run.)  The A, B, S columns stay below, after
+      // the stores: loaded here they stay live across the residual phase and spill (box-u RB
+      // 424 B/lane).
+      const int iu = li < nu ? li : 0, ix = li < nx ? li : 0;
+      const real u_old = c.u()[(size_t)(k < N ? k : N - 1) * nu + iu];
+      const real x_old = c.x()[(size_t)k * nx + ix];
+      const real pi_old = c.pi()[(size_t)k * nx + ix];
+      const real du_s = stk[kStStep + li], dx_s = stk[kStStep + 12 + li], dpi_s = stk[kStStep + 24 + li];
+      Bar bu = c.bar(stk, 0, li), bx = c.bar(stk, 1, li);
+      const BarStep du = c.bstep(stk, 0, li), dx = c.bstep(stk, 1, li);
+      const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
+      const real qk = c.el(c.q() + (size_t)k * nx, nx, li);
+      const real rk = k < N ? c.el(c.r() + (size_t)k * nu, nu, li) : real(0.0);
+      if (k == N) c.col(c.Q() + (size_t)N * c.nxx(), nx, col, xel, P);  // P_N = Q_N + ...
       // ---- apply the previous step to stage k ----
       real uk = real(0.0), xk = real(0.0), pik = real(0.0);
       if (k < N && uel) {
-        uk = step(c.u()[(size_t)k * nu + lane], alpha_p, stk[kStStep + lane]);
+        uk = step(u_old, alpha_p, du_s);
         c.u()[(size_t)k * nu + lane] = uk;
       }
       if (xel) {
         if (k == 0) {
-          xk = c.x()[li];  // x_0 = x0 (never updated); pi_0 is not an iterate
+          xk = x_old;  // x_0 = x0 (never updated); pi_0 is not an iterate
         } else {
-          xk = step(c.x()[(size_t)k * nx + lane], alpha_p, stk[kStStep + 12 + lane]);
-          pik = step(c.pi()[(size_t)k * nx + lane], alpha_d, stk[kStStep + 24 + lane]);
+          xk = step(x_old, alpha_p, dx_s);
+          pik = step(pi_old, alpha_d, dpi_s);
           c.x()[(size_t)k * nx + lane] = xk;
           c.pi()[(size_t)k * nx + lane] = pik;
         }
       }
-      Bar bu{0, 0, 1, 1}, bx{0, 0, 1, 1};
-      const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
-      if (lane < kMaxDim) {
-        bu = c.bar(stk, 0, lane);
-        bx = c.bar(stk, 1, lane);
-        const BarStep du = c.bstep(stk, 0, lane), dx = c.bstep(stk, 1, lane);
+      if (lane >= kMaxDim) {
+        bu = Bar{0, 0, 1, 1};
+        bx = Bar{0, 0, 1, 1};
+      } else {
         bu.tl = step(bu.tl, alpha_p, du.dtl);
         bu.tu = step(bu.tu, alpha_p, du.dtu);
         bu.ll = step(bu.ll, alpha_d, du.dll);
@@ -964,8 +975,6 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         c.put_bar(stk, 1, lane, bx);
       }
       // ---- residual terms without the stage blocks (element-owned) ----
-      const real qk = c.el(c.q() + (size_t)k * nx, nx, li);
-      const real rk = k < N ? c.el(c.r() + (size_t)k * nu, nu, li) : real(0.0);
       real rgx = qk - pik, rgu = rk;
       // general rows, one pass per 12-row chunk with C / D read once: apply the
       // step, row values (row-owned through LDS), res_d / res_m, res_g += C'(lam_u -
@@ -1126,8 +1135,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       SRBD_PHASE_FENCE();
       tstamp(21);
       if (k == N) {
-        // terminal stage: P_N = Q_N + diag(Gamma_x) (+ C'Gamma C), p_N = q~_N
-        c.col(c.Q() + (size_t)N * c.nxx(), nx, col, xel, P);
+        // terminal stage: P_N = Q_N + diag(Gamma_x) (+ C'Gamma C), p_N = q~_N (Q_N loaded above)
         const real qx = dot_bcast(P, xk, real(0.0));
         if (k > 0) objl += xk * (real(0.5) * qx + qk);
         finish_u(real(0.0));  // no u_N: res_g,u = 0
@@ -1146,26 +1154,24 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
       } else {
         // ---- A, B (kept by the factorization), S (kept in LDS): residual products ----
-        real A_[12], B_[12];
+        real A_[12], B_[12], Sh[12];
         c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, A_);
         c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, B_);
+        c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, Sh);
+        const real bk = c.el(c.b() + (size_t)k * nx, nx, li);
         rgx = dot_bcast(A_, pin, rgx);  // + A'pi_{k+1}
         rgu = dot_bcast(B_, pin, rgu);  // + B'pi_{k+1}
         lds_put_col(ldsA, lane, A_);
         lds_put_col(ldsB, lane, B_);
         real sxu;  // (S x)_l
-        {
-          real Sc[12];
-          c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, Sc);
-          rgx = dot_bcast(Sc, uk, rgx);  // + S'u
-          lds_put_col(ldsS, lane, Sc);
-        }
+        rgx = dot_bcast(Sh, uk, rgx);  // + S'u
+        lds_put_col(ldsS, lane, Sh);
         lds_wave_fence();
         real rb;  // res_b = A x + B u + b - x_{k+1}
         {
           real M[12];
           lds_get_row(ldsA, li, M);
-          rb = dot_bcast(M, xk, c.el(c.b() + (size_t)k * nx, nx, li) - xn);
+          rb = dot_bcast(M, xk, bk - xn);
           lds_get_row(ldsB, li, M);
           rb = dot_bcast(M, uk, rb);
           lds_get_row(ldsS, li, M);
@@ -1247,7 +1253,10 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
         }
         lds_wave_fence();
-        if constexpr (kRecImg<GEN>) rec_copy(rec, img, lane);
+#ifndef SRBD_DIAG_NO_REC_STORE
+#define SRBD_DIAG_NO_REC_STORE 0
+#endif
+        if constexpr (kRecImg<GEN> && !SRBD_DIAG_NO_REC_STORE) rec_copy(rec, img, lane);
         // the next stage overwrites this group's LDS blocks: reads done first
         lds_wave_fence();
         tstamp(23);
@@ -1331,31 +1340,40 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           real* stk = c.st(k);
           real* rec = stk + par * kRecSize;
           const real* recn = c.st(k + 1) + par * kRecSize;
+          // the stage's element-owned loads, all issued before any is waited for (valid
+          // addresses on every lane, masked after; a load under a lane condition would be a
+          // branch that waits for it)
           const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
-          // x, u enter only through the barrier terms of the bound families present
-          const real uv = uel && c.has_bars(0) ? c.u()[(size_t)k * nu + lane] : real(0.0);
-          const real xv = xel && c.has_bars(1) ? c.x()[(size_t)k * nx + lane] : real(0.0);
-          real Gu = real(0.0), gu = real(0.0), Gx = real(0.0), gx = real(0.0);
-          if (lane < kMaxDim) {
-            const BarStep du = c.bstep(stk, 0, lane), dx = c.bstep(stk, 1, lane);
-            gamma_of(su, c.bar(stk, 0, lane), uv, du.dll * du.dtl, du.dlu * du.dtu, sigma_mu, Gu, gu);
-            gamma_of(sx, c.bar(stk, 1, lane), xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, Gx, gx);
-          }
-          real rt = lane < kMaxDim && uel ? stk[kStRes + lane] + gu : real(0.0);
-          real qt = lane < kMaxDim && xel ? stk[kStRes + 12 + lane] + gx : real(0.0);
+          const int iu = li < nu ? li : 0, ix = li < nx ? li : 0;
+          const real u_ld = c.u()[(size_t)k * nu + iu], x_ld = c.x()[(size_t)k * nx + ix];
+          const Bar bu = c.bar(stk, 0, li), bx = c.bar(stk, 1, li);
+          const BarStep du = c.bstep(stk, 0, li), dx = c.bstep(stk, 1, li);
+          const real r_ld = stk[kStRes + li], q_ld = stk[kStRes + 12 + li], b_ld = stk[kStRes + 24 + li];
+          real gv_ld = real(0.0);
           if constexpr (GEN == 1) {
             // D'gamma_corr = D'gamma_pred + sigma mu D'e + D'z (gamma is affine in both)
-            if (lane < kMaxDim && uel) {
-              const real* v = c.gv(k);
-              rt += v[lane] + v[24 + lane] + sigma_mu * v[12 + lane];
-            }
+            const real* v = c.gv(k);
+            gv_ld = v[li] + v[24 + li] + sigma_mu * v[12 + li];
+          }
+          // x, u enter only through the barrier terms of the bound families present
+          const real uv = uel && c.has_bars(0) ? u_ld : real(0.0);
+          const real xv = xel && c.has_bars(1) ? x_ld : real(0.0);
+          real Gu = real(0.0), gu = real(0.0), Gx = real(0.0), gx = real(0.0);
+          if (lane < kMaxDim) {
+            gamma_of(su, bu, uv, du.dll * du.dtl, du.dlu * du.dtu, sigma_mu, Gu, gu);
+            gamma_of(sx, bx, xv, dx.dll * dx.dtl, dx.dlu * dx.dtu, sigma_mu, Gx, gx);
+          }
+          real rt = lane < kMaxDim && uel ? r_ld + gu : real(0.0);
+          real qt = lane < kMaxDim && xel ? q_ld + gx : real(0.0);
+          if constexpr (GEN == 1) {
+            if (lane < kMaxDim && uel) rt += gv_ld;
           } else if constexpr (GEN) {
             real ra, qa;
             g_grad(k, true, sigma_mu, ra, qa);
             if (lane < kMaxDim && uel) rt += ra;
             if (lane < kMaxDim && xel) qt += qa;
           }
-          const real bt = lane < kMaxDim ? stk[kStRes + 24 + lane] : real(0.0);
+          const real bt = lane < kMaxDim ? b_ld : real(0.0);
           // w = P_{k+1} b~ + p_{k+1}
           const real w = rec_P_mul(recn, bt, pnext);
           // g = r~ + B'w ; f = q~ + A'w

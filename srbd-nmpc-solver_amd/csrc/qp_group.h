@@ -390,13 +390,16 @@ __device__ __forceinline__ void store_packed_col(T* pk, int lane, const T (&v)[1
     if (I >= lane) pk[cj + I] = v[I];
   });
 }
+// (The loaders below read every element at an address inside the 78-value block, valid
+// for every r, c in 0..11, and select: a load under a lane-dependent condition becomes a
+// branch of its own that waits for its load, one memory round trip per element.)
 // row r (= column r) of a symmetric matrix stored as its packed lower triangle
 template <typename T>
 __device__ __forceinline__ void load_packed_sym(const T* pk, int r, T (&v)[12]) {
   const int cr = packed_col(r) - r;
   sfor<0, 12>([&](auto j) {
     constexpr int J = decltype(j)::value;
-    v[J] = J <= r ? pk[packed_col(J) + r - J] : pk[cr + J];
+    v[J] = pk[J <= r ? packed_col(J) + r - J : cr + J];
   });
 }
 // row r of a packed lower-triangular L, diagonal included: v[j] = L[r][j] (j <= r), else 0
@@ -404,7 +407,8 @@ template <typename T>
 __device__ __forceinline__ void load_packed_lrow_d(const T* pk, int r, T (&v)[12]) {
   sfor<0, 12>([&](auto j) {
     constexpr int J = decltype(j)::value;
-    v[J] = J <= r ? pk[packed_col(J) + r - J] : T(0);
+    const T x = pk[packed_col(J) + r - J];
+    v[J] = J <= r ? x : T(0);
   });
 }
 // column c of a packed lower-triangular L, diagonal included: v[i] = L[i][c] (i >= c), else 0
@@ -413,7 +417,8 @@ __device__ __forceinline__ void load_packed_lcol_d(const T* pk, int c, T (&v)[12
   const int cc = packed_col(c) - c;
   sfor<0, 12>([&](auto i) {
     constexpr int I = decltype(i)::value;
-    v[I] = I >= c ? pk[cc + I] : T(0);
+    const T x = pk[cc + I];
+    v[I] = I >= c ? x : T(0);
   });
 }
 // strictly-lower row r of a packed lower-triangular L: v[j] = L[r][j] (j < r), else 0
@@ -421,7 +426,8 @@ template <typename T>
 __device__ __forceinline__ void load_packed_lrow(const T* pk, int r, T (&v)[12]) {
   sfor<0, 12>([&](auto j) {
     constexpr int J = decltype(j)::value;
-    v[J] = J < r ? pk[packed_col(J) + r - J] : T(0);
+    const T x = pk[packed_col(J) + r - J];
+    v[J] = J < r ? x : T(0);
   });
 }
 // strictly-lower column c of a packed lower-triangular L: v[i] = L[i][c] (i > c), else 0
@@ -430,7 +436,8 @@ __device__ __forceinline__ void load_packed_lcol(const T* pk, int c, T (&v)[12])
   const int cc = packed_col(c) - c;
   sfor<0, 12>([&](auto i) {
     constexpr int I = decltype(i)::value;
-    v[I] = I > c ? pk[cc + I] : T(0);
+    const T x = pk[cc + I];
+    v[I] = I > c ? x : T(0);
   });
 }
 
