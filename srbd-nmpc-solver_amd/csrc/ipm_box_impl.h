@@ -303,17 +303,16 @@ struct Ctx {
   __device__ void put_bstep(real* stk, int which, int i, const BarStep& d) const {
     if (has_bars(which)) store_bstep(stk, which, i, d);
   }
+  // (An absent family reads element 0 of q instead and is masked: no branch either.)
   __device__ Side side_u(int k, int i) const {
-    if (!blbu) return Side{real(0.0), real(0.0), real(0.0), real(0.0)};
-    const bool ok = i < nu && k < N;
-    const size_t o = (sN() + (k < N ? k : N - 1)) * nu + (ok ? i : 0);
-    return side_at(blbu, bubu, blbum, bubum, o, ok);
+    const bool has = blbu != nullptr, ok = has && i < nu && k < N;
+    const size_t o = has ? (sN() + (k < N ? k : N - 1)) * nu + (ok ? i : 0) : 0;
+    return side_at(has ? blbu : bq, has ? bubu : bq, blbum, bubum, o, ok);
   }
   __device__ Side side_x(int k, int i) const {
-    if (!blbx) return Side{real(0.0), real(0.0), real(0.0), real(0.0)};
-    const bool ok = i < nx && k > 0;  // stage-0 x bounds dropped (x0 embedding)
-    const size_t o = (sN1() + k) * nx + (ok ? i : 0);
-    return side_at(blbx, bubx, blbxm, bubxm, o, ok);
+    const bool has = blbx != nullptr, ok = has && i < nx && k > 0;  // stage-0 x bounds dropped
+    const size_t o = has ? (sN1() + k) * nx + (ok ? i : 0) : 0;
+    return side_at(has ? blbx : bq, has ? bubx : bq, blbxm, bubxm, o, ok);
   }
 };
 
@@ -1154,10 +1153,14 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
       } else {
         // ---- A, B (kept by the factorization), S (kept in LDS): residual products ----
-        real A_[12], B_[12], Sh[12];
+        real A_[12], B_[12], Sh[12], Rh[12];
         c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, A_);
         c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, B_);
         c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, Sh);
+        // the box kernels take R with them (one round trip less); the general-row kernels,
+        // at their register limit, when the factorization asks for it (cone +0.7% otherwise)
+        constexpr bool kEarlyR = GEN == 0;
+        if constexpr (kEarlyR) c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, Rh);
         const real bk = c.el(c.b() + (size_t)k * nx, nx, li);
         rgx = dot_bcast(A_, pin, rgx);  // + A'pi_{k+1}
         rgu = dot_bcast(B_, pin, rgu);  // + B'pi_{k+1}
@@ -1191,8 +1194,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         SRBD_PHASE_FENCE();
         real rt = real(0.0);
         auto loadR = [&](greal (&Rc)[12]) {
-          real Rr[12];
-          c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, Rr);
+          real (&Rr)[12] = Rh;
+          if constexpr (!kEarlyR) c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, Rr);
           const real ru = dot_bcast(Rr, uk, real(0.0));  // R u, before the barrier Hessian goes in
           objl += uk * (real(0.5) * ru + rk + sxu);
           rt = finish_u(rgu + ru);
