@@ -24,8 +24,10 @@ batch = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 pkg = bench.import_pkg()
 capi = pkg.capi
 L = capi.lib()
-L.srbd_qp_diag_tstamps_ipm.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-L.srbd_qp_diag_tstamps_ipm.restype = C.c_int
+STAMPS = hasattr(L, "srbd_qp_diag_tstamps_ipm")  # a -DSRBD_TSTAMP=1 build; else timing only
+if STAMPS:
+    L.srbd_qp_diag_tstamps_ipm.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    L.srbd_qp_diag_tstamps_ipm.restype = C.c_int
 N, constraints = bench.WORKLOADS[name][:2]
 dtype = bench.WORKLOADS[name][4] if len(bench.WORKLOADS[name]) > 4 else "f64"
 ng = 24 if constraints == "cone" else 0
@@ -50,15 +52,17 @@ names = {20: "RB stage", 21: "RB step applied, rows", 22: "RB A,B,S, residuals",
          40: "B2 stage"}
 res = []
 for rep in range(4):
-    L.srbd_qp_diag_tstamps_ipm(buf, 4096)  # reset
+    if STAMPS:
+        L.srbd_qp_diag_tstamps_ipm(buf, 4096)  # reset
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(ext)
     h.solve_device(batch, s, data, sol)
     e1.record(ext)
     h.synchronize()
-    n = L.srbd_qp_diag_tstamps_ipm(buf, 4096)
+    n = L.srbd_qp_diag_tstamps_ipm(buf, 4096) if STAMPS else 0
     res.append((e0.elapsed_time(e1) * 1e3, np.frombuffer(buf, dtype=np.uint64)[:2 * n].reshape(n, 2).astype(np.int64)))
-us, arr = res[-1]
+us = min(r[0] for r in res)
+arr = res[-1][1]
 ids, cyc = arr[:, 0], arr[:, 1]
 per = {}
 for i in range(1, len(ids)):
