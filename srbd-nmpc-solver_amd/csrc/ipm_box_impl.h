@@ -1256,10 +1256,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
         }
         lds_wave_fence();
-#ifndef SRBD_DIAG_NO_REC_STORE
-#define SRBD_DIAG_NO_REC_STORE 0
-#endif
-        if constexpr (kRecImg<GEN> && !SRBD_DIAG_NO_REC_STORE) rec_copy(rec, img, lane);
+        if constexpr (kRecImg<GEN>) rec_copy(rec, img, lane);
         // the next stage overwrites this group's LDS blocks: reads done first
         lds_wave_fence();
         tstamp(23);
