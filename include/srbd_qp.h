@@ -126,7 +126,8 @@ enum { SRBD_QP_LAYOUT_QP_MAJOR = 0, SRBD_QP_LAYOUT_STAGE_MAJOR = 1 };
 /* hpipm::OcpQpIpmSolverSettings (ocp_qp_ipm_solver_settings.hpp:26-86);
  * srbd_qp_default_settings() gives the same defaults.                     */
 typedef struct srbd_qp_settings {
-  int mode;
+  int mode;       /* HpipmMode: 0 SpeedAbs, 1 Speed, 2 Balance, 3 Robust; selects
+                  * itref_corr_max 0 / 0 / 2 / 4 (boxes)      */
   int iter_max;
   double alpha_min;
   double mu0;
@@ -189,8 +190,11 @@ typedef struct srbd_qp_solution_f64 {
                             * rows hpipm-cpp copies into OcpQpIpmSolverStatistics
                             * (ocp_qp_ipm_solver.cpp:381-403): alpha_aff, mu_aff,
                             * sigma, alpha_prim, alpha_dual, mu, res_stat, res_eq,
-                            * res_ineq, res_comp, obj, then 7 columns that stay 0
-                            * (no LQ factorization / iterative refinement).    */
+                            * res_ineq, res_comp, obj, lq_fact (0: none),
+                            * itref_pred (0), itref_corr (corrections of the
+                            * step, mode Balance / Robust with boxes), then
+                            * lin_res_stat, lin_res_eq of the last refinement
+                            * check, lin_res_ineq, lin_res_comp (0: exact).    */
 } srbd_qp_solution_f64;
 
 /* fp32 twins (BASELINE config 5; HPIPM's s_ocp_qp_ipm, hpipm_s_ocp_qp_ipm.h:238):

@@ -584,7 +584,6 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
   double* cdx = (double*)calloc((size_t)(N + 1) * nx, sizeof(double));
   double* cdu = (double*)calloc((size_t)N * nu + 1, sizeof(double));
   double* cdpi = (double*)calloc((size_t)(N + 1) * nx, sizeof(double));
-  int itref_g[1025];
   int nc = 0;
   stage_rows_t* st = build_rows(&d, &nc);
   int rc = 0;
@@ -773,52 +772,68 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
       riccati_forward(&d, &w, zero, dx, du, dpi);
       STEP_TLAM();
     }
-    /* iterative refinement of the final step on the reduced (Gamma-augmented) KKT
-     * system: the dt / dlam equations hold exactly by construction (STEP_TLAM), so
-     * the residual lives in the stationarity and dynamics rows; solve again with the
-     * same factors and add the correction.                                           */
-    for (int ir = 0; ir < set->itref_corr_max; ++ir) {
-      double* gsave = rg; (void)gsave;
-      for (int s = 0; s <= N; ++s) {
-        int nu_k = st[s].nu_k, ns = nu_k + nx;
-        const double* Ht = w.Ht + s * w.hstride;
-        double* gt = w.gt + s * w.gstride;
-        double v[64], r1[64];
-        for (int i = 0; i < nu_k; ++i) v[i] = du[(size_t)s * nu + i];
-        for (int i = 0; i < nx; ++i) v[nu_k + i] = dx[(size_t)s * nx + i];
-        for (int i = 0; i < ns; ++i) {
-          double acc = gt[i];
-          for (int j = 0; j < ns; ++j) acc += M_(Ht, ns, i, j) * v[j];
-          r1[i] = acc;
+    /* iterative refinement of the final step (HPIPM itref_corr_max: Balance 2, Robust 4;
+     * restated from HPIPM's d_ocp_qp_ipm_solve / d_ocp_qp_res_compute_lin, not vendored):
+     * the linear residual of the Newton system at the step, in its full form (QP Hessian,
+     * multiplier steps of the rows, dynamics); the dt / dlam rows hold exactly by
+     * construction (STEP_TLAM), so they are not formed.  Each check stops the refinement
+     * when the residual's infinity norms are below the tolerances (or below 1e-3 of the
+     * first check's); otherwise the same factors solve for the correction, which is added.
+     * ipm_box_impl.h kPhIR / kPhF3 restate the same for the HIP kernels.                */
+    {
+      double n0g = 0.0, n0b = 0.0;
+      for (int ir = 0; ir < set->itref_corr_max; ++ir) {
+        double ng = 0.0, nb = 0.0;
+        for (int s = 0; s <= N; ++s) {
+          int nu_k = st[s].nu_k, ns = nu_k + nx;
+          double H[64 * 64], gdum[64], v[64], r1[64];
+          fill_stage_H(&d, s, H, gdum);
+          for (int i = 0; i < nu_k; ++i) v[i] = du[(size_t)s * nu + i];
+          for (int i = 0; i < nx; ++i) v[nu_k + i] = dx[(size_t)s * nx + i];
+          for (int i = 0; i < ns; ++i) {
+            double acc = rg[(size_t)s * w.gstride + i];
+            for (int j = 0; j < ns; ++j) acc += M_(H, ns, i, j) * v[j];
+            r1[i] = acc;
+          }
+          for (int i = 0; i < st[s].nrow; ++i) {
+            row_t* rw = &st[s].rows[i];
+            double c = (rw->has_u ? rw->dlam_u : 0.0) - (rw->has_l ? rw->dlam_l : 0.0);
+            row_axpy(&d, rw, nu_k, c, r1, r1 + nu_k);
+          }
+          if (s < N) {
+            double t[32];
+            mtv(nx, nu, qB(&d, s), dpi + (size_t)(s + 1) * nx, t);
+            for (int i = 0; i < nu; ++i) r1[i] += t[i];
+            mtv(nx, nx, qA(&d, s), dpi + (size_t)(s + 1) * nx, t);
+            for (int i = 0; i < nx; ++i) r1[nu_k + i] += t[i];
+          }
+          if (s > 0) for (int i = 0; i < nx; ++i) r1[nu_k + i] -= dpi[(size_t)s * nx + i];
+          else for (int i = 0; i < nx; ++i) r1[nu_k + i] = 0.0;  /* x_0 fixed */
+          for (int i = 0; i < ns; ++i) ng = fmax(ng, fabs(r1[i]));
+          memcpy(itg + (size_t)s * w.gstride, r1, sizeof(double) * ns);
+          if (s < N) {
+            double t1[32], t2[32];
+            mv(nx, nx, qA(&d, s), dx + (size_t)s * nx, t1);
+            mv(nx, nu, qB(&d, s), du + (size_t)s * nu, t2);
+            for (int i = 0; i < nx; ++i) {
+              double rbi = rb[(size_t)s * nx + i] + t1[i] + t2[i] - dx[(size_t)(s + 1) * nx + i];
+              itb[(size_t)s * nx + i] = rbi;
+              nb = fmax(nb, fabs(rbi));
+            }
+          }
         }
-        if (s < N) {
-          double t[32];
-          mtv(nx, nu, qB(&d, s), dpi + (size_t)(s + 1) * nx, t);
-          for (int i = 0; i < nu; ++i) r1[i] += t[i];
-          mtv(nx, nx, qA(&d, s), dpi + (size_t)(s + 1) * nx, t);
-          for (int i = 0; i < nx; ++i) r1[nu_k + i] += t[i];
-        }
-        if (s > 0) for (int i = 0; i < nx; ++i) r1[nu_k + i] -= dpi[(size_t)s * nx + i];
-        else for (int i = 0; i < nx; ++i) r1[nu_k + i] = 0.0;
-        itref_g[s] = 0;
-        memcpy(itg + (size_t)s * w.gstride, r1, sizeof(double) * ns);
-        if (s < N) {
-          double t1[32], t2[32];
-          mv(nx, nx, qA(&d, s), dx + (size_t)s * nx, t1);
-          mv(nx, nu, qB(&d, s), du + (size_t)s * nu, t2);
-          for (int i = 0; i < nx; ++i)
-            itb[(size_t)s * nx + i] = t1[i] + t2[i] + w.bt[(size_t)s * nx + i] - dx[(size_t)(s + 1) * nx + i];
-        }
+        if (ir == 0) { n0g = ng; n0b = nb; }
+        if ((ng < set->tol_stat || ng < 1e-3 * n0g) && (nb < set->tol_eq || nb < 1e-3 * n0b)) break;
+        /* correction: same factors, right-hand side = the residual */
+        double* gkeep = w.gt; double* bkeep = w.bt;
+        w.gt = itg; w.bt = itb;
+        riccati_vectors(&d, &w);
+        riccati_forward(&d, &w, zero, cdx, cdu, cdpi);
+        w.gt = gkeep; w.bt = bkeep;
+        for (size_t i = 0; i < (size_t)(N + 1) * nx; ++i) { dx[i] += cdx[i]; if (i >= (size_t)nx) dpi[i] += cdpi[i]; }
+        for (size_t i = 0; i < (size_t)N * nu; ++i) du[i] += cdu[i];
+        STEP_TLAM();
       }
-      /* correction: same factors, rhs = the residual */
-      double* gkeep = w.gt; double* bkeep = w.bt;
-      w.gt = itg; w.bt = itb;
-      riccati_vectors(&d, &w);
-      riccati_forward(&d, &w, zero, cdx, cdu, cdpi);
-      w.gt = gkeep; w.bt = bkeep;
-      for (size_t i = 0; i < (size_t)(N + 1) * nx; ++i) { dx[i] += cdx[i]; if (i >= (size_t)nx) dpi[i] += cdpi[i]; }
-      for (size_t i = 0; i < (size_t)N * nu; ++i) du[i] += cdu[i];
-      STEP_TLAM();
     }
 #undef STEP_TLAM
 

@@ -80,10 +80,19 @@ DEFAULT_SETTINGS = dict(iter_max=15, alpha_min=1e-8, mu0=1e2, tol_stat=1e-8, tol
                         split_step=0, ric_alg=1, itref_corr_max=0)  # hpipm-cpp defaults (settings.hpp:26-86)
 
 
-def _settings(s: Optional[Dict]) -> _Settings:
+# HPIPM's mode-dependent itref_corr_max (d_ocp_qp_ipm_arg_set_default; the HIP library
+# derives it from settings.mode the same way, srbd_qp_capi.hip)
+MODE_ITREF = {"SpeedAbs": 0, "Speed": 0, "Balance": 2, "Robust": 4, 0: 0, 1: 0, 2: 2, 3: 4}
+
+
+def _settings(s: Optional[Dict], ng: int = 0) -> _Settings:
     d = dict(DEFAULT_SETTINGS)
     if s:
         d.update({k: v for k, v in s.items() if k in d})
+        if "mode" in s and "itref_corr_max" not in s:
+            # the HIP kernels refine box-constrained steps only: with general
+            # rows the checker runs the GPU's algorithm, without refinement
+            d["itref_corr_max"] = MODE_ITREF[s["mode"]] if ng == 0 else 0
     return _Settings(**d)
 
 
@@ -104,7 +113,7 @@ def solve(batch, settings: Optional[Dict] = None, x0: Optional[np.ndarray] = Non
     """Solve every QP of an OcpQpBatch one by one; returns a dict of arrays."""
     p = batch.packed()
     N, nx, nu, ng, nb = batch.N, batch.nx, batch.nu, batch.ng, batch.batch
-    st = _settings(settings)
+    st = _settings(settings, batch.ng)
     out = {
         "x": np.zeros((nb, N + 1, nx)), "u": np.zeros((nb, N, nu)), "pi": np.zeros((nb, N + 1, nx)),
         "P": np.zeros((nb, N + 1, nx, nx)), "p": np.zeros((nb, N + 1, nx)),
@@ -155,7 +164,7 @@ def solve_batch_threaded(batch, settings: Optional[Dict] = None, x0=None, thread
     threads = threads or os.cpu_count() or 1
     keep = []
     qp = _make_qp(p, N, nx, nu, ng, keep)
-    st = _settings(settings)
+    st = _settings(settings, batch.ng)
     x0 = np.zeros((nb, nx)) if x0 is None else np.ascontiguousarray(x0, dtype=np.float64).reshape(nb, nx)
     x = np.zeros((nb, N + 1, nx))
     u = np.zeros((nb, N, nu))

@@ -13,10 +13,16 @@ constexpr real kThr0 = real(0.1);     // minimum initial slack (HPIPM init_var)
 
 // phase kernels (one launch each, per IPM iteration; see launch_ipm_box)
 constexpr int kPhInit = 0, kPhRB = 1, kPhF1 = 2, kPhB2 = 3, kPhF2 = 4, kPhOut = 5;
+// iterative refinement of the corrector step (boxes): IR = residual of the step's linear
+// system + the correction's backward recursion, F3 = the correction's forward sweep
+constexpr int kPhIR = 6, kPhF3 = 7;
 // per-QP scalar state, kQsSize reals at the head of the QP's workspace
 constexpr int kQsAlphaP = 0, kQsAlphaD = 1, kQsLastAmin = 2, kQsMu = 3, kQsMuSum = 4,
               kQsSigmaMu = 5, kQsStatus = 6, kQsIter = 7, kQsNc = 8, kQsResStat = 9,
-              kQsResEq = 10, kQsResIneq = 11, kQsResComp = 12, kQsObj = 13, kQsSize = 16;
+              kQsResEq = 10, kQsResIneq = 11, kQsResComp = 12, kQsObj = 13,
+              // iterative refinement of this iteration's step: corrections applied, done flag,
+              // the first check's linear-residual norms (HPIPM's itref_qp_norm0)
+              kQsItCnt = 14, kQsItDone = 15, kQsItN0g = 16, kQsItN0b = 17, kQsSize = 20;
 constexpr real kStepTau = real(0.995);  // fraction to the boundary
 
 __device__ __forceinline__ real gsum(real v) {
@@ -1312,6 +1318,230 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 
     return;
   }
+  if constexpr (PH == kPhIR || PH == kPhF3) {
+    // =========== iterative refinement of the step (HPIPM itref_corr_max; boxes) ===========
+    // The step (du, dx, dpi and the bounds' dt, dlam) solves the Newton system only up to the
+    // factorization's rounding.  IR (k = N..0) forms the linear residual of that system at the
+    // step in its full form -- QP Hessian and multiplier steps, not the Gamma-reduced one, so
+    // no right-hand side of the corrector is needed again (the dt / dlam rows hold exactly by
+    // construction, bar_step) --
+    //   r_u = res_g,u + R du + S dx + B'dpi_{k+1} - dlam_l + dlam_u
+    //   r_x = res_g,x + S'du + Q dx + A'dpi_{k+1} - dpi_k - dlam_l + dlam_u   (k >= 1)
+    //   r_b = res_b + A dx + B du - dx_{k+1}
+    // and runs the corrector's backward recursion with (r_u, r_x, r_b) as its right-hand side
+    // (same factors: the record of this iteration's RB).  Its infinity norms decide, as in
+    // HPIPM: below the tolerances (or 1e-3 of the first check's) the refinement stops, else
+    // F3 (k = 0..N) forms the correction, adds it to the step, updates dt / dlam (linear in
+    // the primal step: ddt = +-ddv, ddlam = -lam ddt / t) and redoes the step lengths.
+    // (F2 advanced iter: the step's factorization has the parity of iter - 1.)
+    static_assert(GEN == 0, "iterative refinement: box constraints only");
+    if (qs[kQsItDone] != real(0.0)) return;
+    const int fpar = (iter - 1) & 1;
+    real* const next = a.stat && lane == 0 ? a.stat + ((size_t)qp * a.stat_rows + iter) * kStatCols
+                                           : nullptr;
+    if constexpr (PH == kPhIR) {
+      real* const ldsA = group_lds_blocks<GEN>();
+      real* const ldsB = ldsA + 144;
+      real* const ldsS = ldsA + 288;
+      real ng = real(0.0), nb = real(0.0), pnext = real(0.0);
+      for (int k = N; k >= 0; --k) {
+        real* stk = c.st(k);
+        real* rec = stk + fpar * kRecSize;
+        const real* stn = c.st(k < N ? k + 1 : k);
+        // the stage's element-owned loads first (valid addresses on every lane, masked after)
+        const real du_ld = stk[kStStep + li], dx_ld = stk[kStStep + 12 + li], dpi_ld = stk[kStStep + 24 + li];
+        const real dpin_ld = stn[kStStep + 24 + li], dxn_ld = stn[kStStep + 12 + li];
+        const real rgu = stk[kStRes + li], rgx = stk[kStRes + 12 + li], rbk = stk[kStRes + 24 + li];
+        const BarStep bdu = c.bstep(stk, 0, li), bdx = c.bstep(stk, 1, li);
+        const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
+        const bool el = lane < kMaxDim;
+        const real duv = el && uel && k < N ? du_ld : real(0.0);
+        const real dxv = el && xel && k > 0 ? dx_ld : real(0.0);
+        const real dpinv = el && xel && k < N ? dpin_ld : real(0.0);
+        real ru = rgu + su.mu * bdu.dlu - su.ml * bdu.dll;
+        real rx = rgx + sx.mu * bdx.dlu - sx.ml * bdx.dll - dpi_ld;
+        real rb = rbk - dxn_ld;
+        real Ac[12], Bc[12];
+        if (k < N) {
+          c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, Ac);
+          c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, Bc);
+          real Sc[12];
+          c.col(c.S() + (size_t)k * c.nxu(), nu, col, xel, Sc);
+          rx = dot_bcast(Ac, dpinv, rx);  // + A'dpi_{k+1}
+          ru = dot_bcast(Bc, dpinv, ru);  // + B'dpi_{k+1}
+          rx = dot_bcast(Sc, duv, rx);    // + S'du
+          lds_put_col(ldsA, lane, Ac);
+          lds_put_col(ldsB, lane, Bc);
+          lds_put_col(ldsS, lane, Sc);
+          lds_wave_fence();
+          real M[12];
+          lds_get_row(ldsA, li, M);
+          rb = dot_bcast(M, dxv, rb);  // + A dx
+          lds_get_row(ldsB, li, M);
+          rb = dot_bcast(M, duv, rb);  // + B du
+          lds_get_row(ldsS, li, M);
+          ru = dot_bcast(M, dxv, ru);  // + S dx
+          lds_wave_fence();
+          real Rc[12];
+          c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, Rc);
+          ru = dot_bcast(Rc, duv, ru);  // + R du
+        }
+        {
+          real Qc[12];
+          c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
+          rx = dot_bcast(Qc, dxv, rx);  // + Q dx
+        }
+        if (!(el && uel && k < N)) ru = real(0.0);
+        if (!(el && xel && k > 0)) rx = real(0.0);  // (x_0 is fixed)
+        if (!(el && xel && k < N)) rb = real(0.0);
+        ng = fmax(ng, fmax(nabs(ru), nabs(rx)));
+        nb = fmax(nb, nabs(rb));
+        // the correction's b~ for F3, in the other parity's record slot (the previous
+        // factorization's, dead until the next RB overwrites it)
+        if (el) stk[(fpar ^ 1) * kRecSize + lane] = rb;
+        if (k == N) {
+          pnext = rx;  // p_N = q~_N (the terminal P_N carries Q_N + Gamma)
+          if (el) rec[kRecPv + lane] = pnext;
+          continue;
+        }
+        // the corrector's recursion (B2) with (r_u, r_x, r_b) as its right-hand side
+        const real* recn = stn + fpar * kRecSize;
+        const real w = rec_P_mul(recn, rb, pnext);
+        real g = ru, f = rx;
+        dot_bcast2(Bc, Ac, w, g, f);
+        if (lane >= kMaxDim) g = real(0.0);
+        real Kc[12];
+        load12(rec + kRecK + col * 12, Kc);
+        const real pv = dot_bcast(Kc, g, f);
+        real Lr[12], Lc[12];
+        load_packed_lrow(rec + kRecL, li, Lr);
+        load_packed_lcol(rec + kRecL, col, Lc);
+        const real rs = rec[kRecRs + li];
+        real y = g;
+        sfor<0, 12>([&](auto kk) {
+          constexpr int K = decltype(kk)::value;
+          const real yk = bc<K>(y * rs);
+          if (lane == K) y = yk;
+          if (lane > K) y = fmadd(-Lr[K], yk, y);
+        });
+        sfor_down<0, 12>([&](auto kk) {
+          constexpr int K = decltype(kk)::value;
+          const real zk = bc<K>(y * rs);
+          if (lane == K) y = zk;
+          if (lane < K) y = fmadd(-Lc[K], zk, y);
+        });
+        const real kv = el && uel ? -y : real(0.0);
+        if (el) {
+          rec[kRecKv + lane] = kv;
+          rec[kRecPv + lane] = xel ? pv : real(0.0);
+        }
+        pnext = xel ? pv : real(0.0);
+      }
+      const real nga = gmax(ng), nba = gmax(nb);
+      const int cnt = (int)qs[kQsItCnt];
+      const real n0g = cnt == 0 ? nga : qs[kQsItN0g], n0b = cnt == 0 ? nba : qs[kQsItN0b];
+      const bool small = (nga < a.tol_stat || nga < real(1e-3) * n0g) &&
+                         (nba < a.tol_eq || nba < real(1e-3) * n0b);
+      if (lane == 0) {
+        if (cnt == 0) {
+          qs[kQsItN0g] = nga;
+          qs[kQsItN0b] = nba;
+        }
+        if (small) qs[kQsItDone] = real(1.0);
+      }
+      if (next) {  // HPIPM stat: lin_res_stat, lin_res_eq (the dt / dlam rows are exact)
+        next[14] = nga;
+        next[15] = nba;
+      }
+      return;
+    } else {
+      // ---- F3: the correction (forward, row-owned), added to the step ----
+      real ap = real(1e30), ad = real(1e30);
+      bool bad = false;
+      real dxc = real(0.0);  // correction of dx_0: 0 (x0 fixed)
+      for (int k = 0; k <= N; ++k) {
+        real* stk = c.st(k);
+        const real* rec = stk + fpar * kRecSize;
+        const real dpc = k > 0 ? rec_P_mul(rec, dxc, rec[kRecPv + li]) : real(0.0);
+        real duc = real(0.0), dxn = real(0.0);
+        if (k < N) {
+          real Kr[12], Ar[12];
+          sfor<0, 12>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            Kr[J] = rec[kRecK + J * 12 + li];
+          });
+          c.row(c.A() + (size_t)k * c.nxx(), nx, nx, li, xel, Ar);
+          duc = rec[kRecKv + li];
+          dxn = stk[(fpar ^ 1) * kRecSize + li];
+          dot_bcast2(Kr, Ar, dxc, duc, dxn);
+          if (!uel) duc = real(0.0);
+          real Br[12];
+          c.row(c.B() + (size_t)k * c.nxu(), nx, nu, li, xel, Br);
+          dxn = dot_bcast(Br, duc, dxn);
+        }
+        if (!uel || k == N) duc = real(0.0);
+        real dpcv = dpc;
+        if (!xel) {
+          dxn = real(0.0);
+          dpcv = real(0.0);
+        }
+        if (lane < kMaxDim) {
+          const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
+          const Bar bu = c.bar(stk, 0, lane), bx = c.bar(stk, 1, lane);
+          BarStep nu_ = c.bstep(stk, 0, lane), nx_ = c.bstep(stk, 1, lane);
+          const real du = stk[kStStep + lane] + duc, dx = stk[kStStep + 12 + lane] + dxc;
+          const real dpi = k > 0 ? stk[kStStep + 24 + lane] + dpcv : real(0.0);
+          auto upd = [&](const Side& sd, const Bar& b, BarStep& d, real dv) {
+            if (sd.ml != real(0.0)) {
+              d.dtl += dv;
+              d.dll -= b.ll * dv / b.tl;
+            }
+            if (sd.mu != real(0.0)) {
+              d.dtu -= dv;
+              d.dlu += b.lu * dv / b.tu;
+            }
+          };
+          upd(su, bu, nu_, k < N ? duc : real(0.0));
+          upd(sx, bx, nx_, dxc);
+          ratio(su, bu, nu_, ap, ad);
+          ratio(sx, bx, nx_, ap, ad);
+          bad |= huge(du) || huge(dx) || huge(dpi) || huge(nu_.dtl) || huge(nu_.dtu) || huge(nu_.dll) ||
+                 huge(nu_.dlu);
+          c.put_bstep(stk, 0, lane, nu_);
+          c.put_bstep(stk, 1, lane, nx_);
+          stk[kStStep + lane] = du;
+          stk[kStStep + 12 + lane] = dx;
+          stk[kStStep + 24 + lane] = dpi;
+        }
+        dxc = dxn;
+      }
+      ap = gmin(lane < kMaxDim ? ap : real(1e30));
+      ad = gmin(lane < kMaxDim ? ad : real(1e30));
+      if (gmax((lane < kMaxDim && bad) ? real(1.0) : real(0.0)) > real(0.0)) {
+        ap = real(0.0);
+        ad = real(0.0);
+      }
+      if (!a.split_step) {
+        ap = fmin(ap, ad);
+        ad = ap;
+      }
+      const real alpha_p_new = fmin(real(1.0), kStepTau * ap);
+      const real alpha_d_new = fmin(real(1.0), kStepTau * ad);
+      const int cnt = (int)qs[kQsItCnt] + 1;
+      if (lane == 0) {
+        qs[kQsAlphaP] = alpha_p_new;
+        qs[kQsAlphaD] = alpha_d_new;
+        qs[kQsLastAmin] = fmin(alpha_p_new, alpha_d_new);
+        qs[kQsItCnt] = (real)cnt;
+      }
+      if (next) {
+        next[3] = alpha_p_new;
+        next[4] = alpha_d_new;
+        next[13] = (real)cnt;  // HPIPM stat: itref_corr
+      }
+      return;
+    }
+  }
   const real mu = qs[kQsMu], musum_all = qs[kQsMuSum];
   real sigma_mu = qs[kQsSigmaMu];
   if constexpr (PH == kPhB2) {
@@ -1578,6 +1808,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         qs[kQsAlphaD] = alpha_d_new;
         qs[kQsLastAmin] = fmin(alpha_p_new, alpha_d_new);
         qs[kQsIter] = (real)(iter + 1);
+        qs[kQsItCnt] = real(0.0);  // this step's refinement (kPhIR / kPhF3) starts afresh
+        qs[kQsItDone] = real(0.0);
       }
       if (next) {
         next[3] = alpha_p_new;
@@ -1721,6 +1953,14 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
       hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF2, SQRT>), grid, block, 0, stream, b);
     } else if (a.pred_corr) {
       hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhB2, kPhF2, SQRT>), grid, block, 0, stream, b);
+    }
+    // HPIPM's iterative refinement of the corrector step (Balance / Robust; boxes only): at
+    // most itref_corr_max corrections, each after a check of the step's linear residual; a
+    // QP whose check passed returns at the top of the later ones
+    if constexpr (GEN == 0) {
+      if (a.pred_corr)
+        for (int r = 0; r < a.itref_corr_max; ++r)
+          hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhIR, kPhF3, SQRT>), grid, block, 0, stream, b);
     }
     if (ctl && it >= 1) {
       hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(a.ctl_ev[(it - 1) & 1]));

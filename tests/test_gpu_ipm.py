@@ -323,3 +323,49 @@ def test_batch_over_capacity_is_rejected(pkg):
     h = pkg.capi.Handle(5, 12, 12, 0, False, False, capacity=4)
     with pytest.raises(pkg.capi.SrbdQpError, match="exceeds capacity"):
         pkg.capi.solve(qp, x0, None, handle=h)
+
+
+@pytest.mark.parametrize("mode,ric_alg,nmax", [("Balance", 0, 2), ("Robust", 1, 4)])
+def test_itref_corrections_vs_oracle(pkg, oracle, mode, ric_alg, nmax):
+    """HPIPM's iterative refinement of the corrector step (mode Balance: at most 2
+    corrections per iteration, Robust: 4).  Tolerances below anything the
+    IPM reaches make every check fail, so every iteration runs its corrections (kPhIR /
+    kPhF3): the GPU and the oracle (the same refinement, ocp_qp_oracle.c) must follow the
+    same iterates, and the stat table counts the corrections (column 13) and holds the
+    checks' linear-residual norms (14, 15)."""
+    qp, x0 = helpers.random_constrained(16, 10, 12, 12, 0, 41, pkg.OcpQpBatch)
+    tiny = dict(tol_stat=1e-30, tol_eq=1e-30, tol_ineq=1e-30, tol_comp=1e-30)
+    st = dict(iter_max=8, mode=mode, ric_alg=ric_alg, **tiny)
+    out = pkg.capi.solve(qp, x0, st, stats=True)
+    ref = oracle.solve(qp, st, x0=x0)
+    plain = oracle.solve(qp, dict(st, itref_corr_max=0), x0=x0)
+    assert np.all(out["status"] == 1) and np.all(ref["status"] == 1), (out["status"], ref["status"])
+    for i in range(qp.batch):
+        for key in ("x", "u"):
+            assert helpers.is_approx(out[key][i], ref[key][i], 1e-7), (key, i)
+    cnt = out["stat"][:, 1:9, 13]
+    assert np.all((cnt >= 1) & (cnt <= nmax)), cnt
+    assert np.all(out["stat"][:, 1:9, 14] >= 0) and np.all(np.isfinite(out["stat"][:, 1:9, 14:16]))
+    # the refinement moves the iterates at most at the linear solve's rounding level
+    for i in range(qp.batch):
+        assert helpers.is_approx(ref["u"][i], plain["u"][i], 1e-6), i
+
+
+@pytest.mark.parametrize("mode", ["Balance", "Robust"])
+def test_itref_converged_solutions(pkg, oracle, mode):
+    """At the default tolerances the refinement changes nothing measurable: box-u SRBD
+    and random box QPs converge to the oracle's solution (which refines the same way) and
+    to the Speed-mode solution."""
+    for qp, x0 in (pkg.srbd_model.generate_batch(24, N=20, seed=5, constraints="box_u"),
+                   helpers.random_constrained(16, 12, 12, 4, 0, 43, pkg.OcpQpBatch)):
+        st = dict(iter_max=40, mode=mode)
+        out = pkg.capi.solve(qp, x0, st, stats=True)
+        speed = pkg.capi.solve(qp, x0, dict(st, mode="Speed"))
+        ref = oracle.solve(qp, st, x0=x0)
+        assert np.all(out["status"] == 0) and np.all(ref["status"] == 0), (out["status"], ref["status"])
+        assert np.all(np.abs(out["iter"] - ref["iter"]) <= 1), (out["iter"], ref["iter"])
+        assert np.all(out["res"] <= 1e-8)
+        for i in range(qp.batch):
+            for key in ("x", "u"):
+                assert helpers.is_approx(out[key][i], ref[key][i], 1e-7), (key, i)
+                assert helpers.is_approx(out[key][i], speed[key][i], 1e-6), (key, i)
