@@ -127,7 +127,7 @@ enum { SRBD_QP_LAYOUT_QP_MAJOR = 0, SRBD_QP_LAYOUT_STAGE_MAJOR = 1 };
  * srbd_qp_default_settings() gives the same defaults.                     */
 typedef struct srbd_qp_settings {
   int mode;       /* HpipmMode: 0 SpeedAbs, 1 Speed, 2 Balance, 3 Robust; selects
-                  * itref_corr_max 0 / 0 / 2 / 4 (boxes)      */
+                  * itref_corr_max 0 / 0 / 2 / 4             */
   int iter_max;
   double alpha_min;
   double mu0;

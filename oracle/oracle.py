@@ -90,9 +90,7 @@ def _settings(s: Optional[Dict], ng: int = 0) -> _Settings:
     if s:
         d.update({k: v for k, v in s.items() if k in d})
         if "mode" in s and "itref_corr_max" not in s:
-            # the HIP kernels refine box-constrained steps only: with general
-            # rows the checker runs the GPU's algorithm, without refinement
-            d["itref_corr_max"] = MODE_ITREF[s["mode"]] if ng == 0 else 0
+            d["itref_corr_max"] = MODE_ITREF[s["mode"]]
     return _Settings(**d)
 
 

@@ -13,7 +13,7 @@ constexpr real kThr0 = real(0.1);     // minimum initial slack (HPIPM init_var)
 
 // phase kernels (one launch each, per IPM iteration; see launch_ipm_box)
 constexpr int kPhInit = 0, kPhRB = 1, kPhF1 = 2, kPhB2 = 3, kPhF2 = 4, kPhOut = 5;
-// iterative refinement of the corrector step (boxes): IR = residual of the step's linear
+// iterative refinement of the corrector step: IR = residual of the step's linear
 // system + the correction's backward recursion, F3 = the correction's forward sweep
 constexpr int kPhIR = 6, kPhF3 = 7;
 // per-QP scalar state, kQsSize reals at the head of the QP's workspace
@@ -1319,7 +1319,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     return;
   }
   if constexpr (PH == kPhIR || PH == kPhF3) {
-    // =========== iterative refinement of the step (HPIPM itref_corr_max; boxes) ===========
+    // ============== iterative refinement of the step (HPIPM itref_corr_max) ==============
     // The step (du, dx, dpi and the bounds' dt, dlam) solves the Newton system only up to the
     // factorization's rounding.  IR (k = N..0) forms the linear residual of that system at the
     // step in its full form -- QP Hessian and multiplier steps, not the Gamma-reduced one, so
@@ -1334,7 +1334,6 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     // F3 (k = 0..N) forms the correction, adds it to the step, updates dt / dlam (linear in
     // the primal step: ddt = +-ddv, ddlam = -lam ddt / t) and redoes the step lengths.
     // (F2 advanced iter: the step's factorization has the parity of iter - 1.)
-    static_assert(GEN == 0, "iterative refinement: box constraints only");
     if (qs[kQsItDone] != real(0.0)) return;
     const int fpar = (iter - 1) & 1;
     real* const next = a.stat && lane == 0 ? a.stat + ((size_t)qp * a.stat_rows + iter) * kStatCols
@@ -1361,6 +1360,19 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         real ru = rgu + su.mu * bdu.dlu - su.ml * bdu.dll;
         real rx = rgx + sx.mu * bdx.dlu - sx.ml * bdx.dll - dpi_ld;
         real rb = rbk - dxn_ld;
+        if constexpr (GEN) {
+          // the rows' multiplier steps: + D'(dlam_u - dlam_l) on the u rows, C'(..) on x
+          for (int ch = 0; ch < c.nch; ++ch) {
+            const real* g = c.gs(k, ch);
+            const Side sg = c.side_g(k, ch, lane);
+            const BarStep d = load_gstep(g, li);
+            const real dl = lane < kMaxDim ? sg.mu * d.dlu - sg.ml * d.dll : real(0.0);
+            real Cc[12], Dc[12];
+            c.g_col(k, ch, col, Cc, Dc);
+            ru = dot_bcast(Dc, dl, ru);
+            if constexpr (GEN == 2) rx = dot_bcast(Cc, dl, rx);
+          }
+        }
         real Ac[12], Bc[12];
         if (k < N) {
           c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, Ac);
@@ -1459,6 +1471,17 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       real ap = real(1e30), ad = real(1e30);
       bool bad = false;
       real dxc = real(0.0);  // correction of dx_0: 0 (x0 fixed)
+      // dt / dlam are linear in the primal step: ddt = +-ddv, ddlam = -lam ddt / t
+      auto upd = [&](const Side& sd, const Bar& b, BarStep& d, real dv) {
+        if (sd.ml != real(0.0)) {
+          d.dtl += dv;
+          d.dll -= b.ll * dv / b.tl;
+        }
+        if (sd.mu != real(0.0)) {
+          d.dtu -= dv;
+          d.dlu += b.lu * dv / b.tu;
+        }
+      };
       for (int k = 0; k <= N; ++k) {
         real* stk = c.st(k);
         const real* rec = stk + fpar * kRecSize;
@@ -1485,22 +1508,30 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           dxn = real(0.0);
           dpcv = real(0.0);
         }
+        if constexpr (GEN) {
+          // the rows' steps: ddv = C ddx + D ddu
+          for (int ch = 0; ch < c.nch; ++ch) {
+            real* g = c.gs(k, ch);
+            real Cr[12], Dr[12];
+            c.g_row(k, ch, lane, Cr, Dr);
+            const real dv = dot_bcast(Dr, duc, GEN == 2 ? dot_bcast(Cr, dxc, real(0.0)) : real(0.0));
+            if (lane < kMaxDim) {
+              const Side sg = c.side_g(k, ch, lane);
+              const Bar bg = load_gbar(g, lane);
+              BarStep d = load_gstep(g, lane);
+              upd(sg, bg, d, dv);
+              bad |= huge(d.dtl) || huge(d.dtu) || huge(d.dll) || huge(d.dlu);
+              ratio(sg, bg, d, ap, ad);
+              store_gstep(g, lane, d);
+            }
+          }
+        }
         if (lane < kMaxDim) {
           const Side su = c.side_u(k, lane), sx = c.side_x(k, lane);
           const Bar bu = c.bar(stk, 0, lane), bx = c.bar(stk, 1, lane);
           BarStep nu_ = c.bstep(stk, 0, lane), nx_ = c.bstep(stk, 1, lane);
           const real du = stk[kStStep + lane] + duc, dx = stk[kStStep + 12 + lane] + dxc;
           const real dpi = k > 0 ? stk[kStStep + 24 + lane] + dpcv : real(0.0);
-          auto upd = [&](const Side& sd, const Bar& b, BarStep& d, real dv) {
-            if (sd.ml != real(0.0)) {
-              d.dtl += dv;
-              d.dll -= b.ll * dv / b.tl;
-            }
-            if (sd.mu != real(0.0)) {
-              d.dtu -= dv;
-              d.dlu += b.lu * dv / b.tu;
-            }
-          };
           upd(su, bu, nu_, k < N ? duc : real(0.0));
           upd(sx, bx, nx_, dxc);
           ratio(su, bu, nu_, ap, ad);
@@ -1954,14 +1985,12 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
     } else if (a.pred_corr) {
       hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhB2, kPhF2, SQRT>), grid, block, 0, stream, b);
     }
-    // HPIPM's iterative refinement of the corrector step (Balance / Robust; boxes only): at
+    // HPIPM's iterative refinement of the corrector step (Balance / Robust): at
     // most itref_corr_max corrections, each after a check of the step's linear residual; a
     // QP whose check passed returns at the top of the later ones
-    if constexpr (GEN == 0) {
-      if (a.pred_corr)
-        for (int r = 0; r < a.itref_corr_max; ++r)
-          hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhIR, kPhF3, SQRT>), grid, block, 0, stream, b);
-    }
+    if (a.pred_corr)
+      for (int r = 0; r < a.itref_corr_max; ++r)
+        hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhIR, kPhF3, SQRT>), grid, block, 0, stream, b);
     if (ctl && it >= 1) {
       hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(a.ctl_ev[(it - 1) & 1]));
       if (e != hipSuccess) return e;

@@ -47,7 +47,7 @@ struct ProblemArgsT {
   int ric_alg;    // 0: classical Riccati, else the square-root recursion (riccati.h)
   int stat_rows;  // rows per QP of `stat` (the caller's iter_max + 2)
   // iterative refinement of the corrector step (HPIPM itref_corr_max; the C-ABI derives it
-  // from settings.mode: Balance 2, Robust 4, else 0).  Box constraints only (ng = 0).
+  // from settings.mode: Balance 2, Robust 4, else 0).
   int itref_corr_max;
   // warm_start 2 only (internal: the fp64 continuation of srbd_qp_settings.f64_rescue):
   // per QP and stage the barrier state [kStLam block 96][nch chunks x 48], see ipm_box.hip

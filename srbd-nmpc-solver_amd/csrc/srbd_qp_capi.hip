@@ -349,7 +349,7 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   a.split_step = st->split_step;
   a.ric_alg = st->ric_alg != 0;  // HPIPM: any nonzero square_root_alg
   // HPIPM's mode-dependent iterative refinement of the corrector (d_ocp_qp_ipm_arg_set_default:
-  // itref_corr_max 2 in Balance, 4 in Robust, 0 in Speed / SpeedAbs); boxes only
+  // itref_corr_max 2 in Balance, 4 in Robust, 0 in Speed / SpeedAbs)
   a.itref_corr_max = st->mode == 2 ? 2 : st->mode == 3 ? 4 : 0;
   a.warm_start = st->warm_start;
   a.alpha_min = st->alpha_min;
