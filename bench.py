@@ -252,7 +252,13 @@ def main():
                          "rank) or gloo (host-staged gather; ranks may share a GPU, for tests)")
     ap.add_argument("--print-ranks", action="store_true",
                     help="print each rank's RANK / WORLD_SIZE / MASTER_* and exit (launcher check)")
+    ap.add_argument("--mode", choices=("SpeedAbs", "Speed", "Balance", "Robust"), default=None,
+                    help="IPM workloads: settings.mode instead of the NMPC's Speed (Balance / Robust "
+                         "add HPIPM's iterative refinement of the corrector, DESIGN.md 4.8)")
     args = ap.parse_args()
+    if args.mode:
+        NMPC_SETTINGS["mode"] = args.mode
+        F32_SETTINGS["mode"] = args.mode
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
 
