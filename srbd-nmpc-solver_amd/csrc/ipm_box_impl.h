@@ -13,9 +13,9 @@ constexpr real kThr0 = real(0.1);     // minimum initial slack (HPIPM init_var)
 
 // phase kernels (one launch each, per IPM iteration; see launch_ipm_box)
 constexpr int kPhInit = 0, kPhRB = 1, kPhF1 = 2, kPhB2 = 3, kPhF2 = 4, kPhOut = 5;
-// iterative refinement of the corrector step: IR = residual of the step's linear
-// system + the correction's backward recursion, F3 = the correction's forward sweep
-constexpr int kPhIR = 6, kPhF3 = 7;
+// iterative refinement of the corrector step: IR = residual of the step's linear system
+// and the check, IS = the correction's backward recursion, F3 = its forward sweep
+constexpr int kPhIR = 6, kPhF3 = 7, kPhIS = 8;
 // per-QP scalar state, kQsSize reals at the head of the QP's workspace
 constexpr int kQsAlphaP = 0, kQsAlphaD = 1, kQsLastAmin = 2, kQsMu = 3, kQsMuSum = 4,
               kQsSigmaMu = 5, kQsStatus = 6, kQsIter = 7, kQsNc = 8, kQsResStat = 9,
@@ -1318,34 +1318,35 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 
     return;
   }
-  if constexpr (PH == kPhIR || PH == kPhF3) {
+  if constexpr (PH == kPhIR || PH == kPhIS || PH == kPhF3) {
     // ============== iterative refinement of the step (HPIPM itref_corr_max) ==============
     // The step (du, dx, dpi and the bounds' dt, dlam) solves the Newton system only up to the
     // factorization's rounding.  IR (k = N..0) forms the linear residual of that system at the
     // step in its full form -- QP Hessian and multiplier steps, not the Gamma-reduced one, so
     // no right-hand side of the corrector is needed again (the dt / dlam rows hold exactly by
     // construction, bar_step) --
-    //   r_u = res_g,u + R du + S dx + B'dpi_{k+1} - dlam_l + dlam_u
-    //   r_x = res_g,x + S'du + Q dx + A'dpi_{k+1} - dpi_k - dlam_l + dlam_u   (k >= 1)
+    //   r_u = res_g,u + R du + S dx + B'dpi_{k+1} + D'(dlam_u - dlam_l)   (boxes: D = I)
+    //   r_x = res_g,x + S'du + Q dx + A'dpi_{k+1} - dpi_k + C'(dlam_u - dlam_l)   (k >= 1)
     //   r_b = res_b + A dx + B du - dx_{k+1}
-    // and runs the corrector's backward recursion with (r_u, r_x, r_b) as its right-hand side
-    // (same factors: the record of this iteration's RB).  Its infinity norms decide, as in
-    // HPIPM: below the tolerances (or 1e-3 of the first check's) the refinement stops, else
-    // F3 (k = 0..N) forms the correction, adds it to the step, updates dt / dlam (linear in
-    // the primal step: ddt = +-ddv, ddlam = -lam ddt / t) and redoes the step lengths.
+    // Its infinity norms decide, as in HPIPM: below the tolerances (or 1e-3 of the first
+    // check's) the refinement stops.  Otherwise IS (k = N..0) runs the corrector's backward
+    // recursion with (r_u, r_x, r_b) as its right-hand side (same factors: the record of this
+    // iteration's RB) and F3 (k = 0..N) forms the correction, adds it to the step, updates
+    // dt / dlam (linear in the primal step: ddt = +-ddv, ddlam = -lam ddt / t) and redoes the
+    // step lengths.  (A check that passes costs IR alone: IS and F3 return at the top.)
     // (F2 advanced iter: the step's factorization has the parity of iter - 1.)
     if (qs[kQsItDone] != real(0.0)) return;
     const int fpar = (iter - 1) & 1;
     real* const next = a.stat && lane == 0 ? a.stat + ((size_t)qp * a.stat_rows + iter) * kStatCols
                                            : nullptr;
     if constexpr (PH == kPhIR) {
-      real* const ldsA = group_lds_blocks<GEN>();
-      real* const ldsB = ldsA + 144;
-      real* const ldsS = ldsA + 288;
-      real ng = real(0.0), nb = real(0.0), pnext = real(0.0);
+      // one 12 x 12 LDS block per QP group (A, B, S in turn): 18 KB per workgroup, so the
+      // sweep runs at its register occupancy (RB's three blocks would cap it at 2 waves/SIMD)
+      __shared__ real ir_lds[(256 / kGroup) * 144];
+      real* const blk = ir_lds + (threadIdx.x / kGroup) * 144;
+      real ng = real(0.0), nb = real(0.0);
       for (int k = N; k >= 0; --k) {
         real* stk = c.st(k);
-        real* rec = stk + fpar * kRecSize;
         const real* stn = c.st(k < N ? k + 1 : k);
         // the stage's element-owned loads first (valid addresses on every lane, masked after)
         const real du_ld = stk[kStStep + li], dx_ld = stk[kStStep + 12 + li], dpi_ld = stk[kStStep + 24 + li];
@@ -1382,16 +1383,20 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           rx = dot_bcast(Ac, dpinv, rx);  // + A'dpi_{k+1}
           ru = dot_bcast(Bc, dpinv, ru);  // + B'dpi_{k+1}
           rx = dot_bcast(Sc, duv, rx);    // + S'du
-          lds_put_col(ldsA, lane, Ac);
-          lds_put_col(ldsB, lane, Bc);
-          lds_put_col(ldsS, lane, Sc);
-          lds_wave_fence();
           real M[12];
-          lds_get_row(ldsA, li, M);
+          lds_put_col(blk, lane, Ac);
+          lds_wave_fence();
+          lds_get_row(blk, li, M);
           rb = dot_bcast(M, dxv, rb);  // + A dx
-          lds_get_row(ldsB, li, M);
+          lds_wave_fence();
+          lds_put_col(blk, lane, Bc);
+          lds_wave_fence();
+          lds_get_row(blk, li, M);
           rb = dot_bcast(M, duv, rb);  // + B du
-          lds_get_row(ldsS, li, M);
+          lds_wave_fence();
+          lds_put_col(blk, lane, Sc);
+          lds_wave_fence();
+          lds_get_row(blk, li, M);
           ru = dot_bcast(M, dxv, ru);  // + S dx
           lds_wave_fence();
           real Rc[12];
@@ -1408,16 +1413,52 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         if (!(el && xel && k < N)) rb = real(0.0);
         ng = fmax(ng, fmax(nabs(ru), nabs(rx)));
         nb = fmax(nb, nabs(rb));
-        // the correction's b~ for F3, in the other parity's record slot (the previous
-        // factorization's, dead until the next RB overwrites it)
-        if (el) stk[(fpar ^ 1) * kRecSize + lane] = rb;
+        // the residual waits for the correction's recursion (kPhIS) and F3 in the other
+        // parity's record slot (the previous factorization's, dead until the next RB
+        // overwrites it): r_b, r_u, r_x
+        if (el) {
+          real* slot = stk + (fpar ^ 1) * kRecSize;
+          slot[lane] = rb;
+          slot[12 + lane] = ru;
+          slot[24 + lane] = rx;
+        }
+      }
+      const real nga = gmax(ng), nba = gmax(nb);
+      const int cnt = (int)qs[kQsItCnt];
+      const real n0g = cnt == 0 ? nga : qs[kQsItN0g], n0b = cnt == 0 ? nba : qs[kQsItN0b];
+      const bool small = (nga < a.tol_stat || nga < real(1e-3) * n0g) &&
+                         (nba < a.tol_eq || nba < real(1e-3) * n0b);
+      if (lane == 0) {
+        if (cnt == 0) {
+          qs[kQsItN0g] = nga;
+          qs[kQsItN0b] = nba;
+        }
+        if (small) qs[kQsItDone] = real(1.0);
+      }
+      if (next) {  // HPIPM stat: lin_res_stat, lin_res_eq (the dt / dlam rows are exact)
+        next[14] = nga;
+        next[15] = nba;
+      }
+      return;
+    } else if constexpr (PH == kPhIS) {
+      // ---- IS: the correction's backward recursion (B2's, right-hand side r_u, r_x, r_b) ----
+      real pnext = real(0.0);
+      for (int k = N; k >= 0; --k) {
+        real* stk = c.st(k);
+        real* rec = stk + fpar * kRecSize;
+        const real* slot = stk + (fpar ^ 1) * kRecSize;
+        const bool el = lane < kMaxDim;
+        const real rb = el ? slot[li] : real(0.0), ru = el ? slot[12 + li] : real(0.0);
+        const real rx = el ? slot[24 + li] : real(0.0);
         if (k == N) {
           pnext = rx;  // p_N = q~_N (the terminal P_N carries Q_N + Gamma)
           if (el) rec[kRecPv + lane] = pnext;
           continue;
         }
-        // the corrector's recursion (B2) with (r_u, r_x, r_b) as its right-hand side
-        const real* recn = stn + fpar * kRecSize;
+        real Ac[12], Bc[12];
+        c.col(c.A() + (size_t)k * c.nxx(), nx, col, xel, Ac);
+        c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, Bc);
+        const real* recn = c.st(k + 1) + fpar * kRecSize;
         const real w = rec_P_mul(recn, rb, pnext);
         real g = ru, f = rx;
         dot_bcast2(Bc, Ac, w, g, f);
@@ -1448,22 +1489,6 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           rec[kRecPv + lane] = xel ? pv : real(0.0);
         }
         pnext = xel ? pv : real(0.0);
-      }
-      const real nga = gmax(ng), nba = gmax(nb);
-      const int cnt = (int)qs[kQsItCnt];
-      const real n0g = cnt == 0 ? nga : qs[kQsItN0g], n0b = cnt == 0 ? nba : qs[kQsItN0b];
-      const bool small = (nga < a.tol_stat || nga < real(1e-3) * n0g) &&
-                         (nba < a.tol_eq || nba < real(1e-3) * n0b);
-      if (lane == 0) {
-        if (cnt == 0) {
-          qs[kQsItN0g] = nga;
-          qs[kQsItN0b] = nba;
-        }
-        if (small) qs[kQsItDone] = real(1.0);
-      }
-      if (next) {  // HPIPM stat: lin_res_stat, lin_res_eq (the dt / dlam rows are exact)
-        next[14] = nga;
-        next[15] = nba;
       }
       return;
     } else {
@@ -1989,8 +2014,10 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
     // most itref_corr_max corrections, each after a check of the step's linear residual; a
     // QP whose check passed returns at the top of the later ones
     if (a.pred_corr)
-      for (int r = 0; r < a.itref_corr_max; ++r)
-        hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhIR, kPhF3, SQRT>), grid, block, 0, stream, b);
+      for (int r = 0; r < a.itref_corr_max; ++r) {
+        hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhIR, SQRT>), grid, block, 0, stream, b);
+        hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhIS, kPhF3, SQRT>), grid, block, 0, stream, b);
+      }
     if (ctl && it >= 1) {
       hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(a.ctl_ev[(it - 1) & 1]));
       if (e != hipSuccess) return e;
