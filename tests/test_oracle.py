@@ -112,3 +112,24 @@ def test_fast_unconstr_port_matches_oracle(pkg, oracle, threads):
     out, _ = oracle.fast_unconstr_batch(qp, x0, threads=threads)
     for key in ("x", "u", "pi"):
         assert helpers.is_approx(out[key], ref[key], 1e-10), key
+
+
+@pytest.mark.parametrize("ng", [0, 14])
+def test_itref_oracle(OcpQpBatch, oracle, ng):
+    """The oracle's restatement of HPIPM's iterative refinement of the corrector (mode
+    Balance: 2 corrections at most, Robust: 4).  At the default tolerances
+    the refined solve lands on the unrefined one; with tolerances nothing reaches, every
+    iteration refines and the iterates move only at the linear solve's rounding level."""
+    qp, x0 = helpers.random_constrained(4, 10, 12, 4, ng, 45 + ng, OcpQpBatch)
+    speed = oracle.solve(qp, dict(iter_max=40, mode="Speed"), x0=x0)
+    for mode in ("Balance", "Robust"):
+        out = oracle.solve(qp, dict(iter_max=40, mode=mode), x0=x0)
+        assert np.all(out["status"] == 0) and np.all(speed["status"] == 0)
+        assert np.all(out["res"] <= 1e-8)
+        for i in range(qp.batch):
+            assert helpers.is_approx(out["u"][i], speed["u"][i], 1e-7), (mode, i)
+    tiny = dict(iter_max=6, tol_stat=1e-30, tol_eq=1e-30, tol_ineq=1e-30, tol_comp=1e-30)
+    ref = oracle.solve(qp, dict(tiny, itref_corr_max=2), x0=x0)
+    plain = oracle.solve(qp, dict(tiny, itref_corr_max=0), x0=x0)
+    for i in range(qp.batch):
+        assert helpers.is_approx(ref["u"][i], plain["u"][i], 1e-6), i
