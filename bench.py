@@ -417,6 +417,8 @@ def main():
                                                           f32_iters=MIXED_F32_ITERS)
         secondary["cone_n40_f64_mixed"] = secondary_workload(pkg, capi, "cone_n40_f64", device, args.seed,
                                                              f32_iters=MIXED_F32_ITERS_CONE)
+        secondary["box_u_n20_balance"] = secondary_workload(pkg, capi, "box_u_n20", device, args.seed,
+                                                            mode="Balance")
         secondary["cone_n40_f32_f64_rescue"] = secondary_workload(pkg, capi, "cone_n40_f32", device,
                                                                   args.seed, rescue=RESCUE_CAP)
         secondary["nmpc_step_config1"] = nmpc_config1(pkg, capi, device, args.seed,
@@ -479,7 +481,8 @@ def main():
         dist.destroy_process_group()
 
 
-def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=0, f32_iters=0):
+def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=0, f32_iters=0,
+                       mode=None):
     """One IPM workload (its own handle and synthetic shard) timed the same way as
     the main line: kernel time from HIP events on the handle's stream, wall time
     around `steps` solves.  Reported beside `value`, never as it.  rescue = n > 0 runs
@@ -487,7 +490,8 @@ def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=
     iterations, the QPs it leaves unsolved solved again in fp64).  f32_iters = n > 0
     runs an fp64 workload as the mixed-precision IPM (settings.f32_iters: n fp32
     iterations, then fp64 to the fp64 tolerances) and reports its distance to the
-    plain fp64 solve of the same shard."""
+    plain fp64 solve of the same shard.  mode = "Balance" / "Robust" runs it with
+    HPIPM's iterative refinement of the corrector."""
     import torch
     N, constraints, batch, desc = WORKLOADS[name][:4]
     dtype = WORKLOADS[name][4] if len(WORKLOADS[name]) > 4 else "f64"
@@ -507,6 +511,10 @@ def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=
     settings = capi.settings_struct(F32_SETTINGS if dtype == "f32" else NMPC_SETTINGS)
     settings.f64_rescue = int(rescue)  # 0: off
     settings.f32_iters = int(f32_iters)  # 0: off
+    if mode:
+        settings.mode = capi.MODES[mode]
+        desc += (f"; settings.mode = {mode}: HPIPM's iterative refinement of the corrector step "
+                 "(the mode of the reference's own test, test/ocp_qp_ipm_solver.cpp:243)")
     ext = torch.cuda.ExternalStream(h.stream(), device=device)
     for _ in range(warmup):
         h.solve_device(batch, settings, data, sol)
