@@ -446,7 +446,18 @@ __device__ __forceinline__ int group_qp(const ProblemArgsT<real>& a) {
 
 template <bool FULL, int GEN, int PH, bool SQRT = false>
 __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
-  const int qp = group_qp(a);
+  // the refinement check runs stage-parallel: group g on QP slot g / (N + 1), stage
+  // g % (N + 1) (its rows are independent across stages); every other phase: one QP per group
+  int kst = 0;
+  int qp;
+  if constexpr (PH == kPhIR) {
+    const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4);
+    const int slot = g / (a.N + 1);
+    kst = g - slot * (a.N + 1);
+    qp = a.qp_list ? (slot < a.qp_list[a.batch] ? a.qp_list[slot] : -1) : (slot < a.batch ? slot : -1);
+  } else {
+    qp = group_qp(a);
+  }
   const int lane = threadIdx.x & (kGroup - 1);
   if (qp < 0) return;
   const int N = a.N;
@@ -1321,7 +1332,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   if constexpr (PH == kPhIR || PH == kPhIS || PH == kPhF3) {
     // ============== iterative refinement of the step (HPIPM itref_corr_max) ==============
     // The step (du, dx, dpi and the bounds' dt, dlam) solves the Newton system only up to the
-    // factorization's rounding.  IR (k = N..0) forms the linear residual of that system at the
+    // factorization's rounding.  IR (one group per stage) forms the linear residual of that system at the
     // step in its full form -- QP Hessian and multiplier steps, not the Gamma-reduced one, so
     // no right-hand side of the corrector is needed again (the dt / dlam rows hold exactly by
     // construction, bar_step) --
@@ -1345,7 +1356,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       __shared__ real ir_lds[(256 / kGroup) * 144];
       real* const blk = ir_lds + (threadIdx.x / kGroup) * 144;
       real ng = real(0.0), nb = real(0.0);
-      for (int k = N; k >= 0; --k) {
+      {
+        const int k = kst;
         real* stk = c.st(k);
         const real* stn = c.st(k < N ? k + 1 : k);
         // the stage's element-owned loads first (valid addresses on every lane, masked after)
@@ -1416,11 +1428,30 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         // the residual waits for the correction's recursion (kPhIS) and F3 in the other
         // parity's record slot (the previous factorization's, dead until the next RB
         // overwrites it): r_b, r_u, r_x
+        // the stage's norms (slot[36], slot[37]) wait for IS, which decides
+        const real ngk = gmax(ng), nbk = gmax(nb);
+        real* slot = stk + (fpar ^ 1) * kRecSize;
         if (el) {
-          real* slot = stk + (fpar ^ 1) * kRecSize;
           slot[lane] = rb;
           slot[12 + lane] = ru;
           slot[24 + lane] = rx;
+        }
+        if (lane == 0) {
+          slot[36] = ngk;
+          slot[37] = nbk;
+        }
+      }
+      return;
+    } else if constexpr (PH == kPhIS) {
+      // ---- the check's verdict: the stages' norms (lane l: stages l, l + 16, ...) ----
+      real ng = real(0.0), nb = real(0.0);
+      for (int k0 = 0; k0 <= N; k0 += kGroup) {
+        const int k = k0 + lane;
+        const real* slot = c.st(k <= N ? k : N) + (fpar ^ 1) * kRecSize;
+        const real g1 = slot[36], b1 = slot[37];
+        if (k <= N) {
+          ng = fmax(ng, g1);
+          nb = fmax(nb, b1);
         }
       }
       const real nga = gmax(ng), nba = gmax(nb);
@@ -1439,8 +1470,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         next[14] = nga;
         next[15] = nba;
       }
-      return;
-    } else if constexpr (PH == kPhIS) {
+      if (small) return;  // (F3 returns on the flag)
       // ---- IS: the correction's backward recursion (B2's, right-hand side r_u, r_x, r_b) ----
       real pnext = real(0.0);
       for (int k = N; k >= 0; --k) {
@@ -2015,7 +2045,8 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
     // QP whose check passed returns at the top of the later ones
     if (a.pred_corr)
       for (int r = 0; r < a.itref_corr_max; ++r) {
-        hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhIR, SQRT>), grid, block, 0, stream, b);
+        hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhIR, SQRT>), dim3(grid.x * (unsigned)(a.N + 1)),
+                           block, 0, stream, b);
         hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhIS, kPhF3, SQRT>), grid, block, 0, stream, b);
       }
     if (ctl && it >= 1) {
