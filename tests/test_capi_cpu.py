@@ -105,3 +105,17 @@ def test_no_cpu_fallback(pkg):
     qp, x0 = helpers.random_unconstrained(2, 5, 4, 3, 0, pkg.OcpQpBatch)
     with pytest.raises(pkg.capi.SrbdQpError):
         pkg.capi.solve(qp, x0)
+
+
+def test_mode_selects_the_same_refinement_in_library_and_checker(pkg, oracle):
+    """settings.mode follows hpipm::HpipmMode (SpeedAbs, Speed, Balance, Robust =
+    0..3, ocp_qp_ipm_solver_settings.hpp) and selects HPIPM's itref_corr_max 0 / 0 / 2 / 4
+    in the HIP library (srbd_qp_capi.hip) and in the CPU checker alike."""
+    assert pkg.capi.MODES == {"SpeedAbs": 0, "Speed": 1, "Balance": 2, "Robust": 3}
+    src = (helpers.REPO / "srbd-nmpc-solver_amd" / "csrc" / "srbd_qp_capi.hip").read_text()
+    assert "a.itref_corr_max = st->mode == 2 ? 2 : st->mode == 3 ? 4 : 0;" in src
+    for name, code in pkg.capi.MODES.items():
+        want = {0: 0, 1: 0, 2: 2, 3: 4}[code]
+        assert oracle.MODE_ITREF[name] == want and oracle.MODE_ITREF[code] == want
+        assert oracle._settings({"mode": name}).itref_corr_max == want
+    assert oracle._settings({"mode": "Balance", "itref_corr_max": 0}).itref_corr_max == 0
