@@ -8,6 +8,9 @@ namespace SRBD_NS {
 
 using real = SRBD_REAL;
 
+#ifndef SRBD_ITREF_CHECK_ONLY
+#define SRBD_ITREF_CHECK_ONLY 0
+#endif
 
 constexpr real kThr0 = real(0.1);     // minimum initial slack (HPIPM init_var)
 
@@ -438,10 +441,17 @@ __device__ __forceinline__ void gather12(real v, real (&out)[12]) {
 // register P_k, riccati.h SYMP).
 // QP of this thread's group: the grid position, or (ProblemArgsT::qp_list) the position's
 // entry of the active-QP list; -1 past the batch / the list
-__device__ __forceinline__ int group_qp(const ProblemArgsT<real>& a) {
-  const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4);
-  if (a.qp_list) return g < a.qp_list[a.batch] ? a.qp_list[g] : -1;
+// (the list is on once a compaction kernel of this solve built it: ctl[kCtlListOn])
+__device__ __forceinline__ const int* active_list(const ProblemArgsT<real>& a) {
+  return a.qp_list && __atomic_load_n(a.ctl + kCtlListOn, __ATOMIC_RELAXED) ? a.qp_list : nullptr;
+}
+__device__ __forceinline__ int slot_qp(const ProblemArgsT<real>& a, int g) {
+  const int* l = active_list(a);
+  if (l) return g < l[a.batch] ? l[g] : -1;
   return g < a.batch ? g : -1;
+}
+__device__ __forceinline__ int group_qp(const ProblemArgsT<real>& a) {
+  return slot_qp(a, (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4));
 }
 
 template <bool FULL, int GEN, int PH, bool SQRT = false>
@@ -454,7 +464,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4);
     const int slot = g / (a.N + 1);
     kst = g - slot * (a.N + 1);
-    qp = a.qp_list ? (slot < a.qp_list[a.batch] ? a.qp_list[slot] : -1) : (slot < a.batch ? slot : -1);
+    qp = slot_qp(a, slot);
   } else {
     qp = group_qp(a);
   }
@@ -1457,8 +1467,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       const real nga = gmax(ng), nba = gmax(nb);
       const int cnt = (int)qs[kQsItCnt];
       const real n0g = cnt == 0 ? nga : qs[kQsItN0g], n0b = cnt == 0 ? nba : qs[kQsItN0b];
-      const bool small = (nga < a.tol_stat || nga < real(1e-3) * n0g) &&
-                         (nba < a.tol_eq || nba < real(1e-3) * n0b);
+      // (diagnostic builds, -DSRBD_ITREF_CHECK_ONLY=1: the check records the unrefined step's
+      // linear residual in the stat table and never corrects -- Speed's iterates)
+      const bool small = SRBD_ITREF_CHECK_ONLY ||
+                         ((nga < a.tol_stat || nga < real(1e-3) * n0g) &&
+                          (nba < a.tol_eq || nba < real(1e-3) * n0b));
       if (lane == 0) {
         if (cnt == 0) {
           qs[kQsItN0g] = nga;
@@ -1914,14 +1927,9 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 template <int GEN>
 constexpr int kIpmMinBlocks = sizeof(real) == 4 && GEN < 2 ? 3 : 2;
 
-// the host verdict word of an RB sweep: the solve's tag (16 bits) and its live-workgroup count
-__host__ __device__ constexpr int ctl_word(int tag, int live) {
-  return ((tag & 0x7fff) << 16) | (live < 0xffff ? live : 0xffff);
-}
-
 // Live-QP report after an RB sweep (ProblemArgsT::ctl): one count per workgroup with a QP
-// still running, and the workgroup that finishes last hands the verdict to the host.  Every
-// thread of the workgroup reaches this (the phase functions return, the kernels do not).
+// still running; the workgroup that finishes last marks the solve done when none is left.
+// Every thread of the workgroup reaches this (the phase functions return, the kernels do not).
 __device__ __forceinline__ void report_running(const ProblemArgsT<real>& a) {
   if (!a.ctl) return;
   const int qp = group_qp(a);
@@ -1935,20 +1943,27 @@ __device__ __forceinline__ void report_running(const ProblemArgsT<real>& a) {
     __threadfence();
     if (atomicAdd(cnt + 1, 1) == (int)gridDim.x - 1) {
       __threadfence();
-      const int live = atomicAdd(cnt, 0);  // workgroups with a QP still running
-      __hip_atomic_store(a.ctl_host + a.launch_it, ctl_word(a.ctl_tag, live), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+      if (atomicAdd(cnt, 0) == 0)  // no workgroup has a QP still running
+        __hip_atomic_store(a.ctl + kCtlDone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
 
+// A sweep launched after every QP of the solve has exited returns at once (a uniform load of
+// one control word; the launch costs its dispatch only).
+__device__ __forceinline__ bool solve_done(const ProblemArgsT<real>& a) {
+  return a.ctl && __atomic_load_n(a.ctl + kCtlDone, __ATOMIC_RELAXED) != 0;
+}
+
 template <bool FULL, int GEN, int PH, bool SQRT = false>
 __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase_kernel(ProblemArgsT<real> a) {
-  if constexpr (PH == kPhInit) {  // this solve's live-QP counters start at 0
+  if constexpr (PH == kPhInit) {  // this solve's live-QP counters and control words start at 0
     if (a.ctl)
-      for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * a.ctl_cap; i += gridDim.x * blockDim.x)
-        a.ctl[i] = 0;
+      for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < kCtlInts; i += gridDim.x * blockDim.x)
+        a.ctl[i] = i == kCtlCur ? (int)gridDim.x : 0;  // cur: the full grid
   }
+  if constexpr (PH != kPhInit && PH != kPhOut)
+    if (solve_done(a)) return;
   ipm_phase<FULL, GEN, PH, SQRT>(a);
   if constexpr (PH == kPhRB) report_running(a);
 }
@@ -1960,18 +1975,35 @@ __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase_
 // visible after the workgroup-scope fence).
 template <bool FULL, int GEN, int PH1, int PH2, bool SQRT = false>
 __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase2_kernel(ProblemArgsT<real> a) {
+  if (solve_done(a)) return;
   ipm_phase<FULL, GEN, PH1, SQRT>(a);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   ipm_phase<FULL, GEN, PH2, SQRT>(a);
   if constexpr (PH1 == kPhRB) report_running(a);
 }
 
-// The active-QP list: every QP whose status is still "running", in no particular order (a
-// QP's arithmetic does not depend on its place in the grid), the count at buf[batch].  One
-// atomic add per wave.  buf[batch] must be 0 on entry (zero_count_kernel).
-__global__ void __launch_bounds__(256) zero_count_kernel(int* buf, int batch) { buf[batch] = 0; }
+// Active-QP compaction, decided on the device after the RB sweep of iteration `it`: when the
+// workgroups with a live QP are at most 3/4 of the workgroups the current grid (or list) keeps
+// busy, the list is rebuilt and the later sweeps run on it.  compact_decide_kernel (one
+// thread) decides and clears the list's count; compact_running_kernel then lists every QP
+// whose status is still "running", in no particular order (a QP's arithmetic does not depend
+// on its place in the grid), the count at buf[batch], one atomic add per wave.
+__global__ void __launch_bounds__(64) compact_decide_kernel(int* __restrict__ ctl, int it, int* __restrict__ buf,
+                                                           int batch) {
+  if (threadIdx.x != 0) return;
+  const int live = ctl[2 * it], cur = ctl[kCtlCur];
+  const bool rebuild = ctl[kCtlDone] == 0 && live > 0 && 4 * (long long)live <= 3 * (long long)cur;
+  ctl[kCtlRebuild] = rebuild;
+  if (rebuild) {
+    buf[batch] = 0;
+    ctl[kCtlListOn] = 1;
+    ctl[kCtlCur] = live;
+  }
+}
 __global__ void __launch_bounds__(256) compact_running_kernel(const real* __restrict__ ws, size_t ws_qp,
-                                                              int batch, int* __restrict__ buf) {
+                                                              int batch, int* __restrict__ buf,
+                                                              const int* __restrict__ ctl) {
+  if (ctl[kCtlRebuild] == 0) return;
   const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   const bool run = q < batch && ws[(size_t)q * ws_qp + kQsStatus] < real(0.0);
   const unsigned long long m = __ballot(run);
@@ -1983,6 +2015,7 @@ __global__ void __launch_bounds__(256) compact_running_kernel(const real* __rest
 }
 
 // diagnostic builds (-DSRBD_IPM_SPLIT=1, profiling only): every sweep its own launch
+// (SRBD_ITREF_CHECK_ONLY: see kPhIS)
 #ifndef SRBD_IPM_SPLIT
 #define SRBD_IPM_SPLIT 0
 #endif
@@ -1993,28 +2026,28 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
   const int threads = 256;
   const long long lanes = (long long)a.batch * kGroup;
   const dim3 full_grid((unsigned)((lanes + threads - 1) / threads)), block(threads);
-  dim3 grid = full_grid;
-  // Host-driven iteration: each sweep is its own launch, so every kernel gets
-  // the registers (and occupancy) of its own phase; QPs that have exited return
-  // at the top of every later launch.  iter_max + 1 factorization sweeps at
-  // most: the last one always decides (converged or MaxIterReached).
-  // Live-QP control (ProblemArgsT::ctl): the host runs one iteration ahead of the verdict
-  // of RB(it - 1) and stops launching once it says every QP has exited, so a solve costs
-  // the launches of the iterations its slowest QP takes (+ one), not 2 iter_max + 3.
-  const bool ctl = a.ctl && a.ctl_host && a.ctl_ev[0] && a.ctl_ev[1] && a.iter_max < a.ctl_cap;
+  const dim3 grid = full_grid;
+  // Each sweep is its own launch, so every kernel gets the registers (and occupancy) of its
+  // own phase; QPs that have exited return at the top of every later launch.  iter_max + 1
+  // factorization sweeps at most: the last one always decides (converged or MaxIterReached).
+  // The whole sequence is enqueued at once and the host never waits (the call is
+  // asynchronous on `stream`): the stop decision lives on the device (ProblemArgsT::ctl):
+  // once an RB sweep leaves no QP running, every later sweep returns at its first
+  // instruction, so a finished solve's remaining launches cost their dispatch only.
+  const bool ctl = a.ctl && a.iter_max < a.ctl_cap;
 
   ProblemArgsT<real> b = a;
   if (!ctl) b.ctl = nullptr;
   b.launch_it = 0;
-  b.qp_list = nullptr;
+  // Active-QP compaction (compact_decide_kernel): once the workgroups with a live QP are at
+  // most 3/4 of the ones the grid keeps busy, the sweeps run on a list of the running QPs
+  // (the grid keeps its size: groups past the list's count return at the top).  A wave then
+  // carries four live QPs instead of the one or two a thinned-out batch leaves it.  Only for
+  // grids large enough to thin out (>= 64 workgroups, 1024 QPs); smaller solves skip the
+  // two launches per iteration.
+  const bool compact = ctl && a.qp_buf && full_grid.x >= 64;
+  b.qp_list = compact ? a.qp_buf : nullptr;
   hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhInit>), grid, block, 0, stream, b);
-  // Active-QP compaction: once the verdict one iteration back says the workgroups with a live
-  // QP are at most 3/4 of the grid, the next sweeps run on a list of the running QPs (built
-  // after the last enqueued sweep, so it is exact for them; QPs exiting later return at the
-  // top as before) on a grid of (live workgroups of the verdict) x 16 QPs, an upper bound.
-  // A wave then carries four live QPs instead of the one or two a thinned-out batch leaves it.
-  const bool compact = ctl && a.qp_buf;
-  long long grid_wg = full_grid.x;
   // (SQRT changes RB and how B2, F1, F2 and the outputs apply the record's P)
   for (int it = 0;; ++it) {
     b.launch_it = it;
@@ -2029,10 +2062,10 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
     } else {
       hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT>), grid, block, 0, stream, b);
     }
-    hipEvent_t ev = ctl ? reinterpret_cast<hipEvent_t>(a.ctl_ev[it & 1]) : nullptr;
-    if (ctl) {
-      hipError_t e = hipEventRecord(ev, stream);
-      if (e != hipSuccess) return e;
+    if (compact) {  // RB(it) has counted its live workgroups: compact for the rest of the solve?
+      hipLaunchKernelGGL(compact_decide_kernel, dim3(1), dim3(64), 0, stream, a.ctl, it, a.qp_buf, a.batch);
+      hipLaunchKernelGGL(compact_running_kernel, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, stream,
+                         a.ws, a.ws_qp, a.batch, a.qp_buf, a.ctl);
     }
     if (a.pred_corr && kIpmSplit) {
       hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhB2, SQRT>), grid, block, 0, stream, b);
@@ -2049,25 +2082,6 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
                            block, 0, stream, b);
         hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhIS, kPhF3, SQRT>), grid, block, 0, stream, b);
       }
-    if (ctl && it >= 1) {
-      hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(a.ctl_ev[(it - 1) & 1]));
-      if (e != hipSuccess) return e;
-      const int v = __atomic_load_n(a.ctl_host + (it - 1), __ATOMIC_ACQUIRE);
-      if ((v >> 16) == (a.ctl_tag & 0x7fff)) {  // this solve's RB(it - 1)
-        const long long live_wg = v & 0xffff;
-        if (live_wg == 0) break;  // no QP left running
-        if (compact && live_wg < 0xffff && 4 * live_wg <= 3 * grid_wg) {
-          long long qps = live_wg * 16;
-          if (qps > a.batch) qps = a.batch;
-          hipLaunchKernelGGL(zero_count_kernel, dim3(1), dim3(1), 0, stream, a.qp_buf, a.batch);
-          hipLaunchKernelGGL(compact_running_kernel, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, stream,
-                             a.ws, a.ws_qp, a.batch, a.qp_buf);
-          b.qp_list = a.qp_buf;
-          grid_wg = (qps * kGroup + threads - 1) / threads;
-          grid = dim3((unsigned)grid_wg);
-        }
-      }
-    }
   }
   b.qp_list = nullptr;  // outputs for every QP
   hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhOut, SQRT>), full_grid, block, 0, stream, b);

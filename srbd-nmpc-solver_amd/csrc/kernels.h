@@ -56,24 +56,29 @@ struct ProblemArgsT {
   // step without the sweep that would apply it; the step is handed to the fp64 continuation
   int skip_last_rb;
   T alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp;
-  // Live-QP control of the host-driven IPM loop (the handle's; ctl NULL = off).  After the
-  // RB sweep of launch iteration it, ctl[2 it] counts the workgroups with a QP still
-  // running and ctl[2 it + 1] the workgroups done; the last one writes ctl_host[it] =
-  // (tag, number of workgroups with a live QP) into pinned host memory (ipm_box_impl.h
-  // ctl_word).  The host waits on ctl_ev (one iteration behind the launches) and stops
-  // launching once every QP has exited.
+  // Live-QP control of the IPM launch sequence, decided on the device (the handle's; ctl
+  // NULL = off).  The host enqueues every launch of a solve up front and never waits.  After
+  // the RB sweep of launch iteration it, ctl[2 it] counts the workgroups with a QP still
+  // running and ctl[2 it + 1] the workgroups done; the last one sets ctl[kCtlDone] when no
+  // QP is left, and every later sweep of the solve returns at its first instruction.  The
+  // compaction kernels (ipm_box_impl.h) switch the sweeps to the active-QP list once the
+  // live workgroups are at most 3/4 of the grid the list last covered.
   int* ctl;
-  int* ctl_host;
-  int ctl_tag, ctl_cap;  // ctl_cap: iterations the arrays hold
-  int launch_it;         // set per launch
-  void* ctl_ev[2];       // hipEvent_t (host side only)
+  int ctl_cap;    // ctl_cap: iterations the counter arrays hold
+  int launch_it;  // set per launch
   // Active-QP list of the IPM sweeps (the handle's; capacity + 1 ints, the count last).
-  // qp_list set for a launch: QP group g of the grid works on QP qp_list[g] if g < count.
+  // qp_list set for a launch and ctl[kCtlListOn] set: QP group g of the grid works on QP
+  // qp_list[g] if g < count.
   int* qp_buf;
   const int* qp_list;
 };
-// iterations of the live-QP control arrays (iter_max >= this runs without the control)
+// iterations of the live-QP counter arrays (iter_max >= this runs without the control)
 constexpr int kCtlCap = 257;
+// control words after the per-iteration counters: every later sweep returns at once
+// (done), the sweeps read the active-QP list (list on), the compaction kernel of this
+// iteration rebuilds the list (rebuild), the workgroups the current grid covers (cur)
+constexpr int kCtlDone = 2 * kCtlCap, kCtlListOn = kCtlDone + 1, kCtlRebuild = kCtlDone + 2,
+              kCtlCur = kCtlDone + 3, kCtlInts = kCtlDone + 4;
 using ProblemArgs = ProblemArgsT<double>;
 
 constexpr int kStatCols = 18;  // HPIPM ws->stat row width

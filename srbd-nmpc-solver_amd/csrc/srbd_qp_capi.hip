@@ -65,12 +65,9 @@ struct srbd_qp_handle_s {
   // settings.f32_iters: fp32 copy of the data, fp32 iterate, barrier state (first use)
   void* mixed = nullptr;
   size_t mixed_bytes = 0;
-  // live-QP control of the IPM launch loop (ProblemArgsT::ctl): device counters, the pinned
-  // verdicts the last workgroup writes, two events, and the solve tag
+  // live-QP control of the IPM launch sequence (ProblemArgsT::ctl): device counters and
+  // control words, decided on the device (the host never waits on them)
   int* ctl = nullptr;
-  int* ctl_host = nullptr;
-  hipEvent_t ctl_ev[2] = {nullptr, nullptr};
-  int ctl_tag = 0;
   int* qp_buf = nullptr;  // active-QP list of the IPM sweeps: capacity + 1 ints
 };
 
@@ -190,9 +187,7 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srb
   if (e == hipSuccess) e = srbd::prepare_riccati_device();  // per-device kernel attributes
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&h->ws), h->ws_bytes);
   if (e == hipSuccess && constrained(*dims)) {
-    e = hipMalloc(reinterpret_cast<void**>(&h->ctl), sizeof(int) * 2 * srbd::kCtlCap);
-    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&h->ctl_host), sizeof(int) * srbd::kCtlCap);
-    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&h->ctl_ev[i], hipEventDisableTiming);
+    e = hipMalloc(reinterpret_cast<void**>(&h->ctl), sizeof(int) * srbd::kCtlInts);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&h->qp_buf), sizeof(int) * ((size_t)batch_capacity + 1));
   }
   hipSetDevice(prev);
@@ -224,9 +219,6 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   if (h->resc_count_host) hipHostFree(h->resc_count_host);
   if (h->ctl) hipFree(h->ctl);
   if (h->qp_buf) hipFree(h->qp_buf);
-  if (h->ctl_host) hipHostFree(h->ctl_host);
-  for (hipEvent_t ev : h->ctl_ev)
-    if (ev) hipEventDestroy(ev);
   if (h->stream) hipStreamDestroy(h->stream);
   hipSetDevice(prev);
   delete h;
@@ -239,7 +231,7 @@ size_t srbd_qp_workspace_bytes(srbd_qp_handle h) { return h ? h->ws_bytes : 0; }
 size_t srbd_qp_memory_bytes(srbd_qp_handle h) {
   if (!h) return 0;
   return h->ws_bytes + h->stage_bytes + h->pinned_bytes + h->pad_bytes + h->nmpc_bytes +
-         (h->ctl ? sizeof(int) * 3 * srbd::kCtlCap : 0) +
+         (h->ctl ? sizeof(int) * srbd::kCtlInts : 0) +
          (h->qp_buf ? sizeof(int) * ((size_t)h->capacity + 1) : 0) +
          h->resc_bytes + h->resc2_bytes + h->mixed_bytes +
          (h->resc_idx ? sizeof(int) * (2 * (size_t)h->capacity + 1) : 0);
@@ -360,11 +352,7 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   a.tol_comp = st->tol_comp;
   if (h->ctl) {
     a.ctl = h->ctl;
-    a.ctl_host = h->ctl_host;
     a.ctl_cap = srbd::kCtlCap;
-    a.ctl_tag = h->ctl_tag = (h->ctl_tag + 1) & 0x3fffffff;
-    a.ctl_ev[0] = h->ctl_ev[0];
-    a.ctl_ev[1] = h->ctl_ev[1];
     a.qp_buf = h->qp_buf;
   }
   hipError_t e = hipSuccess;
@@ -840,6 +828,9 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
     }
   }
   if (e != hipSuccess) {
+    // an earlier copy from the pinned buffer may still be queued: drain the stream before
+    // the next call may overwrite (or free) that buffer
+    hipStreamSynchronize(h->stream);
     hipSetDevice(prev);
     return fail(SRBD_QP_EDEVICE, std::string("host->device copy: ") + hipGetErrorString(e));
   }

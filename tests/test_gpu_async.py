@@ -1,0 +1,73 @@
+"""The constrained (IPM) device solve is asynchronous on its stream (include/srbd_qp.h
+srbd_qp_solve_f64): the stop decision lives on the device (ipm_box_impl.h report_running /
+solve_done), so the host enqueues the whole launch sequence and returns.  One host thread can
+therefore keep several handles busy at once -- the reference's hpipm-cpp is reentrant with
+separate memory per solver, and this is the batched equivalent."""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+NMPC = dict(iter_max=30, tol_stat=1e-4, tol_eq=1e-4, tol_ineq=1e-4, tol_comp=1e-4, split_step=1,
+            ric_alg=0, mode="Speed")
+
+
+def _setup(pkg, batch, seed):
+    qp, x0 = pkg.srbd_model.generate_batch(batch, N=20, seed=seed, constraints="box_u")
+    h = pkg.capi.Handle(qp.N, qp.nx, qp.nu, qp.ng, qp.has_box_u, qp.has_box_x, capacity=batch)
+    s = pkg.capi.settings_struct(NMPC)
+    dt, st, data, sol = pkg.capi.device_buffers(qp, x0, "cuda:0")
+    return qp, x0, h, s, (dt, st, data, sol)
+
+
+def test_ipm_solve_returns_before_its_stream_drains(pkg):
+    import torch
+    qp, x0, h, s, (dt, st, data, sol) = _setup(pkg, 8192, 41)
+    torch.cuda.synchronize()
+    h.solve_device(qp.batch, s, data, sol, order=False)  # warm-up (module load, first launch)
+    h.synchronize()
+    t0 = time.perf_counter()
+    h.solve_device(qp.batch, s, data, sol, order=False)
+    t_call = time.perf_counter() - t0
+    busy = not h.torch_stream().query()
+    h.synchronize()
+    t_all = time.perf_counter() - t0
+    assert busy, "the stream had drained when the call returned"
+    assert t_call < 0.5 * t_all, (t_call, t_all)
+    out = {k: v.cpu().numpy() for k, v in st.items()}
+    ref = pkg.capi.solve(qp, x0, NMPC)
+    assert np.all(out["status"] == 0)
+    for key in ("x", "u", "pi", "status", "iter"):
+        np.testing.assert_array_equal(out[key], ref[key])
+    h.close()
+
+
+def test_two_handles_overlap_from_one_thread(pkg):
+    """Two small latency-bound solves (64 QPs each: one chain of sweeps per QP group) on two
+    handles, launched from one thread: together they take well under the sum of their times."""
+    import torch
+    A = _setup(pkg, 64, 51)
+    B = _setup(pkg, 64, 52)
+    torch.cuda.synchronize()
+
+    def run(both):
+        t0 = time.perf_counter()
+        for qp, _, h, s, (_, _, data, sol) in (A, B):
+            h.solve_device(qp.batch, s, data, sol, order=False)
+            if not both:
+                h.synchronize()
+        A[2].synchronize()
+        B[2].synchronize()
+        return time.perf_counter() - t0
+
+    run(False)
+    seq = min(run(False) for _ in range(3))
+    par = min(run(True) for _ in range(3))
+    assert par < 0.8 * seq, (par, seq)
+    for qp, x0, h, _, (_, st, _, _) in (A, B):
+        ref = pkg.capi.solve(qp, x0, NMPC)
+        for key in ("x", "u", "status", "iter"):
+            np.testing.assert_array_equal(st[key].cpu().numpy(), ref[key])
+        h.close()
