@@ -2046,8 +2046,10 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
   // grids large enough to thin out (>= 64 workgroups, 1024 QPs); smaller solves skip the
   // two launches per iteration.
   const bool compact = ctl && a.qp_buf && full_grid.x >= 64;
-  b.qp_list = compact ? a.qp_buf : nullptr;
+  // (init covers every QP and clears the control words: no list, whatever they held before)
+  b.qp_list = nullptr;
   hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhInit>), grid, block, 0, stream, b);
+  b.qp_list = compact ? a.qp_buf : nullptr;
   // (SQRT changes RB and how B2, F1, F2 and the outputs apply the record's P)
   for (int it = 0;; ++it) {
     b.launch_it = it;

@@ -28,6 +28,10 @@ template <typename T>
 struct ProblemArgsT {
   int batch, N, nx, nu, ng;
   int layout;  // 0: QP-major inputs, 1: stage-major (srbd_qp_dims.layout)
+  // unconstrained solves: the single-QP (LDS) kernel may compute res / obj / stat itself
+  // (set by the C-ABI when the problem is not embedded; unconstr_fused_residuals says
+  // whether the launch did, so the separate residual pass is skipped)
+  int fuse_res;
   // QP data (device)
   const T *A, *B, *b, *Q, *S, *R, *q, *r, *x0;
   const T *lbu, *ubu, *lbu_mask, *ubu_mask;
@@ -126,6 +130,13 @@ hipError_t prepare_riccati_device();
 // KKT residual norms / objective of an unconstrained solution into a.res / a.obj
 template <typename T>
 hipError_t launch_unconstr_residuals(const ProblemArgsT<T>& a, hipStream_t stream);
+// true when launch_riccati_unconstr(a) computes res / obj / stat in its own kernel
+template <typename T>
+bool unconstr_fused_residuals(const ProblemArgsT<T>& a);
+// true when launch_riccati_unconstr(a) reads each QP's data exactly once, in one kernel
+// (the single-QP kernel's copy into LDS): the data may then live in mapped host memory
+template <typename T>
+bool unconstr_reads_once(const ProblemArgsT<T>& a);
 
 // nx < 12 or nu < 12: embed the problem in 12 x 12 stages (pad.hip).  pad_elems
 // is the pad buffer size (elements of T); pad_problem fills it from `a` and

@@ -1,0 +1,363 @@
+// riccati_latency_impl.h -- the single-QP unconstrained solve on one workgroup with fp64
+// matrix cores: the reference's own call pattern (NMPC_solver.cpp:316-330 builds one QP per
+// SQP iteration and calls OcpQpIpmSolver::solve on it) is a latency problem, not a
+// bandwidth one.  Included by riccati_unconstr.hip inside namespace ric_f64, after
+// riccati_unconstr_impl.h (its LDS image, copy and residual pass are reused).
+//
+// Why MFMA here and not in the batched kernels: a 16-lane QP group's 12 x 12 product is 144
+// dependent-free FMAs on 12 of 16 lanes, ~13 VALU instructions per column step; on the
+// batched path the chip is HBM-bound and the VALU is idle half the time anyway (DESIGN.md
+// 4.2).  For ONE QP the backward sweep is a chain of 20 stages on one wave, and
+// v_mfma_f64_16x16x4_f64 retires 1024 FMAs per wave instruction: the stage's seven 12 x 12
+// products (13 x 13 with the vector column) become 3 MFMAs each.
+//
+// Tiles.  A 12 x 12 block with its vector column (13 columns: [P | p], [A | b], [H | g], ...)
+// is held in the MFMA's C/D layout: lane l = (g = l >> 4, c = l & 15) register r holds
+// M[g + 4 r][c] (rows >= 12, columns >= 13: zero or unused).  That layout is the B operand of
+// the next product (k-block kb: lane (g, c) supplies M[4 kb + g][c] = register kb) and, for a
+// symmetric M, its A operand (A[c][4 kb + g] = M[4 kb + g][c]), so P_k+1 P_k+1 B, B'(P B),
+// ... chain in registers.  Transposed operands (B', A', Y') come from the LDS image, where
+// blocks are column-major: lane (g, c) reads M[4 kb + g][c] at c * 12 + 4 kb + g.
+//
+// Backward sweep, stage k (wave 0; the four 16-lane rows compute the same column-owned
+// Cholesky and solves redundantly, for free -- they issue the same instructions):
+//   WB = P B,  G = R + B'WB                                      6 MFMAs (critical path)
+//   W = P [A | b] + [0 | p],  [H | g] = [S | r] + B'W,  [F | f] = [Q | q] + A'W
+//                                                                9 MFMAs (overlap the Cholesky)
+//   L = chol(G) (column-owned, G through LDS), [Y | y] = L^-1 [H | g]
+//   [P | p]_k = [F | f] - Y'[Y | y]                              3 MFMAs
+// Wave 1 follows one stage behind: K = -L^-T [Y | y] (L, Y handed over in LDS), the stage
+// record ([K | k] rows, P packed, p: kernels.h kWs*, the batched kernel's layout, in the HBM
+// workspace) and the closed loop [Acl | bcl] = [A | b] + B [K | k] as rows in LDS.
+// Forward sweep (wave 0): x_k+1 = Acl x_k + bcl; then every stage at once (one group per
+// stage): u_k = K x_k + k, pi_k = P x_k + p.  Then, when asked, the residual pass.
+//
+// Same algorithm as riccati_step + fwd_sweep (classical Riccati, HPIPM's
+// d_ocp_qp_fact_solve_kkt_unconstr), another summation order: the outputs match the batched
+// kernel's to rounding (tests/test_gpu_riccati.py), not bit for bit.
+
+typedef double lat_d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kLatThreads = 512;  // wave 0: factorization, wave 1: records, all: the passes
+constexpr int kLatTile = 156;     // 13 columns x 12 rows, column-major (ld 12)
+constexpr int kLatL = 90;         // packed L (78) + 1 / diag (12)
+constexpr int kLatAcl = 156;      // [Acl | bcl]: 12 rows of 13
+
+__device__ __forceinline__ lat_d4 lat_mfma(double a, double b, lat_d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// LDS of the kernel (doubles): the image, the closed-loop rows, then a region the backward
+// sweep uses as scratch (the G / H tile, two Y tiles and two L factors, double-buffered for
+// wave 1) and the passes after it as the solution copy x, u, pi.
+__host__ __device__ constexpr int lat_acl_off(int N) { return (N + 1) * kImgStage; }
+__host__ __device__ constexpr int lat_scr_off(int N) { return lat_acl_off(N) + N * kLatAcl; }
+__host__ __device__ constexpr int lat_scr_size(int N) {
+  return (3 * N + 2) * 12 > 3 * kLatTile + 2 * kLatL ? (3 * N + 2) * 12 : 3 * kLatTile + 2 * kLatL;
+}
+size_t lat_lds_bytes(int N) { return (size_t)(lat_scr_off(N) + lat_scr_size(N)) * sizeof(double); }
+
+// Column-owned Cholesky with the pivots' reciprocals by v_rcp_f64 and two Newton steps
+// (3 dependent FMAs instead of the IEEE division's ~10 instructions on the stage's critical
+// path); otherwise chol_cols (riccati.h): `reg` on each pivot, a non-positive pivot zeroes
+// its column (BLASFEO dpotrf_l).
+__device__ __forceinline__ double lat_recip(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ void lat_chol(double (&G)[12], const int lane, const double reg, double (&Lc)[12],
+                                         double& rs) {
+  double dmine = 1.0;
+  sfor<0, 12>([&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    const double dk = bc<K>(G[K]) + reg;
+    const double inv = dk > 0.0 ? lat_recip(dk) : 0.0;
+    const double s = lane > K ? G[K] * inv : 0.0;
+    sfor<K + 1, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      G[I] = fmadd(-bc<K>(G[I]), s, G[I]);
+    });
+    dmine = lane == K ? dk : dmine;
+  });
+  rs = dmine > 0.0 ? 1.0 / __builtin_sqrt(dmine) : 0.0;
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    Lc[I] = G[I] * rs;
+  });
+}
+
+template <bool RES>
+__global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(ProblemArgsT<double> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  double* const img = reinterpret_cast<double*>(lds_raw);
+  const int N = a.N;
+  double* const acl = img + lat_acl_off(N);
+  double* const scr = img + lat_scr_off(N);
+  double* const gh = scr;                   // G, then [H | g] (13 x 12)
+  double* const ybuf = scr + kLatTile;      // [Y | y] of stages k (k & 1)
+  double* const lbuf = scr + 3 * kLatTile;  // L packed + 1 / diag (k & 1)
+  double* const so = scr;                   // after the sweep: x [N+1][12], u [N][12], pi [N+1][12]
+  const int qp = blockIdx.x;
+  const int wave = threadIdx.x >> 6;
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, c = l & 15;  // tile row block, column
+  const bool cv = c < 12;           // a column of a 12 x 12 block
+  const bool cw = c <= 12;          // ... or the vector column
+  const int cc = cv ? c : 11;       // clamped column for addressing
+  auto rec = [&](int k) { return a.ws + ((size_t)k * a.batch + qp) * kWsStage; };
+  tstamp(16);
+  lds_copy_qp(a, img, qp);
+
+  // ---------------- backward sweep ----------------
+  lat_d4 Pt;  // [P | p]_k+1 (wave 0)
+  if (wave == 0) {
+    const double* sl = img + N * kImgStage;
+    sfor<0, 4>([&](auto rr) {
+      constexpr int R = decltype(rr)::value;
+      const int row = g + 4 * R < 12 ? g + 4 * R : 11;
+      const double v = sl[cv ? kImgQ + c * 12 + row : kImgq + row];
+      Pt[R] = (g + 4 * R < 12 && cw) ? v : 0.0;
+    });
+    // terminal record: P_N packed, p_N
+    double* rn = rec(N);
+    sfor<0, 3>([&](auto rr) {
+      constexpr int R = decltype(rr)::value;
+      const int row = g + 4 * R;
+      if (cv && row >= c) rn[kWsP + packed_col(c) + row - c] = Pt[R];
+      if (c == 12) rn[kWsp + row] = Pt[R];
+    });
+  }
+  // stage j's second half (wave 1): K = -L^-T [Y | y], the record, [Acl | bcl]
+  auto finish_stage = [&](int j) {
+    const double* lb = lbuf + (j & 1) * kLatL;
+    const double* yb = ybuf + (j & 1) * kLatTile;
+    double Lc[12], Yc[12], Kc[12];
+    load_packed_lcol(lb, cc, Lc);  // (strictly lower part: the solve uses 1 / diag)
+    const double rs = lb[78 + cc];
+    sfor<0, 12>([&](auto i) { Yc[decltype(i)::value] = cw ? yb[c * 12 + decltype(i)::value] : 0.0; });
+    trsv_upper_t_neg_axpy(Lc, rs, Yc, Kc);  // lane c < 12: K[:, c]; lane 12: k
+    double* rj = rec(j);
+    if (l < 16 && cw)
+      sfor<0, 12>([&](auto i) { rj[kWsK + decltype(i)::value * kWsRow + c] = Kc[decltype(i)::value]; });
+    // [Acl | bcl][:, c] = [A | b][:, c] + B [K | k][:, c]
+    const double* sl = img + j * kImgStage;
+    double Ac[12], Bc[12];
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      const double av = sl[cv ? kImgA + c * 12 + I : kImgb + I];
+      Ac[I] = cw ? av : 0.0;
+      const double bv = sl[kImgB + cc * 12 + I];
+      Bc[I] = cv ? bv : 0.0;
+    });
+    sfor<0, 12>([&](auto m) {
+      constexpr int M = decltype(m)::value;
+      fma_bcast_src<M>(Ac, Bc, Kc[M]);
+    });
+    if (l < 16 && cw)
+      sfor<0, 12>([&](auto i) { acl[j * kLatAcl + decltype(i)::value * 13 + c] = Ac[decltype(i)::value]; });
+  };
+#pragma unroll 1
+  for (int k = N - 1; k >= 0; --k) {
+    if (wave == 0) {
+      tstamp(0);
+      const double* sl = img + k * kImgStage;
+      double bo[3], ao[3];
+      sfor<0, 3>([&](auto kb) {
+        constexpr int KB = decltype(kb)::value;
+        const int m = 4 * KB + g;
+        const double bv = sl[kImgB + cc * 12 + m];
+        bo[KB] = cv ? bv : 0.0;  // B[m][c]: B operand of P B; A operand (B') of B'WB, B'W
+        const double av = sl[cv ? kImgA + c * 12 + m : kImgb + m];
+        ao[KB] = cw ? av : 0.0;  // [A | b][m][c]: B operand of P [A | b]; A operand (A') of A'W
+      });
+      lat_d4 Rt, St, Qt;
+      sfor<0, 4>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        const bool rok = g + 4 * R < 12;
+        const int row = rok ? g + 4 * R : 11;
+        const double rv = sl[kImgR + cc * 12 + row];
+        const double sv = sl[cv ? kImgS + c * 12 + row : kImgr + row];
+        const double qv = sl[cv ? kImgQ + c * 12 + row : kImgq + row];
+        Rt[R] = rok && cv ? rv : 0.0;
+        St[R] = rok && cw ? sv : 0.0;
+        Qt[R] = rok && cw ? qv : 0.0;
+      });
+      // WB = P B; G = R + B'WB
+      lat_d4 WB = {0.0, 0.0, 0.0, 0.0};
+      sfor<0, 3>([&](auto kb) { WB = lat_mfma(Pt[decltype(kb)::value], bo[decltype(kb)::value], WB); });
+      lat_d4 Gt = Rt;
+      sfor<0, 3>([&](auto kb) { Gt = lat_mfma(bo[decltype(kb)::value], WB[decltype(kb)::value], Gt); });
+      // W = P [A | b] + [0 | p]; [H | g] = [S | r] + B'W; [F | f] = [Q | q] + A'W
+      lat_d4 Wt;
+      sfor<0, 4>([&](auto rr) { Wt[decltype(rr)::value] = c == 12 ? Pt[decltype(rr)::value] : 0.0; });
+      sfor<0, 3>([&](auto kb) { Wt = lat_mfma(Pt[decltype(kb)::value], ao[decltype(kb)::value], Wt); });
+      lat_d4 Ht = St, Ft = Qt;
+      sfor<0, 3>([&](auto kb) {
+        constexpr int KB = decltype(kb)::value;
+        Ht = lat_mfma(bo[KB], Wt[KB], Ht);
+        Ft = lat_mfma(ao[KB], Wt[KB], Ft);
+      });
+      tstamp(1);
+      // G to column-owned registers through LDS, Cholesky
+      lds_wave_fence();
+      sfor<0, 3>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        if (cv) gh[c * 12 + g + 4 * R] = Gt[R];
+      });
+      lds_wave_fence();
+      double Gc[12], Lc[12], rs;
+      sfor<0, 12>([&](auto i) {
+        const double v = gh[cc * 12 + decltype(i)::value];
+        Gc[decltype(i)::value] = cv ? v : 0.0;
+      });
+      lat_chol(Gc, c, a.reg, Lc, rs);
+      tstamp(3);
+      // [Y | y] = L^-1 [H | g]
+      lds_wave_fence();
+      sfor<0, 3>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        if (cw) gh[c * 12 + g + 4 * R] = Ht[R];
+      });
+      lds_wave_fence();
+      double Yc[12];
+      sfor<0, 12>([&](auto i) {
+        const double v = gh[(cw ? c : 12) * 12 + decltype(i)::value];
+        Yc[decltype(i)::value] = cw ? v : 0.0;
+      });
+      trsv_lower(Lc, rs, Yc);
+      tstamp(7);
+      // hand L and [Y | y] to wave 1 (and to the Y'Y operands)
+      double* yb = ybuf + (k & 1) * kLatTile;
+      double* lb = lbuf + (k & 1) * kLatL;
+      if (l < 16) {
+        if (cw) store12(yb + c * 12, Yc);
+        if (cv) {
+          store_packed_col(lb, c, Lc);
+          lb[78 + c] = rs;
+        }
+      }
+      lds_wave_fence();
+      // [P | p]_k = [F | f] - Y'[Y | y]
+      lat_d4 Pn = Ft;
+      sfor<0, 3>([&](auto kb) {
+        constexpr int KB = decltype(kb)::value;
+        const double yv = yb[(cw ? c : 12) * 12 + 4 * KB + g];
+        const double yB = cw ? yv : 0.0;  // [Y | y][m][c]
+        const double yA = cv ? -yv : 0.0;  // -(Y')[c][m]
+        Pn = lat_mfma(yA, yB, Pn);
+      });
+      Pt = Pn;
+      tstamp(9);
+      // record: P packed, p (the batched kernel's layout)
+      double* rk = rec(k);
+      sfor<0, 3>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        const int row = g + 4 * R;
+        if (cv && row >= c) rk[kWsP + packed_col(c) + row - c] = Pt[R];
+        if (c == 12) rk[kWsp + row] = Pt[R];
+      });
+    } else if (wave == 1 && k < N - 1) {
+      finish_stage(k + 1);
+    }
+    __syncthreads();
+  }
+  if (wave == 1) finish_stage(0);
+  __syncthreads();  // records and closed-loop rows complete; the scratch region is free
+  tstamp(12);
+
+  // ---------------- forward sweep: x_k+1 = Acl x_k + bcl (wave 0, row-owned) ----------------
+  if (wave == 0) {
+    const int row = cv ? c : 11;
+    double xv = cv ? a.x0[(size_t)qp * 12 + c] : 0.0;
+    double* xo = a.x + (size_t)qp * (N + 1) * 12;
+    double Ar[12], bv;
+    auto load_row = [&](int k) {
+      const double* r = acl + k * kLatAcl + row * 13;
+      sfor<0, 12>([&](auto j) { Ar[decltype(j)::value] = r[decltype(j)::value]; });
+      bv = r[12];
+    };
+    load_row(0);
+#pragma unroll 1
+    for (int k = 0; k < N; ++k) {
+      if (l < 12) {
+        so[k * 12 + l] = xv;
+        xo[(size_t)k * 12 + l] = xv;
+      }
+      double An[12], bn = 0.0;
+      if (k + 1 < N) {
+        const double* r = acl + (k + 1) * kLatAcl + row * 13;
+        sfor<0, 12>([&](auto j) { An[decltype(j)::value] = r[decltype(j)::value]; });
+        bn = r[12];
+      }
+      const double xn = dot_bcast(Ar, xv, bv);
+      xv = cv ? xn : 0.0;
+      sfor<0, 12>([&](auto j) { Ar[decltype(j)::value] = An[decltype(j)::value]; });
+      bv = bn;
+    }
+    if (l < 12) {
+      so[N * 12 + l] = xv;
+      xo[(size_t)N * 12 + l] = xv;
+    }
+  }
+  __syncthreads();
+  tstamp(13);
+
+  // ---------------- every stage at once: u_k = K x_k + k, pi_k = P x_k + p ----------------
+  bool bad = false;
+  {
+    const int grp = threadIdx.x >> 4;  // one 16-lane group per stage
+    const int lane = threadIdx.x & 15;
+    const int row = lane < 12 ? lane : 11;
+    for (int k = grp; k <= N; k += kLatThreads / 16) {
+      const double* rk = rec(k);
+      const double xk = lane < 12 ? so[k * 12 + lane] : 0.0;
+      double Pr[12];
+      load_packed_sym(rk + kWsP, row, Pr);
+      const double pv = rk[kWsp + row];
+      const double piv = dot_bcast(Pr, xk, pv);
+      if (lane < 12) {
+        so[(2 * N + 1) * 12 + k * 12 + lane] = piv;
+        a.pi[((size_t)qp * (N + 1) + k) * 12 + lane] = piv;
+        bad |= !(xk == xk);
+      }
+      // hpipm-cpp's Riccati getters (P column = row: symmetric; p), when asked for
+      if (a.P && lane < 12) store12(a.P + ((size_t)qp * (N + 1) + k) * 144 + (size_t)lane * 12, Pr);
+      if (a.p && lane < 12) a.p[((size_t)qp * (N + 1) + k) * 12 + lane] = pv;
+      if (k < N) {
+        double Kr[12];
+        sfor<0, 12>([&](auto j) { Kr[decltype(j)::value] = rk[kWsK + row * kWsRow + decltype(j)::value]; });
+        const double kv = rk[kWsK + row * kWsRow + 12];
+        const double uv = dot_bcast(Kr, xk, kv);
+        if (lane < 12) {
+          so[(N + 1) * 12 + k * 12 + lane] = uv;
+          a.u[((size_t)qp * N + k) * 12 + lane] = uv;
+          bad |= !(uv == uv);
+          if (a.k) a.k[((size_t)qp * N + k) * 12 + lane] = kv;
+          if (a.K) {  // column `lane` of K (nu x nx, column-major)
+            double Kc[12];
+            sfor<0, 12>([&](auto i) { Kc[decltype(i)::value] = rk[kWsK + decltype(i)::value * kWsRow + lane]; });
+            store12(a.K + ((size_t)qp * N + k) * 144 + (size_t)lane * 12, Kc);
+          }
+        }
+      }
+    }
+  }
+  const int any_bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) {
+    if (a.status) a.status[qp] = any_bad ? 3 : 0;
+    if (a.iter) a.iter[qp] = 0;
+  }
+  if constexpr (RES) {
+    ResLds acc{};
+    acc.img = img;
+    acc.so = so;
+    acc.N = N;
+    unconstr_residuals_body(a, acc, qp);
+  }
+}
+
+// the latency kernel's LDS fits the device (N <= 20 at fp64)
+bool lat_fits(int N) { return lat_lds_bytes(N) + kLdsResStatic <= kLdsBytesMax; }

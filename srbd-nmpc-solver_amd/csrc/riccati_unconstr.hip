@@ -22,9 +22,12 @@
 
 #define SRBD_REAL double
 #define SRBD_NS ric_f64
+#define SRBD_WITH_LATENCY 1  // the fp64 matrix-core single-QP kernel (riccati_latency_impl.h)
 #include "riccati_unconstr_impl.h"
+#undef SRBD_WITH_LATENCY
 #undef SRBD_REAL
 #undef SRBD_NS
+#define SRBD_WITH_LATENCY 0
 #define SRBD_REAL float
 #define SRBD_NS ric_f32
 #include "riccati_unconstr_impl.h"
@@ -55,6 +58,22 @@ hipError_t launch_unconstr_residuals<double>(const ProblemArgsT<double>& a, hipS
 template <>
 hipError_t launch_unconstr_residuals<float>(const ProblemArgsT<float>& a, hipStream_t stream) {
   return ric_f32::launch_residuals(a, stream);
+}
+template <>
+bool unconstr_fused_residuals<double>(const ProblemArgsT<double>& a) {
+  return ric_f64::fused_residuals(a);
+}
+template <>
+bool unconstr_fused_residuals<float>(const ProblemArgsT<float>& a) {
+  return ric_f32::fused_residuals(a);
+}
+template <>
+bool unconstr_reads_once<double>(const ProblemArgsT<double>& a) {
+  return ric_f64::reads_once(a);
+}
+template <>
+bool unconstr_reads_once<float>(const ProblemArgsT<float>& a) {
+  return ric_f32::reads_once(a);
 }
 
 }  // namespace srbd

@@ -64,6 +64,11 @@ static_assert(kImgRec + kWsStage <= kImgStage, "a record fits its stage slot pas
 
 struct LdsSrc {
   real* img;
+  // records in the HBM workspace instead of over the image's Q, S, R (the fused-residual
+  // kernel, whose residual pass reads those blocks after the forward sweep): stage-major
+  // like HbmSrc, null = in the image
+  real* grec = nullptr;
+  int batch = 0, qp = 0;
   __device__ real* slot(int k) const { return img + k * kImgStage; }
   __device__ const real* A(int k) const { return slot(k) + kImgA; }
   __device__ const real* B(int k) const { return slot(k) + kImgB; }
@@ -73,7 +78,9 @@ struct LdsSrc {
   __device__ const real* R(int k) const { return slot(k) + kImgR; }
   __device__ const real* q(int k) const { return slot(k) + kImgq; }
   __device__ const real* r(int k) const { return slot(k) + kImgr; }
-  __device__ real* rec(int k) const { return slot(k) + kImgRec; }
+  __device__ real* rec(int k) const {
+    return grec ? grec + ((size_t)k * batch + qp) * kWsStage : slot(k) + kImgRec;
+  }
 };
 
 // ---- stage records ----
@@ -151,9 +158,11 @@ __device__ __forceinline__ void store_riccati_out(const ProblemArgsT<real>& a, i
 // per stage and the record 156 reals).  The record and data rows of stage k+1 are loaded
 // while stage k computes (the loads do not depend on x), so each stage pays one memory
 // latency less.
+// so (optional, the fused-residual kernel): an LDS copy of the solution, x [N+1][12], then
+// u [N][12], then pi [N+1][12], for the residual pass that follows in the same kernel.
 template <class Src>
 __device__ __forceinline__ void fwd_sweep(const ProblemArgsT<real>& a, const Src& src, const int qp,
-                                          const int lane) {
+                                          const int lane, real* so = nullptr) {
   constexpr int nx = 12, nu = 12;
   const int N = a.N;
   const bool own = lane < kMaxDim;
@@ -205,6 +214,10 @@ __device__ __forceinline__ void fwd_sweep(const ProblemArgsT<real>& a, const Src
     if (own) {
       xo[(size_t)k * nx + lane] = xv;
       po[(size_t)k * nx + lane] = pp;
+      if (so) {
+        so[k * nx + lane] = xv;
+        so[(2 * N + 1) * nx + k * nx + lane] = pp;
+      }
     }
     if (k == N) break;
     real uu = kv, xn = bv;
@@ -213,7 +226,10 @@ __device__ __forceinline__ void fwd_sweep(const ProblemArgsT<real>& a, const Src
       uu = fmadd(Kr[J], bx[J], uu);
       xn = fmadd(Ar[J], bx[J], xn);
     });
-    if (own) uo[(size_t)k * nu + lane] = uu;
+    if (own) {
+      uo[(size_t)k * nu + lane] = uu;
+      if (so) so[(N + 1) * nx + k * nu + lane] = uu;
+    }
     xn = dot_bcast(Br, uu, xn);  // + B u (u element-owned, broadcast inside the FMAs)
     bad |= own && (!(uu == uu) || !(xn == xn));
     xv = xn;
@@ -243,7 +259,7 @@ __device__ __forceinline__ void fwd_sweep(const ProblemArgsT<real>& a, const Src
 // and outputs are the same (P_k = F - Y'Y of the stage, which Lx factors).
 template <bool SQRT, class Src>
 __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src& src, const int qp,
-                                         const int lane) {
+                                         const int lane, real* so = nullptr) {
   const int N = a.N;
   const bool isv = lane == kVecLane;
   const bool own = lane < kMaxDim;  // lane owns a block column
@@ -310,7 +326,7 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
     if constexpr (SQRT) sqrt_factor(P, lane);
   }
   tstamp(12);
-  fwd_sweep(a, src, qp, lane);
+  fwd_sweep(a, src, qp, lane, so);
   tstamp(13);
 }
 
@@ -356,13 +372,10 @@ __device__ __forceinline__ const real* img_source(const ProblemArgsT<real>& a, i
   return a.r + s * 12 + (o - kImgr);
 }
 
-template <bool SQRT>
-__global__ void __launch_bounds__(kLdsCopyThreads, 1) riccati_unconstr_lds_kernel(ProblemArgsT<real> a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-  real* img = reinterpret_cast<real*>(lds_raw);
-  const int qp = blockIdx.x;
+// The QP's blocks into the LDS image by every thread of the workgroup (global->LDS DMA;
+// the source may be device memory or mapped host memory), waited for and fenced.
+__device__ __forceinline__ void lds_copy_qp(const ProblemArgsT<real>& a, real* img, int qp) {
   const int lane = threadIdx.x;
-  tstamp(16);
   const int total = (a.N + 1) * kImgStage;
   const int wave_off = (lane >> 6) * 64 * kRealsPerDma;  // this wave's 1 KiB of each round
   for (int c0 = 0; c0 < total; c0 += kLdsCopyThreads * kRealsPerDma) {
@@ -377,11 +390,22 @@ __global__ void __launch_bounds__(kLdsCopyThreads, 1) riccati_unconstr_lds_kerne
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   tstamp(15);
-  if (lane >= kGroup) return;
-  solve_qp<SQRT>(a, LdsSrc{img}, qp, lane);
+}
+
+template <bool SQRT>
+__global__ void __launch_bounds__(kLdsCopyThreads, 1) riccati_unconstr_lds_kernel(ProblemArgsT<real> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  real* img = reinterpret_cast<real*>(lds_raw);
+  const int qp = blockIdx.x;
+  tstamp(16);
+  lds_copy_qp(a, img, qp);
+  if (threadIdx.x >= kGroup) return;
+  solve_qp<SQRT>(a, LdsSrc{img}, qp, threadIdx.x);
 }
 
 size_t lds_image_bytes(int N) { return (size_t)(N + 1) * kImgStage * sizeof(real); }
+// the fused-residual kernel's LDS: the image plus the solution copy x, u, pi
+size_t lds_res_bytes(int N) { return lds_image_bytes(N) + (size_t)(3 * N + 2) * 12 * sizeof(real); }
 
 
 // KKT residuals and objective of an unconstrained solution: HPIPM's
@@ -397,27 +421,55 @@ size_t lds_image_bytes(int N) { return (size_t)(N + 1) * kImgStage * sizeof(real
 // unpadded).
 constexpr int kResThreads = 256;
 constexpr int kResStages = kResThreads / 12;  // 21 stages per pass
+constexpr int kResWavesMax = 8;                // (the fused single-QP kernel: 512 threads)
 
 __device__ __forceinline__ void max_nan(real& m, real v) {
   v = v < real(0) ? -v : v;
   if (v > m || v != v) m = v;  // NaN propagates
 }
 
-__global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(ProblemArgsT<real> a) {
-  const int qp = blockIdx.x;
+// Where the residual pass finds a QP's blocks and its solution: the C-ABI buffers (QP-major
+// or stage-major, any nx <= 12, nu <= 12), or (the fused single-QP kernel) the LDS image of
+// riccati_unconstr_lds_kernel and its LDS copy of x, u, pi (12 x 12 stages).
+struct ResGlobal {
+  const ProblemArgsT<real>& a;
+  int qp;
+  __device__ const real* at(const real* base, int nstage, size_t blk, int k) const {
+    return a.layout == 1 ? base + ((size_t)k * a.batch + qp) * blk : base + ((size_t)qp * nstage + k) * blk;
+  }
+  __device__ const real* A(int k) const { return at(a.A, a.N, (size_t)a.nx * a.nx, k); }
+  __device__ const real* B(int k) const { return at(a.B, a.N, (size_t)a.nx * a.nu, k); }
+  __device__ const real* b(int k) const { return at(a.b, a.N, a.nx, k); }
+  __device__ const real* Q(int k) const { return at(a.Q, a.N + 1, (size_t)a.nx * a.nx, k); }
+  __device__ const real* S(int k) const { return at(a.S, a.N, (size_t)a.nx * a.nu, k); }
+  __device__ const real* R(int k) const { return at(a.R, a.N, (size_t)a.nu * a.nu, k); }
+  __device__ const real* q(int k) const { return at(a.q, a.N + 1, a.nx, k); }
+  __device__ const real* r(int k) const { return at(a.r, a.N, a.nu, k); }
+  __device__ const real* x() const { return a.x + (size_t)qp * (a.N + 1) * a.nx; }
+  __device__ const real* u() const { return a.u + (size_t)qp * a.N * a.nu; }
+  __device__ const real* pi() const { return a.pi + (size_t)qp * (a.N + 1) * a.nx; }
+};
+struct ResLds : LdsSrc {
+  const real* so;  // x [N+1][12], u [N][12], pi [N+1][12]
+  int N;
+  __device__ const real* x() const { return so; }
+  __device__ const real* u() const { return so + (N + 1) * 12; }
+  __device__ const real* pi() const { return so + (2 * N + 1) * 12; }
+};
+
+// The residual pass of one QP by the whole workgroup (every thread calls it: it ends with a
+// workgroup reduction).  Threads >= kResStages * 12 only take part in the reduction, so a
+// 512-thread workgroup sums the same partial results in the same order as a 256-thread one.
+template <class Acc>
+__device__ __forceinline__ void unconstr_residuals_body(const ProblemArgsT<real>& a, const Acc& acc, int qp) {
   const int N = a.N, nx = a.nx, nu = a.nu;
   if (a.stat) {  // the QP's stat table is cleared here (no separate memset), row 0 filled below
     real* tab = a.stat + (size_t)qp * a.stat_rows * kStatCols;
-    for (int i = threadIdx.x; i < a.stat_rows * kStatCols; i += kResThreads) tab[i] = real(0);
+    for (int i = threadIdx.x; i < a.stat_rows * kStatCols; i += blockDim.x) tab[i] = real(0);
   }
-  const bool smaj = a.layout == 1;
-  auto at = [&](const real* base, int nstage, size_t blk, int k) -> const real* {
-    return smaj ? base + ((size_t)k * a.batch + qp) * blk : base + ((size_t)qp * nstage + k) * blk;
-  };
-  const size_t nxx = (size_t)nx * nx, nxu = (size_t)nx * nu, nuu = (size_t)nu * nu;
-  const real* x = a.x + (size_t)qp * (N + 1) * nx;
-  const real* u = a.u + (size_t)qp * N * nu;
-  const real* pi = a.pi + (size_t)qp * (N + 1) * nx;
+  const real* x = acc.x();
+  const real* u = acc.u();
+  const real* pi = acc.pi();
   const int i = threadIdx.x % 12;
   real mg = real(0), mb = real(0), ob = real(0);
   for (int k = threadIdx.x / 12; threadIdx.x < kResStages * 12 && k <= N; k += kResStages) {
@@ -426,12 +478,12 @@ __global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(Problem
       const real* uk = u + (size_t)k * nu;
       const real* xn = x + (size_t)(k + 1) * nx;
       const real* pn = pi + (size_t)(k + 1) * nx;
-      const real* A = at(a.A, N, nxx, k);
-      const real* B = at(a.B, N, nxu, k);
+      const real* A = acc.A(k);
+      const real* B = acc.B(k);
       if (i < nu) {  // column-major blocks: M[i][j] = M[j * rows + i]
-        const real* S = at(a.S, N, nxu, k);
-        const real* R = at(a.R, N, nuu, k);
-        const real* r = at(a.r, N, nu, k);
+        const real* S = acc.S(k);
+        const real* R = acc.R(k);
+        const real* r = acc.r(k);
         real ru = real(0), sx = real(0), bp = real(0);
         for (int j = 0; j < nu; ++j) ru += R[(size_t)j * nu + i] * uk[j];
         for (int j = 0; j < nx; ++j) sx += S[(size_t)j * nu + i] * xk[j];
@@ -440,7 +492,7 @@ __global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(Problem
         ob += uk[i] * (real(0.5) * ru + r[i] + sx);
       }
       if (i < nx) {
-        const real* b = at(a.b, N, nx, k);
+        const real* b = acc.b(k);
         real v = b[i] - xn[i];
         for (int j = 0; j < nx; ++j) v += A[(size_t)j * nx + i] * xk[j];
         for (int j = 0; j < nu; ++j) v += B[(size_t)j * nx + i] * uk[j];
@@ -448,16 +500,16 @@ __global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(Problem
       }
     }
     if (k > 0 && i < nx) {
-      const real* Q = at(a.Q, N + 1, nxx, k);
-      const real* q = at(a.q, N + 1, nx, k);
+      const real* Q = acc.Q(k);
+      const real* q = acc.q(k);
       real qx = real(0), g = q[i] - pi[(size_t)k * nx + i];
       for (int j = 0; j < nx; ++j) qx += Q[(size_t)j * nx + i] * xk[j];
       g += qx;
       if (k < N) {
         const real* uk = u + (size_t)k * nu;
         const real* pn = pi + (size_t)(k + 1) * nx;
-        const real* A = at(a.A, N, nxx, k);
-        const real* S = at(a.S, N, nxu, k);
+        const real* A = acc.A(k);
+        const real* S = acc.S(k);
         for (int j = 0; j < nu; ++j) g += S[(size_t)i * nu + j] * uk[j];
         for (int j = 0; j < nx; ++j) g += A[(size_t)i * nx + j] * pn[j];
       }
@@ -472,7 +524,7 @@ __global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(Problem
     if (obb > mb || obb != obb) mb = obb;
     ob += __shfl_xor(ob, m);
   }
-  __shared__ real part[3][kResThreads / 64];
+  __shared__ real part[3][kResWavesMax];
   const int w = threadIdx.x / 64;
   if ((threadIdx.x & 63) == 0) {
     part[0][w] = mg;
@@ -481,6 +533,7 @@ __global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(Problem
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    // (waves past the stage-parallel ones hold 0 and add nothing)
     mg = part[0][0], mb = part[1][0], ob = part[2][0];
     for (int j = 1; j < kResThreads / 64; ++j) {
       if (part[0][j] > mg || part[0][j] != part[0][j]) mg = part[0][j];
@@ -502,6 +555,38 @@ __global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(Problem
     }
     if (a.status && (mg != mg || mb != mb)) a.status[qp] = 3;  // NaNDetected
   }
+}
+
+__global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(ProblemArgsT<real> a) {
+  unconstr_residuals_body(a, ResGlobal{a, (int)blockIdx.x}, (int)blockIdx.x);
+}
+
+// The reference's call pattern in one launch (one QP per workgroup, the C-ABI's small
+// batches with res / obj / stat requested): the copy into LDS, the solve (records in the HBM
+// workspace, so the image keeps Q, S, R for the residual pass; x, u, pi also into LDS), then
+// the residual pass over the image by the whole workgroup -- the same arithmetic as
+// riccati_unconstr_lds_kernel followed by unconstr_residuals_kernel, without the second
+// launch and its re-read of the QP (which may live in mapped host memory: the C-ABI's
+// host-buffer path hands its pinned staging buffer straight to this kernel).
+template <bool SQRT>
+__global__ void __launch_bounds__(kLdsCopyThreads, 1) riccati_unconstr_lds_res_kernel(ProblemArgsT<real> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  real* img = reinterpret_cast<real*>(lds_raw);
+  real* so = img + (a.N + 1) * kImgStage;
+  const int qp = blockIdx.x;
+  tstamp(16);
+  lds_copy_qp(a, img, qp);
+  LdsSrc src{img};
+  src.grec = a.ws;
+  src.batch = a.batch;
+  src.qp = qp;
+  if (threadIdx.x < kGroup) solve_qp<SQRT>(a, src, qp, threadIdx.x, so);
+  __syncthreads();  // the solution copy is complete
+  ResLds acc{};
+  acc.img = img;
+  acc.so = so;
+  acc.N = a.N;
+  unconstr_residuals_body(a, acc, qp);
 }
 
 // The same residuals for large batches, on the solve's layout: one 16-lane group per QP
@@ -648,13 +733,54 @@ hipError_t launch_residuals(const ProblemArgsT<real>& a, hipStream_t stream) {
 // image fits a workgroup's LDS (fp64: N <= 26, fp32: N <= 53)
 constexpr int kLdsBatchMax = 256;
 constexpr size_t kLdsBytesMax = 160 * 1024;
+constexpr size_t kLdsResStatic = 1024;  // >= sizeof(part) of unconstr_residuals_body
 
 bool use_lds_kernel(const ProblemArgsT<real>& a) {
   return a.layout == 0 && a.batch <= kLdsBatchMax && lds_image_bytes(a.N) <= kLdsBytesMax;
 }
 
+// The fp64 classical solve of small batches runs on the matrix-core latency kernel
+// (riccati_latency_impl.h; -DSRBD_LATENCY_MFMA=0 builds without it).
+#ifndef SRBD_LATENCY_MFMA
+#define SRBD_LATENCY_MFMA 1
+#endif
+#if SRBD_WITH_LATENCY && SRBD_LATENCY_MFMA
+#include "riccati_latency_impl.h"
+bool lat_eligible(const ProblemArgsT<real>& a) { return use_lds_kernel(a) && lat_fits(a.N); }
+#else
+bool lat_eligible(const ProblemArgsT<real>&) { return false; }
+#endif
+
+// the single-QP kernel computes the residuals itself (one launch, one read of the data)
+bool fused_residuals(const ProblemArgsT<real>& a) {
+  return a.fuse_res && (a.res || a.obj || a.stat) && a.nx == 12 && a.nu == 12 && use_lds_kernel(a) &&
+         lds_res_bytes(a.N) + kLdsResStatic <= kLdsBytesMax;  // (+ the reduction's static LDS)
+}
+// the launch reads each QP's data once, into LDS, and nothing else reads it
+bool reads_once(const ProblemArgsT<real>& a) {
+  return a.nx == 12 && a.nu == 12 && use_lds_kernel(a) &&
+         (fused_residuals(a) || !(a.res || a.obj || a.stat));
+}
+
 template <bool SQRT>
 static hipError_t launch_alg(const ProblemArgsT<real>& a, hipStream_t stream) {
+#if SRBD_WITH_LATENCY && SRBD_LATENCY_MFMA
+  if (!SQRT && lat_eligible(a)) {
+    if (fused_residuals(a)) {
+      hipLaunchKernelGGL(riccati_latency_kernel<true>, dim3((unsigned)a.batch), dim3(kLatThreads),
+                         lat_lds_bytes(a.N), stream, a);
+    } else {
+      hipLaunchKernelGGL(riccati_latency_kernel<false>, dim3((unsigned)a.batch), dim3(kLatThreads),
+                         lat_lds_bytes(a.N), stream, a);
+    }
+    return hipGetLastError();
+  }
+#endif
+  if (fused_residuals(a)) {
+    hipLaunchKernelGGL(riccati_unconstr_lds_res_kernel<SQRT>, dim3((unsigned)a.batch), dim3(kLdsCopyThreads),
+                       lds_res_bytes(a.N), stream, a);
+    return hipGetLastError();
+  }
   if (use_lds_kernel(a)) {
     // (the > 64 KiB dynamic-LDS attribute is set on the handle's device by srbd_qp_create:
     // prepare_device below)
@@ -679,6 +805,21 @@ hipError_t prepare_device() {
   if (e == hipSuccess)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_unconstr_lds_kernel<true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytesMax);
+  // (the fused kernel also has the residual reduction's static LDS: kLdsResStatic at most)
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_unconstr_lds_res_kernel<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_unconstr_lds_res_kernel<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
+#if SRBD_WITH_LATENCY && SRBD_LATENCY_MFMA
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_latency_kernel<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_latency_kernel<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
+#endif
   return e;
 }
 

@@ -188,6 +188,7 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srb
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&h->ws), h->ws_bytes);
   if (e == hipSuccess && constrained(*dims)) {
     e = hipMalloc(reinterpret_cast<void**>(&h->ctl), sizeof(int) * srbd::kCtlInts);
+    if (e == hipSuccess) e = hipMemset(h->ctl, 0, sizeof(int) * srbd::kCtlInts);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&h->qp_buf), sizeof(int) * ((size_t)batch_capacity + 1));
   }
   hipSetDevice(prev);
@@ -387,12 +388,14 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
       }
     }
   } else {
+    // (the single-QP kernel computes the residuals itself when the problem is not embedded)
+    run.fuse_res = st->compute_residuals && !padded;
     e = srbd::launch_riccati_unconstr(run, strm);
     if (e == hipSuccess && padded) e = srbd::unpad_solution<T>(a, run, strm);
     // residual norms / objective of the solution when asked for (HPIPM computes them
     // for nc = 0 too; an extra pass over the QP data, so only on request); the stat
     // table's row 0 gets them as well
-    if (e == hipSuccess && (s->res || s->obj || s->stat)) {
+    if (e == hipSuccess && (s->res || s->obj || s->stat) && !srbd::unconstr_fused_residuals(run)) {
       if (st->compute_residuals) {
         e = srbd::launch_unconstr_residuals<T>(a, strm);
       } else {
@@ -808,9 +811,33 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
     }
     pin = reinterpret_cast<char*>(h->pinned);
   }
+  // Zero copy: when the launch reads each QP's data exactly once (the single-QP kernel's
+  // copy into LDS) and writes each output once, the kernel reads the pinned staging buffer
+  // over PCIe and writes its outputs straight into it -- no DMA either way, one launch, one
+  // wait (the reference's one-QP-per-solve() call pattern, NMPC_solver.cpp:316-330).
+  bool zero_copy = false;
+  if (e == hipSuccess && small && !constrained(m)) {
+    srbd::ProblemArgsT<T> probe{};
+    probe.batch = batch;
+    probe.N = m.N;
+    probe.nx = m.nx;
+    probe.nu = m.nu;
+    probe.layout = m.layout;
+    probe.fuse_res = st->compute_residuals;
+    T dummy = T(0);
+    probe.res = s->res ? &dummy : nullptr;
+    probe.obj = s->obj ? &dummy : nullptr;
+    probe.stat = s->stat ? &dummy : nullptr;
+    zero_copy = srbd::unconstr_reads_once(probe);
+  }
+  if (zero_copy) {
+    void* dev = nullptr;
+    e = hipHostGetDevicePointer(&dev, pin, 0);
+    if (e == hipSuccess) base = reinterpret_cast<char*>(dev);
+  }
   if (e == hipSuccess && small) {
     for (const Field& f : in) std::memcpy(pin + f.off, f.host, f.bytes);
-    e = hipMemcpyAsync(base, pin, in_end, hipMemcpyHostToDevice, h->stream);
+    if (!zero_copy) e = hipMemcpyAsync(base, pin, in_end, hipMemcpyHostToDevice, h->stream);
   }
   for (size_t i = 0; !small && e == hipSuccess && i < in.size(); ++i)
     e = hipMemcpyAsync(base + in[i].off, in[i].host, in[i].bytes, hipMemcpyHostToDevice, h->stream);
@@ -821,7 +848,7 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
       std::memcpy(pin + ox, s->x, bx);
       std::memcpy(pin + ou, s->u, bu);
       // x and u are adjacent in the staging layout (addo order, 256-byte aligned)
-      e = hipMemcpyAsync(base + ox, pin + ox, ou + bu - ox, hipMemcpyHostToDevice, h->stream);
+      if (!zero_copy) e = hipMemcpyAsync(base + ox, pin + ox, ou + bu - ox, hipMemcpyHostToDevice, h->stream);
     } else {
       e = hipMemcpyAsync(base + ox, s->x, bx, hipMemcpyHostToDevice, h->stream);
       if (e == hipSuccess) e = hipMemcpyAsync(base + ou, s->u, bu, hipMemcpyHostToDevice, h->stream);
@@ -859,7 +886,7 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
   }
   hipSetDevice(h->device);
   if (small) {
-    if (e == hipSuccess && in_end < off)
+    if (e == hipSuccess && in_end < off && !zero_copy)
       e = hipMemcpyAsync(pin + in_end, base + in_end, off - in_end, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)
