@@ -76,7 +76,7 @@
 extern "C" {
 #endif
 
-#define SRBD_QP_ABI_VERSION 9
+#define SRBD_QP_ABI_VERSION 10
 #define SRBD_QP_MAX_NX 12
 #define SRBD_QP_MAX_NU 12
 #define SRBD_QP_MAX_NG 64
@@ -234,15 +234,35 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device,
                    srbd_qp_handle* out);
 
 /* Device-resident batch solve, asynchronous on `stream` (a hipStream_t; NULL
- * = the handle's own stream).  Every data/solution pointer is device memory.
- * With settings->warm_start the x/u buffers are read as the warm start.    */
+ * = the handle's own stream): the call enqueues the whole solve and returns
+ * without waiting -- the IPM's stop decision is taken on the device -- except
+ * that settings->f64_rescue / f32_iters wait once for their first pass.
+ * Every data/solution pointer is device memory.  With settings->warm_start the
+ * x/u buffers are read as the warm start.  One handle serves one solve at a
+ * time (its workspace); several handles run concurrently.                  */
 int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
                       const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol,
                       void* stream);
 
-/* Host-buffer batch solve: copies to device, solves, copies back, waits.   */
+/* Host-buffer batch solve: copies to device, solves, copies back, waits.
+ * Small unconstrained batches (<= 256 QPs, nx = nu = 12, N <= 26) are zero copy:
+ * the kernel reads the handle's pinned staging buffer and writes the outputs
+ * into it.                                                                  */
 int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
                            const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol);
+
+/* The handle's pinned host staging for a srbd_qp_solve_host_f64 call of `batch`
+ * QPs with `settings`: every field that *data / *sol have non-NULL (any value,
+ * e.g. (void*)1: a marker) is replaced by its place in the staging buffer, the
+ * others set NULL.  A caller that packs its QPs there and then passes the same
+ * two structs to srbd_qp_solve_host_f64 saves both staging copies (the solve
+ * skips a copy whose source already is its place); the outputs are left there.
+ * Valid until the handle stages a larger call or is destroyed; SRBD_QP_ECAPACITY
+ * when the call's buffers exceed the pinned staging size (8 MiB).  Replaces the
+ * Eigen-pointer marshalling of ocp_qp_ipm_solver.cpp:226-289 for the shim.
+ * (ABI 10)                                                                  */
+int srbd_qp_host_staging_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
+                             srbd_qp_data_f64* data, srbd_qp_solution_f64* sol);
 
 /* fp32 twins of the two solve entry points (the handle serves both).      */
 int srbd_qp_solve_f32(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,

@@ -111,6 +111,9 @@ def lib():
         L.srbd_qp_solve_host_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
                                              C.POINTER(Data), C.POINTER(Solution)]
         L.srbd_qp_solve_host_f64.restype = C.c_int
+        L.srbd_qp_host_staging_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
+                                               C.POINTER(Data), C.POINTER(Solution)]
+        L.srbd_qp_host_staging_f64.restype = C.c_int
         L.srbd_qp_solve_f32.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
                                         C.POINTER(Data32), C.POINTER(Solution32), C.c_void_p]
         L.srbd_qp_solve_f32.restype = C.c_int
@@ -238,6 +241,12 @@ class Handle:
         check(f(self._h, int(batch), C.byref(settings), C.byref(data), C.byref(sol),
                 C.c_void_p(stream or None)), f.__name__)
         _order_after(o)
+
+    def host_staging(self, batch: int, settings: Settings, data, sol) -> None:
+        """srbd_qp_host_staging_f64: the non-NULL fields of data / sol (markers) become
+        pointers into the handle's pinned staging buffer (in place)."""
+        check(lib().srbd_qp_host_staging_f64(self._h, int(batch), C.byref(settings), C.byref(data),
+                                             C.byref(sol)), "srbd_qp_host_staging_f64")
 
     def solve_host(self, batch: int, settings: Settings, data, sol) -> None:
         f = lib().srbd_qp_solve_host_f32 if isinstance(data, Data32) else lib().srbd_qp_solve_host_f64

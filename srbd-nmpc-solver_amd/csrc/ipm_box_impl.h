@@ -1279,6 +1279,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           P[I] = f.F[I];
         });
         if constexpr (SQRT) {
+          if constexpr (SRBD_SYM_AVG) symmetrize_avg(P, lane);
           sqrt_factor(P, lane);
           if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
         }
@@ -1516,13 +1517,13 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         real y = g;
         sfor<0, 12>([&](auto kk) {
           constexpr int K = decltype(kk)::value;
-          const real yk = bc<K>(y * rs);
+          const real yk = bc<K>(apply_rs(y, rs));
           if (lane == K) y = yk;
           if (lane > K) y = fmadd(-Lr[K], yk, y);
         });
         sfor_down<0, 12>([&](auto kk) {
           constexpr int K = decltype(kk)::value;
-          const real zk = bc<K>(y * rs);
+          const real zk = bc<K>(apply_rs(y, rs));
           if (lane == K) y = zk;
           if (lane < K) y = fmadd(-Lc[K], zk, y);
         });
@@ -1724,13 +1725,13 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           real y = g;
           sfor<0, 12>([&](auto kk) {
             constexpr int K = decltype(kk)::value;
-            const real yk = bc<K>(y * rs);
+            const real yk = bc<K>(apply_rs(y, rs));
             if (lane == K) y = yk;
             if (lane > K) y = fmadd(-Lr[K], yk, y);
           });
           sfor_down<0, 12>([&](auto kk) {
             constexpr int K = decltype(kk)::value;
-            const real zk = bc<K>(y * rs);
+            const real zk = bc<K>(apply_rs(y, rs));
             if (lane == K) y = zk;
             if (lane < K) y = fmadd(-Lc[K], zk, y);
           });

@@ -84,6 +84,32 @@ __device__ __forceinline__ void tmul_acc(const T (&X)[12], const T (&Y)[12], T (
   });
 }
 
+// How a triangular solve applies a diagonal entry of L: by default `rs` holds 1 / L_ll and
+// the solves multiply by it; -DSRBD_TRSV_DIV=1 (diagnostic builds) keeps L_ll itself and
+// divides, as the oracle's chol_solve does (0 stays 0 for a zeroed pivot).
+#ifndef SRBD_TRSV_DIV
+#define SRBD_TRSV_DIV 0
+#endif
+template <typename T>
+__device__ __forceinline__ T apply_rs(T x, T rs) {
+  if constexpr (SRBD_TRSV_DIV) {
+    return rs != T(0) ? x / rs : T(0);
+  } else {
+    return x * rs;
+  }
+}
+// rs of a pivot d (> 0, else the zeroed direction) and 1 / L_ll for scaling L's column
+template <typename T>
+__device__ __forceinline__ void pivot_rs(T d, T& rs, T& inv_l) {
+  if constexpr (SRBD_TRSV_DIV) {
+    rs = d > T(0) ? __builtin_sqrt(d) : T(0);
+    inv_l = rs > T(0) ? T(1) / rs : T(0);
+  } else {
+    rs = d > T(0) ? T(1) / __builtin_sqrt(d) : T(0);
+    inv_l = rs;
+  }
+}
+
 // Right-looking Cholesky of the column-owned symmetric G (lane l holds
 // G[:,l]); `reg` is added to each pivot.  On exit Lc holds column l of L
 // (rows > l meaningful) and rs = 1 / L[l][l] (0 for a non-positive pivot).
@@ -104,10 +130,11 @@ __device__ __forceinline__ void chol_cols(T (&G)[12], const int lane, const T re
     });
     dmine = lane == K ? dk : dmine;
   });
-  rs = dmine > T(0) ? T(1) / __builtin_sqrt(dmine) : T(0);
+  T inv_l;
+  pivot_rs(dmine, rs, inv_l);
   sfor<0, 12>([&](auto i) {
     constexpr int I = decltype(i)::value;
-    Lc[I] = G[I] * rs;
+    Lc[I] = G[I] * inv_l;
   });
 }
 
@@ -116,7 +143,7 @@ template <typename T>
 __device__ __forceinline__ void trsv_lower(const T (&Lc)[12], const T rs, T (&H)[12]) {
   sfor<0, 12>([&](auto kk) {
     constexpr int K = decltype(kk)::value;
-    const T y = H[K] * bc<K>(rs);
+    const T y = apply_rs(H[K], bc<K>(rs));
     H[K] = y;
     sfor<K + 1, 12>([&](auto i) {
       constexpr int I = decltype(i)::value;
@@ -135,7 +162,7 @@ __device__ __forceinline__ void trsv_upper_t_neg_axpy(const T (&Lc)[12], const T
   sfor<0, 12>([&](auto i) { w[decltype(i)::value] = y[decltype(i)::value]; });
   sfor_down<0, 12>([&](auto kk) {
     constexpr int K = decltype(kk)::value;
-    w[K] = w[K] * bc<K>(rs);
+    w[K] = apply_rs(w[K], bc<K>(rs));
     const T nz = -w[K];
     sfor<0, K>([&](auto i) {
       constexpr int I = decltype(i)::value;
@@ -209,6 +236,29 @@ __device__ __forceinline__ void symmetrize_lower(T (&M)[12], const int lane) {
   });
 }
 
+// Column-owned M made exactly symmetric as (M + M')/2: the pair (I, J) of entries is
+// averaged from both lanes' broadcasts, so lane J's M[I] and lane I's M[J] receive the same
+// value (each pair is touched once, no source is read after it changed).
+template <typename T>
+__device__ __forceinline__ void symmetrize_avg(T (&M)[12], const int lane) {
+  sfor<1, 12>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    sfor<0, J>([&](auto ii) {
+      constexpr int I = decltype(ii)::value;
+      const T lo = bc<I>(M[J]);  // M[J][I] (lane I's column, row J)
+      const T up = bc<J>(M[I]);  // M[I][J]
+      const T v = T(0.5) * (lo + up);
+      M[I] = lane == J ? v : M[I];
+      M[J] = lane == I ? v : M[J];
+    });
+    SRBD_PHASE_FENCE();
+  });
+}
+
+#ifndef SRBD_SYM_AVG
+#define SRBD_SYM_AVG 0
+#endif
+
 // The common tail of both step variants: given L = chol(G) and the column-owned
 // H (VL: g) and F (VL: f) of the stage,
 //   Y = L^-1 H, K = -L^-T Y, P_k = F - Y'Y (VL: p_k = f - Y'y).
@@ -249,7 +299,11 @@ __device__ __forceinline__ void riccati_tail(const int lane, StageFactor<T>& o, 
   tstamp(10);
   if constexpr (SYMP) {
     SRBD_PHASE_FENCE();
-    symmetrize_lower(o.F, lane);  // (B dead here: fewer live registers)
+    if constexpr (SRBD_SYM_AVG) {
+      symmetrize_avg(o.F, lane);
+    } else {
+      symmetrize_lower(o.F, lane);  // (B dead here: fewer live registers)
+    }
   }
 }
 
@@ -368,7 +422,7 @@ __device__ __forceinline__ void sqrt_factor(T (&P)[12], const int lane) {
   sfor<0, 12>([&](auto i) {
     constexpr int I = decltype(i)::value;
     const T ri = bc<I>(rs);
-    if (isv) P[I] *= ri;
+    if (isv) P[I] = apply_rs(P[I], ri);
     else if (lane > I) P[I] = T(0);
   });
 }

@@ -82,10 +82,11 @@ __device__ __forceinline__ void lat_chol(double (&G)[12], const int lane, const 
     });
     dmine = lane == K ? dk : dmine;
   });
-  rs = dmine > 0.0 ? 1.0 / __builtin_sqrt(dmine) : 0.0;
+  double inv_l;
+  pivot_rs(dmine, rs, inv_l);
   sfor<0, 12>([&](auto i) {
     constexpr int I = decltype(i)::value;
-    Lc[I] = G[I] * rs;
+    Lc[I] = G[I] * inv_l;
   });
 }
 

@@ -729,9 +729,13 @@ struct Field {
 };
 }  // namespace
 
+// stage_d / stage_s set (srbd_qp_host_staging_*): only lay out the pinned staging buffer for
+// the fields d / s mark and return pointers into it, so a caller can pack its QPs in place.
+// A host pointer that already is its field's place in the staging buffer is not copied.
 template <typename T, typename DataT, typename SolT>
 static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
-                           const DataT* d, const SolT* s) {
+                           const DataT* d, const SolT* s, DataT* stage_d = nullptr,
+                           SolT* stage_s = nullptr) {
   int rc = validate_call(h, batch, st, d, s);
   if (rc) return rc;
   if (batch == 0) return SRBD_QP_OK;
@@ -811,6 +815,28 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
     }
     pin = reinterpret_cast<char*>(h->pinned);
   }
+  if (stage_d) {
+    hipSetDevice(prev);
+    if (e != hipSuccess)
+      return fail(SRBD_QP_ENOMEM, std::string("host staging: ") + hipGetErrorString(e));
+    if (!small) return fail(SRBD_QP_ECAPACITY, "host staging: the batch's buffers exceed the pinned staging size");
+    auto hp = [&](size_t o) -> T* { return o == (size_t)-1 ? nullptr : reinterpret_cast<T*>(pin + o); };
+    auto hi = [&](size_t o) -> int* { return o == (size_t)-1 ? nullptr : reinterpret_cast<int*>(pin + o); };
+    DataT& dd = *stage_d;
+    dd = DataT{};
+    dd.A = hp(oA); dd.B = hp(oB); dd.b = hp(ob); dd.Q = hp(oQ); dd.S = hp(oS); dd.R = hp(oR);
+    dd.q = hp(oq); dd.r = hp(orr); dd.x0 = hp(ox0);
+    dd.lbu = hp(olbu); dd.ubu = hp(oubu); dd.lbu_mask = hp(olbum); dd.ubu_mask = hp(oubum);
+    dd.lbx = hp(olbx); dd.ubx = hp(oubx); dd.lbx_mask = hp(olbxm); dd.ubx_mask = hp(oubxm);
+    dd.C = hp(oC); dd.D = hp(oD); dd.lg = hp(olg); dd.ug = hp(oug); dd.lg_mask = hp(olgm);
+    dd.ug_mask = hp(ougm);
+    SolT& ss = *stage_s;
+    ss = SolT{};
+    ss.x = hp(ox); ss.u = hp(ou); ss.pi = hp(opi); ss.P = hp(oP); ss.p = hp(op); ss.K = hp(oK);
+    ss.k = hp(ok); ss.status = hi(ost); ss.iter = hi(oit); ss.res = hp(ores); ss.obj = hp(oobj);
+    ss.stat = hp(ostat);
+    return SRBD_QP_OK;
+  }
   // Zero copy: when the launch reads each QP's data exactly once (the single-QP kernel's
   // copy into LDS) and writes each output once, the kernel reads the pinned staging buffer
   // over PCIe and writes its outputs straight into it -- no DMA either way, one launch, one
@@ -836,7 +862,8 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
     if (e == hipSuccess) base = reinterpret_cast<char*>(dev);
   }
   if (e == hipSuccess && small) {
-    for (const Field& f : in) std::memcpy(pin + f.off, f.host, f.bytes);
+    for (const Field& f : in)
+      if (f.host != pin + f.off) std::memmove(pin + f.off, f.host, f.bytes);  // (staged in place: no copy)
     if (!zero_copy) e = hipMemcpyAsync(base, pin, in_end, hipMemcpyHostToDevice, h->stream);
   }
   for (size_t i = 0; !small && e == hipSuccess && i < in.size(); ++i)
@@ -845,8 +872,8 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
   if (e == hipSuccess && st->warm_start) {
     const size_t bx = B * (N + 1) * nx * D, bu = B * N * nu * D;
     if (small) {
-      std::memcpy(pin + ox, s->x, bx);
-      std::memcpy(pin + ou, s->u, bu);
+      if ((const void*)s->x != pin + ox) std::memmove(pin + ox, s->x, bx);
+      if ((const void*)s->u != pin + ou) std::memmove(pin + ou, s->u, bu);
       // x and u are adjacent in the staging layout (addo order, 256-byte aligned)
       if (!zero_copy) e = hipMemcpyAsync(base + ox, pin + ox, ou + bu - ox, hipMemcpyHostToDevice, h->stream);
     } else {
@@ -890,7 +917,7 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
       e = hipMemcpyAsync(pin + in_end, base + in_end, off - in_end, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)
-      std::memcpy(outs[i].host, pin + outs[i].off, outs[i].bytes);
+      if (outs[i].host != pin + outs[i].off) std::memmove(outs[i].host, pin + outs[i].off, outs[i].bytes);
   } else {
     for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)
       e = hipMemcpyAsync(outs[i].host, base + outs[i].off, outs[i].bytes, hipMemcpyDeviceToHost, h->stream);
@@ -910,6 +937,13 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
 int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                            const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s) {
   return solve_host_impl<double>(h, batch, st, d, s);
+}
+int srbd_qp_host_staging_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                             srbd_qp_data_f64* d, srbd_qp_solution_f64* s) {
+  if (!d || !s) return fail(SRBD_QP_EINVAL, "host staging: data / solution struct is NULL");
+  const srbd_qp_data_f64 want = *d;
+  const srbd_qp_solution_f64 want_s = *s;
+  return solve_host_impl<double>(h, batch, st, &want, &want_s, d, s);
 }
 void srbd_qp_srbd_default_params(srbd_model_params* p) {
   if (!p) return;

@@ -44,15 +44,22 @@ namespace {
   throw std::runtime_error(std::string(what) + ": " + srbd_qp_last_error());
 }
 
-void copy_block(std::vector<double>& dst, size_t off, const double* src, size_t n) {
-  if (n) std::memcpy(dst.data() + off, src, n * sizeof(double));
+void copy_block(double* dst, size_t off, const double* src, size_t n) {
+  if (n) std::memcpy(dst + off, src, n * sizeof(double));
 }
 
 // rows x cols column-major src (ld = rows) into dst at off with leading dimension ld
+void copy_mat(double* dst, size_t off, size_t ld, const double* src, size_t rows, size_t cols) {
+  if (rows == ld) {  // contiguous columns: one copy
+    if (rows && cols) std::memcpy(dst + off, src, rows * cols * sizeof(double));
+    return;
+  }
+  for (size_t c = 0; c < cols; ++c)
+    if (rows) std::memcpy(dst + off + c * ld, src + c * rows, rows * sizeof(double));
+}
 void copy_mat(std::vector<double>& dst, size_t off, size_t ld, const double* src, size_t rows,
               size_t cols) {
-  for (size_t c = 0; c < cols; ++c)
-    if (rows) std::memcpy(dst.data() + off + c * ld, src + c * rows, rows * sizeof(double));
+  copy_mat(dst.data(), off, ld, src, rows, cols);
 }
 // the leading rows x cols block of a column-major ld x * src into dst (ld = rows)
 void take_mat(double* dst, const double* src, size_t ld, size_t rows, size_t cols) {
@@ -216,25 +223,61 @@ struct OcpQpIpmSolver::Impl {
     return s;
   }
 
+  // Where pack() writes the unconstrained fields and unpack() reads the outputs: the vectors
+  // above, or the C-ABI's pinned staging buffer (srbd_qp_host_staging_f64), which the kernel
+  // then reads and writes in place -- no staging copies on the reference's one-QP path.
+  struct Bufs {
+    double *A = nullptr, *B = nullptr, *b = nullptr, *Q = nullptr, *S = nullptr, *R = nullptr,
+           *q = nullptr, *r = nullptr, *x0 = nullptr;
+    double *x = nullptr, *u = nullptr, *pi = nullptr, *P = nullptr, *p = nullptr, *K = nullptr,
+           *k = nullptr, *res = nullptr, *obj = nullptr, *stat = nullptr;
+    int *status = nullptr, *iter = nullptr;
+  };
+  Bufs buf;  // bound by pack()
+
   void pack(const std::vector<VectorXd>& x0s, const std::vector<std::vector<OcpQp>>& qps,
-            const std::vector<std::vector<OcpQpSolution>>* warm);
+            const std::vector<std::vector<OcpQpSolution>>* warm, const Bufs* staged = nullptr);
   std::vector<HpipmStatus> unpack(std::vector<std::vector<OcpQpSolution>>& sols);
 };
 
 void OcpQpIpmSolver::Impl::pack(const std::vector<VectorXd>& x0s,
                                 const std::vector<std::vector<OcpQp>>& qps,
-                                const std::vector<std::vector<OcpQpSolution>>* warm) {
+                                const std::vector<std::vector<OcpQpSolution>>* warm,
+                                const Bufs* staged) {
   const size_t nb = qps.size(), N = shape.N, nx = shape.nx, nu = shape.nu, ng = shape.ng;
   auto sized = [](std::vector<double>& v, size_t n) { v.assign(n, 0.0); };
-  sized(A, nb * N * nx * nx);
-  sized(B, nb * N * nx * nu);
-  sized(b, nb * N * nx);
-  sized(Q, nb * (N + 1) * nx * nx);
-  sized(S, nb * N * nu * nx);
-  sized(R, nb * N * nu * nu);
-  sized(q, nb * (N + 1) * nx);
-  sized(r, nb * N * nu);
-  sized(x0, nb * nx);
+  // every stage at the uniform dims: each input element is written below, no zero fill needed
+  bool uniform = true;
+  for (unsigned int i = 0; i <= dim.N; ++i)
+    uniform = uniform && static_cast<size_t>(dim.nx[i]) == nx && (i == dim.N || static_cast<size_t>(dim.nu[i]) == nu);
+  if (staged) {
+    buf = *staged;
+    if (!uniform) {
+      auto zero = [](double* p, size_t n) { std::memset(p, 0, n * sizeof(double)); };
+      zero(buf.A, nb * N * nx * nx);
+      zero(buf.B, nb * N * nx * nu);
+      zero(buf.b, nb * N * nx);
+      zero(buf.Q, nb * (N + 1) * nx * nx);
+      zero(buf.S, nb * N * nu * nx);
+      zero(buf.R, nb * N * nu * nu);
+      zero(buf.q, nb * (N + 1) * nx);
+      zero(buf.r, nb * N * nu);
+      zero(buf.x0, nb * nx);
+    }
+  } else {
+    sized(A, nb * N * nx * nx);
+    sized(B, nb * N * nx * nu);
+    sized(b, nb * N * nx);
+    sized(Q, nb * (N + 1) * nx * nx);
+    sized(S, nb * N * nu * nx);
+    sized(R, nb * N * nu * nu);
+    sized(q, nb * (N + 1) * nx);
+    sized(r, nb * N * nu);
+    sized(x0, nb * nx);
+    buf = Bufs{};
+    buf.A = A.data(); buf.B = B.data(); buf.b = b.data(); buf.Q = Q.data(); buf.S = S.data();
+    buf.R = R.data(); buf.q = q.data(); buf.r = r.data(); buf.x0 = x0.data();
+  }
   if (shape.box_u) {
     for (auto* v : {&lbu, &ubu, &lbu_m, &ubu_m}) sized(*v, nb * N * nu);
   }
@@ -251,23 +294,23 @@ void OcpQpIpmSolver::Impl::pack(const std::vector<VectorXd>& x0s,
     const std::vector<OcpQp>& qp = qps[bi];
     if (static_cast<size_t>(x0s[bi].size()) != nx0)
       throw std::runtime_error("x0.size() must be " + std::to_string(nx0));
-    copy_block(x0, bi * nx, x0s[bi].data(), nx0);
+    copy_block(buf.x0, bi * nx, x0s[bi].data(), nx0);
     for (size_t k = 0; k <= N; ++k) {
       const OcpQp& s = qp[k];
       const size_t sk = bi * (N + 1) + k;  // stage index, N+1 stages
       const size_t xk = static_cast<size_t>(dim.nx[k]);  // this stage's dimensions
-      copy_mat(Q, sk * nx * nx, nx, s.Q.data(), xk, xk);
-      copy_block(q, sk * nx, s.q.data(), xk);
+      copy_mat(buf.Q, sk * nx * nx, nx, s.Q.data(), xk, xk);
+      copy_block(buf.q, sk * nx, s.q.data(), xk);
       if (k < N) {
         const size_t si = bi * N + k;  // stage index, N stages
         const size_t uk = static_cast<size_t>(dim.nu[k]), xn = static_cast<size_t>(dim.nx[k + 1]);
-        copy_mat(A, si * nx * nx, nx, s.A.data(), xn, xk);
-        copy_mat(B, si * nx * nu, nx, s.B.data(), xn, uk);
-        copy_block(b, si * nx, s.b.data(), xn);
-        copy_mat(S, si * nu * nx, nu, s.S.data(), uk, xk);
-        copy_mat(R, si * nu * nu, nu, s.R.data(), uk, uk);
-        for (size_t j = uk; j < nu; ++j) R[si * nu * nu + j * nu + j] = 1.0;  // embedded inputs
-        copy_block(r, si * nu, s.r.data(), uk);
+        copy_mat(buf.A, si * nx * nx, nx, s.A.data(), xn, xk);
+        copy_mat(buf.B, si * nx * nu, nx, s.B.data(), xn, uk);
+        copy_block(buf.b, si * nx, s.b.data(), xn);
+        copy_mat(buf.S, si * nu * nx, nu, s.S.data(), uk, xk);
+        copy_mat(buf.R, si * nu * nu, nu, s.R.data(), uk, uk);
+        for (size_t j = uk; j < nu; ++j) buf.R[si * nu * nu + j * nu + j] = 1.0;  // embedded inputs
+        copy_block(buf.r, si * nu, s.r.data(), uk);
         if (shape.box_u) {
           // index form -> dense per-variable bounds + masks (include/srbd_qp.h)
           for (size_t j = 0; j < s.idxbu.size(); ++j) {
@@ -313,25 +356,35 @@ void OcpQpIpmSolver::Impl::pack(const std::vector<VectorXd>& x0s,
       }
     }
   }
-  // outputs (x/u double as the warm start when settings.warm_start)
-  sized(x, nb * (N + 1) * nx);
-  sized(u, nb * N * nu);
-  sized(pi, nb * (N + 1) * nx);
-  sized(P, nb * (N + 1) * nx * nx);
-  sized(p, nb * (N + 1) * nx);
-  sized(K, nb * N * nu * nx);
-  sized(k, nb * N * nu);
-  sized(res, nb * 4);
-  sized(obj, nb);
-  sized(stat, nb * (settings.iter_max + 2) * 18);
-  status.assign(nb, -1);
-  iter.assign(nb, 0);
+  // outputs (x/u double as the warm start when settings.warm_start); the staged ones are
+  // written whole by the solve
+  if (!staged) {
+    sized(x, nb * (N + 1) * nx);
+    sized(u, nb * N * nu);
+    sized(pi, nb * (N + 1) * nx);
+    sized(P, nb * (N + 1) * nx * nx);
+    sized(p, nb * (N + 1) * nx);
+    sized(K, nb * N * nu * nx);
+    sized(k, nb * N * nu);
+    sized(res, nb * 4);
+    sized(obj, nb);
+    sized(stat, nb * (settings.iter_max + 2) * 18);
+    status.assign(nb, -1);
+    iter.assign(nb, 0);
+    buf.x = x.data(); buf.u = u.data(); buf.pi = pi.data(); buf.P = P.data(); buf.p = p.data();
+    buf.K = K.data(); buf.k = k.data(); buf.res = res.data(); buf.obj = obj.data();
+    buf.stat = stat.data(); buf.status = status.data(); buf.iter = iter.data();
+  }
   if (warm) {
+    if (staged && !uniform) {
+      std::memset(buf.x, 0, nb * (N + 1) * nx * sizeof(double));
+      std::memset(buf.u, 0, nb * N * nu * sizeof(double));
+    }
     for (size_t bi = 0; bi < nb; ++bi) {
       const std::vector<OcpQpSolution>& w = (*warm)[bi];
       for (size_t kk = 0; kk < N; ++kk) {
-        copy_block(x, (bi * (N + 1) + kk + 1) * nx, w[kk + 1].x.data(), static_cast<size_t>(dim.nx[kk + 1]));
-        copy_block(u, (bi * N + kk) * nu, w[kk].u.data(), static_cast<size_t>(dim.nu[kk]));
+        copy_block(buf.x, (bi * (N + 1) + kk + 1) * nx, w[kk + 1].x.data(), static_cast<size_t>(dim.nx[kk + 1]));
+        copy_block(buf.u, (bi * N + kk) * nu, w[kk].u.data(), static_cast<size_t>(dim.nu[kk]));
       }
     }
   }
@@ -353,28 +406,28 @@ std::vector<HpipmStatus> OcpQpIpmSolver::Impl::unpack(
       s.pi.resize(xk);
       s.P.resize(xk, xk);
       s.p.resize(xk);
-      std::memcpy(s.x.data(), x.data() + sk * nx, xk * sizeof(double));
-      std::memcpy(s.pi.data(), pi.data() + sk * nx, xk * sizeof(double));
-      take_mat(s.P.data(), P.data() + sk * nx * nx, nx, xk, xk);
-      std::memcpy(s.p.data(), p.data() + sk * nx, xk * sizeof(double));
+      std::memcpy(s.x.data(), buf.x + sk * nx, xk * sizeof(double));
+      std::memcpy(s.pi.data(), buf.pi + sk * nx, xk * sizeof(double));
+      take_mat(s.P.data(), buf.P + sk * nx * nx, nx, xk, xk);
+      std::memcpy(s.p.data(), buf.p + sk * nx, xk * sizeof(double));
       if (kk < N) {
         const size_t si = bi * N + kk, uk = static_cast<size_t>(dim.nu[kk]);
         s.u.resize(uk);
         s.K.resize(uk, xk);
         s.k.resize(uk);
-        std::memcpy(s.u.data(), u.data() + si * nu, uk * sizeof(double));
-        take_mat(s.K.data(), K.data() + si * nu * nx, nu, uk, xk);
-        std::memcpy(s.k.data(), k.data() + si * nu, uk * sizeof(double));
+        std::memcpy(s.u.data(), buf.u + si * nu, uk * sizeof(double));
+        take_mat(s.K.data(), buf.K + si * nu * nx, nu, uk, xk);
+        std::memcpy(s.k.data(), buf.k + si * nu, uk * sizeof(double));
       } else {
         s.k.resize(0);  // nu[N] = 0 (ocp_qp_ipm_solver.cpp:221-223)
       }
     }
     OcpQpIpmSolverStatistics& st = batch_stats[bi];
-    st.iter = iter[bi];
-    st.max_res_stat = res[bi * 4 + 0];
-    st.max_res_eq = res[bi * 4 + 1];
-    st.max_res_ineq = res[bi * 4 + 2];
-    st.max_res_comp = res[bi * 4 + 3];
+    st.iter = buf.iter[bi];
+    st.max_res_stat = buf.res[bi * 4 + 0];
+    st.max_res_eq = buf.res[bi * 4 + 1];
+    st.max_res_ineq = buf.res[bi * 4 + 2];
+    st.max_res_comp = buf.res[bi * 4 + 3];
     st.clear();
     const size_t nrow = std::min(rows, static_cast<size_t>(st.iter) + 2);
     st.reserve(nrow);
@@ -384,8 +437,8 @@ std::vector<HpipmStatus> OcpQpIpmSolver::Impl::unpack(
         &st.itref_pred, &st.itref_corr, &st.lin_res_stat, &st.lin_res_eq, &st.lin_res_ineq,
         &st.lin_res_comp};
     for (size_t i = 0; i < nrow; ++i)
-      for (size_t c = 0; c < 18; ++c) cols[c]->push_back(stat[(bi * rows + i) * 18 + c]);
-    const int code = status[bi];
+      for (size_t c = 0; c < 18; ++c) cols[c]->push_back(buf.stat[(bi * rows + i) * 18 + c]);
+    const int code = buf.status[bi];
     out[bi] = (code >= 0 && code <= 3) ? static_cast<HpipmStatus>(code) : HpipmStatus::UnknownFailure;
   }
   if (nb) stats = batch_stats[0];
@@ -478,9 +531,37 @@ std::vector<HpipmStatus> OcpQpIpmSolver::solveBatch(
                                    std::to_string(m.dim.nu[i]));
     }
   }
+  const srbd_qp_settings st = m.abi_settings();
+  // Unconstrained QPs (the reference's NMPC QP) are packed straight into the C-ABI's pinned
+  // staging buffer: the solve then makes no staging copy (and, for up to 256 QPs, the kernel
+  // reads and writes that buffer in place).
+  srbd_qp_data_f64 d{};
+  srbd_qp_solution_f64 o{};
+  bool staged = false;
+  if (!s.ng && !s.box_u && !s.box_x) {
+    const double* mk = reinterpret_cast<const double*>(16);  // "wanted" markers
+    double* mo = const_cast<double*>(mk);
+    d.A = d.B = d.b = d.Q = d.S = d.R = d.q = d.r = d.x0 = mk;
+    o.x = o.u = o.pi = o.P = o.p = o.K = o.k = o.res = o.obj = o.stat = mo;
+    o.status = o.iter = reinterpret_cast<int*>(16);
+    staged = srbd_qp_host_staging_f64(m.handle, nb, &st, &d, &o) == SRBD_QP_OK;
+    if (staged) {
+      Impl::Bufs bs;
+      bs.A = const_cast<double*>(d.A); bs.B = const_cast<double*>(d.B); bs.b = const_cast<double*>(d.b);
+      bs.Q = const_cast<double*>(d.Q); bs.S = const_cast<double*>(d.S); bs.R = const_cast<double*>(d.R);
+      bs.q = const_cast<double*>(d.q); bs.r = const_cast<double*>(d.r); bs.x0 = const_cast<double*>(d.x0);
+      bs.x = o.x; bs.u = o.u; bs.pi = o.pi; bs.P = o.P; bs.p = o.p; bs.K = o.K; bs.k = o.k;
+      bs.res = o.res; bs.obj = o.obj; bs.stat = o.stat; bs.status = o.status; bs.iter = o.iter;
+      m.pack(x0, ocp_qp, m.settings.warm_start ? &qp_sol : nullptr, &bs);
+      if (srbd_qp_solve_host_f64(m.handle, nb, &st, &d, &o) != SRBD_QP_OK)
+        abi_error("OcpQpIpmSolver::solve");
+      return m.unpack(qp_sol);
+    }
+    d = srbd_qp_data_f64{};
+    o = srbd_qp_solution_f64{};
+  }
   m.pack(x0, ocp_qp, m.settings.warm_start ? &qp_sol : nullptr);
   auto ptr = [](std::vector<double>& v) -> double* { return v.empty() ? nullptr : v.data(); };
-  srbd_qp_data_f64 d{};
   d.A = m.A.data(); d.B = m.B.data(); d.b = m.b.data();
   d.Q = m.Q.data(); d.S = m.S.data(); d.R = m.R.data();
   d.q = m.q.data(); d.r = m.r.data(); d.x0 = m.x0.data();
@@ -498,12 +579,10 @@ std::vector<HpipmStatus> OcpQpIpmSolver::solveBatch(
     d.D = ptr(m.D); d.lg = ptr(m.lg); d.ug = ptr(m.ug);
     d.lg_mask = ptr(m.lg_m); d.ug_mask = ptr(m.ug_m);
   }
-  srbd_qp_solution_f64 o{};
   o.x = m.x.data(); o.u = m.u.data(); o.pi = m.pi.data();
   o.P = m.P.data(); o.p = m.p.data(); o.K = m.K.data(); o.k = m.k.data();
   o.status = m.status.data(); o.iter = m.iter.data(); o.res = m.res.data(); o.obj = m.obj.data();
   o.stat = m.stat.data();
-  const srbd_qp_settings st = m.abi_settings();
   if (srbd_qp_solve_host_f64(m.handle, nb, &st, &d, &o) != SRBD_QP_OK)
     abi_error("OcpQpIpmSolver::solve");
   return m.unpack(qp_sol);
