@@ -7,3 +7,4 @@ done
 SRBD_QP_LIB=$V/tstamp/libsrbd_qp.so timeout -k 10 120 python scripts/dev/latency_breakdown.py > gpurun_out/r4/lat_breakdown.json 2>&1 || exit 1
 timeout -k 10 120 bash scripts/dev/r4_cp_prof.sh > gpurun_out/r4/cp_prof.txt 2>&1 || exit 1
 timeout -k 10 120 python scripts/dev/call_pattern.py > gpurun_out/r4/call_pattern_new2.json 2>&1
+LD_LIBRARY_PATH=$V/block SRBD_QP_LIB=$V/block/libsrbd_qp.so timeout -k 10 120 python scripts/dev/call_pattern.py > gpurun_out/r4/call_pattern_block.json 2>&1

@@ -111,9 +111,10 @@ def lib():
         L.srbd_qp_solve_host_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
                                              C.POINTER(Data), C.POINTER(Solution)]
         L.srbd_qp_solve_host_f64.restype = C.c_int
-        L.srbd_qp_host_staging_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
-                                               C.POINTER(Data), C.POINTER(Solution)]
-        L.srbd_qp_host_staging_f64.restype = C.c_int
+        if hasattr(L, "srbd_qp_host_staging_f64"):  # ABI 10 (older builds: A/B runs)
+            L.srbd_qp_host_staging_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
+                                                   C.POINTER(Data), C.POINTER(Solution)]
+            L.srbd_qp_host_staging_f64.restype = C.c_int
         L.srbd_qp_solve_f32.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
                                         C.POINTER(Data32), C.POINTER(Solution32), C.c_void_p]
         L.srbd_qp_solve_f32.restype = C.c_int

@@ -68,11 +68,16 @@ __device__ __forceinline__ double lat_recip(double d) {
   e = __builtin_fma(-d, r, 1.0);
   return __builtin_fma(r, e, r);
 }
+// `hook(ic<K>)` runs at the top of pivot K: the caller issues its independent matrix-core
+// work there, one MFMA per pivot, so the MFMA pipe runs beside the pivots' VALU chain
+// instead of ahead of it (a wave cannot issue past an MFMA the pipe has not accepted).
+template <typename Hook>
 __device__ __forceinline__ void lat_chol(double (&G)[12], const int lane, const double reg, double (&Lc)[12],
-                                         double& rs) {
+                                         double& rs, Hook&& hook) {
   double dmine = 1.0;
   sfor<0, 12>([&](auto kk) {
     constexpr int K = decltype(kk)::value;
+    hook(kk);
     const double dk = bc<K>(G[K]) + reg;
     const double inv = dk > 0.0 ? lat_recip(dk) : 0.0;
     const double s = lane > K ? G[K] * inv : 0.0;
@@ -186,21 +191,29 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
         St[R] = rok && cw ? sv : 0.0;
         Qt[R] = rok && cw ? qv : 0.0;
       });
-      // WB = P B; G = R + B'WB
+      // WB = P B; G = R + B'WB (the critical path)
       lat_d4 WB = {0.0, 0.0, 0.0, 0.0};
       sfor<0, 3>([&](auto kb) { WB = lat_mfma(Pt[decltype(kb)::value], bo[decltype(kb)::value], WB); });
       lat_d4 Gt = Rt;
       sfor<0, 3>([&](auto kb) { Gt = lat_mfma(bo[decltype(kb)::value], WB[decltype(kb)::value], Gt); });
-      // W = P [A | b] + [0 | p]; [H | g] = [S | r] + B'W; [F | f] = [Q | q] + A'W
+      // W = P [A | b] + [0 | p]; [H | g] = [S | r] + B'W; [F | f] = [Q | q] + A'W: issued one
+      // per pivot inside the Cholesky below (W0 W1 W2 H0 F0 H1 F1 H2 F2)
       lat_d4 Wt;
       sfor<0, 4>([&](auto rr) { Wt[decltype(rr)::value] = c == 12 ? Pt[decltype(rr)::value] : 0.0; });
-      sfor<0, 3>([&](auto kb) { Wt = lat_mfma(Pt[decltype(kb)::value], ao[decltype(kb)::value], Wt); });
       lat_d4 Ht = St, Ft = Qt;
-      sfor<0, 3>([&](auto kb) {
-        constexpr int KB = decltype(kb)::value;
-        Ht = lat_mfma(bo[KB], Wt[KB], Ht);
-        Ft = lat_mfma(ao[KB], Wt[KB], Ft);
-      });
+      auto wh = [&](auto kk) {
+        constexpr int K = decltype(kk)::value;
+        if constexpr (K < 3) {
+          Wt = lat_mfma(Pt[K], ao[K], Wt);
+        } else if constexpr (K < 9) {
+          constexpr int KB = (K - 3) / 2;
+          if constexpr ((K - 3) % 2 == 0) {
+            Ht = lat_mfma(bo[KB], Wt[KB], Ht);
+          } else {
+            Ft = lat_mfma(ao[KB], Wt[KB], Ft);
+          }
+        }
+      };
       tstamp(1);
       // G to column-owned registers through LDS, Cholesky
       lds_wave_fence();
@@ -214,7 +227,7 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
         const double v = gh[cc * 12 + decltype(i)::value];
         Gc[decltype(i)::value] = cv ? v : 0.0;
       });
-      lat_chol(Gc, c, a.reg, Lc, rs);
+      lat_chol(Gc, c, a.reg, Lc, rs, wh);
       tstamp(3);
       // [Y | y] = L^-1 [H | g]
       lds_wave_fence();

@@ -719,6 +719,9 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
 // ---------------------------------------------------------------------------
 // host-buffer convenience path
 // ---------------------------------------------------------------------------
+#ifndef SRBD_SPIN_WAIT
+#define SRBD_SPIN_WAIT 1
+#endif
 namespace {
 // host solves whose staged bytes fit this go through the handle's pinned buffer
 constexpr size_t kPinnedMaxBytes = size_t(8) << 20;
@@ -915,6 +918,13 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
   if (small) {
     if (e == hipSuccess && in_end < off && !zero_copy)
       e = hipMemcpyAsync(pin + in_end, base + in_end, off - in_end, hipMemcpyDeviceToHost, h->stream);
+    // The single-QP launch is a few tens of microseconds: poll for it instead of the blocking
+    // wait, whose wake-up costs about as much as the kernel (-DSRBD_SPIN_WAIT=0: block).
+    if (e == hipSuccess && zero_copy && SRBD_SPIN_WAIT) {
+      hipError_t q;
+      while ((q = hipStreamQuery(h->stream)) == hipErrorNotReady) __builtin_ia32_pause();
+      if (q != hipSuccess) e = q;
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)
       if (outs[i].host != pin + outs[i].off) std::memmove(outs[i].host, pin + outs[i].off, outs[i].bytes);
