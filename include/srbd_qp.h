@@ -345,6 +345,32 @@ int srbd_qp_srbd_nmpc_f64(srbd_qp_handle h, int batch, const srbd_model_params* 
                           int constraints, int sqp_max_loop, double* xs, double* us,
                           const double* x0, double* alpha, int* sqp_iter, int* converged);
 
+/* ------------------------------------------------------------------------
+ * One solver over several devices, driven from one host thread (SURVEY.md 5,
+ * "one process, 8 devices"; BASELINE config 4: a batch sharded over 8 MI355X
+ * with the solutions gathered to one device).  A handle per device; the
+ * shards' solves are all queued before any is waited for, and x, u, pi are
+ * gathered to the root device (devices[0]) by peer copies over xGMI, each
+ * behind its shard's solve on that shard's stream.  (ABI 10)
+ * ---------------------------------------------------------------------- */
+typedef struct srbd_qp_multi_s* srbd_qp_multi;
+
+/* A handle of `capacity_per_device` QPs on each of devices[0..ndev) (a device
+ * may repeat: two shards on one GPU).  Peer access root <-> shard is enabled
+ * where the devices support it.                                              */
+int srbd_qp_multi_create(const srbd_qp_dims* dims, int capacity_per_device, const int* devices,
+                         int ndev, srbd_qp_multi* out);
+void srbd_qp_multi_destroy(srbd_qp_multi m);
+/* Shard i's handle (its stream, workspace size, ...); NULL past the end.    */
+srbd_qp_handle srbd_qp_multi_handle(srbd_qp_multi m, int i);
+/* Shard i: batch[i] QPs with data[i] / sol[i] in devices[i]'s memory.  Every
+ * shard is solved with `settings`; then, when root_x / root_u / root_pi are
+ * given (root-device memory for sum(batch) QPs, the C-ABI layout), the shards'
+ * x, u, pi land there in shard order.  Returns when all of it has finished. */
+int srbd_qp_multi_solve_f64(srbd_qp_multi m, const int* batch, const srbd_qp_settings* settings,
+                            const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol,
+                            double* root_x, double* root_u, double* root_pi);
+
 /* Blocks until all work queued on the handle's stream is done.            */
 int srbd_qp_synchronize(srbd_qp_handle h);
 

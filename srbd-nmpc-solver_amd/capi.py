@@ -111,6 +111,18 @@ def lib():
         L.srbd_qp_solve_host_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
                                              C.POINTER(Data), C.POINTER(Solution)]
         L.srbd_qp_solve_host_f64.restype = C.c_int
+        if hasattr(L, "srbd_qp_multi_create"):  # ABI 10
+            L.srbd_qp_multi_create.argtypes = [C.POINTER(Dims), C.c_int, C.POINTER(C.c_int), C.c_int,
+                                               C.POINTER(C.c_void_p)]
+            L.srbd_qp_multi_create.restype = C.c_int
+            L.srbd_qp_multi_destroy.argtypes = [C.c_void_p]
+            L.srbd_qp_multi_destroy.restype = None
+            L.srbd_qp_multi_handle.argtypes = [C.c_void_p, C.c_int]
+            L.srbd_qp_multi_handle.restype = C.c_void_p
+            L.srbd_qp_multi_solve_f64.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(Settings),
+                                                  C.POINTER(Data), C.POINTER(Solution), C.c_void_p,
+                                                  C.c_void_p, C.c_void_p]
+            L.srbd_qp_multi_solve_f64.restype = C.c_int
         if hasattr(L, "srbd_qp_host_staging_f64"):  # ABI 10 (older builds: A/B runs)
             L.srbd_qp_host_staging_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
                                                    C.POINTER(Data), C.POINTER(Solution)]
@@ -257,6 +269,41 @@ class Handle:
         if getattr(self, "_h", None):
             lib().srbd_qp_destroy(self._h)
             self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Multi:
+    """srbd_qp_multi: one solver over several devices from one thread (a handle per
+    device; shards solved concurrently, x / u / pi gathered to devices[0] by peer copies)."""
+
+    def __init__(self, N: int, nx: int, nu: int, devices, ng: int = 0, has_box_u: bool = False,
+                 has_box_x: bool = False, capacity: int = 1):
+        self.dims = Dims(N, nx, nu, ng, int(has_box_u), int(has_box_x), 0)
+        self.devices = list(devices)
+        arr = (C.c_int * len(self.devices))(*self.devices)
+        m = C.c_void_p()
+        check(lib().srbd_qp_multi_create(C.byref(self.dims), int(capacity), arr, len(self.devices),
+                                         C.byref(m)), "srbd_qp_multi_create")
+        self._m = m
+
+    def solve(self, batches, settings: Settings, datas, sols, root_x=None, root_u=None, root_pi=None):
+        n = len(self.devices)
+        b = (C.c_int * n)(*[int(x) for x in batches])
+        d = (Data * n)(*datas)
+        s = (Solution * n)(*sols)
+        ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        check(lib().srbd_qp_multi_solve_f64(self._m, b, C.byref(settings), d, s, ptr(root_x), ptr(root_u),
+                                            ptr(root_pi)), "srbd_qp_multi_solve_f64")
+
+    def close(self) -> None:
+        if getattr(self, "_m", None):
+            lib().srbd_qp_multi_destroy(self._m)
+            self._m = None
 
     def __del__(self):
         try:

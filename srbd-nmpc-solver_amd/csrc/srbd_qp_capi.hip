@@ -31,6 +31,11 @@ int fail(int code, const std::string& msg) {
 
 }  // namespace
 
+namespace srbd {
+// the thread's last-error message, for the other translation units of the ABI (multi.hip)
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace srbd
+
 struct srbd_qp_handle_s {
   srbd_qp_dims dims{};
   int capacity = 0;

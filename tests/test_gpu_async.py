@@ -71,3 +71,32 @@ def test_two_handles_overlap_from_one_thread(pkg):
         for key in ("x", "u", "status", "iter"):
             np.testing.assert_array_equal(st[key].cpu().numpy(), ref[key])
         h.close()
+
+
+def test_multi_device_shards_and_gather(pkg):
+    """srbd_qp_multi (one solver over several devices, one host thread): two shards -- both
+    on device 0 here, the pool's boxes have one GPU -- of 64 and 96 box-u QPs are solved
+    concurrently and their x, u, pi gathered to the root device in shard order by peer
+    copies; every QP equals the single-handle solve of the whole batch bit for bit."""
+    import torch
+    capi = pkg.capi
+    qp, x0 = pkg.srbd_model.generate_batch(160, N=20, seed=61, constraints="box_u")
+    ref = capi.solve(qp, x0, NMPC)
+    s = capi.settings_struct(NMPC)
+    shards = [(0, 64), (64, 160)]
+    m = capi.Multi(20, 12, 12, [0, 0], has_box_u=True, capacity=96)
+    keep, datas, sols = [], [], []
+    for lo, hi in shards:
+        dt, st, data, sol = capi.device_buffers(qp.subset(slice(lo, hi)), x0[lo:hi], "cuda:0")
+        keep.append((dt, st))
+        datas.append(data)
+        sols.append(sol)
+    f = dict(dtype=torch.float64, device="cuda:0")
+    rx, ru, rpi = torch.zeros(160, 21, 12, **f), torch.zeros(160, 20, 12, **f), torch.zeros(160, 21, 12, **f)
+    torch.cuda.synchronize()
+    m.solve([hi - lo for lo, hi in shards], s, datas, sols, rx, ru, rpi)
+    for key, t in (("x", rx), ("u", ru), ("pi", rpi)):
+        np.testing.assert_array_equal(t.cpu().numpy(), ref[key])
+    for (lo, hi), (_, st) in zip(shards, keep):
+        np.testing.assert_array_equal(st["status"].cpu().numpy(), ref["status"][lo:hi])
+    m.close()

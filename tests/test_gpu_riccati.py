@@ -326,3 +326,44 @@ def test_streaming_kernel_partial_waves(pkg, oracle, ric_alg):
         small = pkg.capi.solve(qp.subset(idx), x0[idx], st, riccati=True)
         for key in ("x", "u", "pi", "P", "p", "K", "k", "status"):
             assert np.array_equal(small[key], big[key][idx]), (key, nb)
+
+
+def test_host_staging_in_place(pkg):
+    """srbd_qp_host_staging_f64 (ABI 10): the staging pointers a caller packs its QPs into
+    and passes back to srbd_qp_solve_host_f64 are solved in place (no staging copy; for a
+    small unconstrained batch the kernel reads and writes the pinned buffer itself) and give
+    the device call's results bit for bit; a second staging call of the same shape returns
+    the same pointers."""
+    import ctypes as C
+    capi = pkg.capi
+    for nb in (1, 3):
+        qp, x0 = pkg.srbd_model.generate_batch(nb, N=20, seed=404 + nb, constraints="none")
+        dev = capi.solve(qp, x0, dict(ric_alg=0), riccati=True)
+        h = capi.Handle(20, 12, 12, capacity=nb)
+        try:
+            s = capi.settings_struct(dict(ric_alg=0))
+            mark = 16
+            d = capi.Data(**{k: mark for k in ("A", "B", "b", "Q", "S", "R", "q", "r", "x0")})
+            o = capi.Solution(**{k: mark for k in ("x", "u", "pi", "P", "p", "K", "k", "status", "iter", "res", "obj")})
+            h.host_staging(nb, s, d, o)
+            d2 = capi.Data(**{k: mark for k in ("A", "B", "b", "Q", "S", "R", "q", "r", "x0")})
+            o2 = capi.Solution(**{k: mark for k in ("x", "u", "pi", "P", "p", "K", "k", "status", "iter", "res", "obj")})
+            h.host_staging(nb, s, d2, o2)
+            assert d2.A == d.A and o2.stat == o.stat is None and o2.x == o.x
+            p = qp.packed()
+            p["x0"] = np.ascontiguousarray(x0)
+            for k in ("A", "B", "b", "Q", "S", "R", "q", "r", "x0"):
+                src = np.ascontiguousarray(p[k], dtype=np.float64)
+                C.memmove(getattr(d, k), src.ctypes.data, src.nbytes)
+            h.solve_host(nb, s, d, o)
+
+            def arr(ptr, shape, ct=C.c_double):
+                n = int(np.prod(shape))
+                return np.ctypeslib.as_array((ct * n).from_address(ptr)).reshape(shape).copy()
+            assert np.array_equal(arr(o.x, dev["x"].shape), dev["x"])
+            assert np.array_equal(arr(o.u, dev["u"].shape), dev["u"])
+            assert np.array_equal(arr(o.pi, dev["pi"].shape), dev["pi"])
+            assert np.array_equal(np.swapaxes(arr(o.K, (nb, 20, 12, 12)), -1, -2), dev["K"])
+            assert np.all(arr(o.status, (nb,), C.c_int) == 0)
+        finally:
+            h.close()
