@@ -33,7 +33,8 @@ for name in ("Q", "R", "S", "A", "B", "q", "r", "b", "C", "D", "lg", "ug", "lbu"
 fam = pkg.OcpQpBatch(N=qp.N, nx=qp.nx, nu=qp.nu, ng=qp.ng, **fields)
 xb = np.repeat(np.asarray(x0)[12:13], M, axis=0)
 res = {}
-for ra in (0, 1):
+ras = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 1]
+for ra in ras:
     out = pkg.capi.solve(fam, xb, dict(iter_max=50, mode="Balance", ric_alg=ra), stats=True)
     rows = []
     for i in range(M):

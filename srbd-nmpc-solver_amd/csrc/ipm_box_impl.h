@@ -11,6 +11,10 @@ using real = SRBD_REAL;
 #ifndef SRBD_ITREF_CHECK_ONLY
 #define SRBD_ITREF_CHECK_ONLY 0
 #endif
+// diagnostic builds: P_k of the square-root RB averaged-symmetrized before its factor is taken
+#ifndef SRBD_SQRT_AVG
+#define SRBD_SQRT_AVG 0
+#endif
 
 constexpr real kThr0 = real(0.1);     // minimum initial slack (HPIPM init_var)
 
@@ -1279,7 +1283,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           P[I] = f.F[I];
         });
         if constexpr (SQRT) {
-          if constexpr (SRBD_SYM_AVG) symmetrize_avg(P, lane);
+          if constexpr (SRBD_SQRT_AVG) symmetrize_avg(P, lane);
           sqrt_factor(P, lane);
           if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
         }

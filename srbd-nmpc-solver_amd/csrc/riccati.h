@@ -258,6 +258,9 @@ __device__ __forceinline__ void symmetrize_avg(T (&M)[12], const int lane) {
 #ifndef SRBD_SYM_AVG
 #define SRBD_SYM_AVG 0
 #endif
+#ifndef SRBD_P_HK
+#define SRBD_P_HK 0
+#endif
 
 // The common tail of both step variants: given L = chol(G) and the column-owned
 // H (VL: g) and F (VL: f) of the stage,
@@ -277,6 +280,10 @@ __device__ __forceinline__ void riccati_tail(const int lane, StageFactor<T>& o, 
     SRBD_PHASE_FENCE();
   }
   // ---- Y = L^-1 H, K = -L^-T Y
+#if SRBD_P_HK
+  T Hs[12];  // (diagnostic form, below)
+  sfor<0, 12>([&](auto i) { Hs[decltype(i)::value] = o.H[decltype(i)::value]; });
+#endif
   trsv_lower(o.Lc, o.rs, o.H);
   SRBD_PHASE_FENCE();
   tstamp(7);
@@ -289,11 +296,17 @@ __device__ __forceinline__ void riccati_tail(const int lane, StageFactor<T>& o, 
     SRBD_PHASE_FENCE();
   }
   // ---- P_k = F - Y'Y (VL: p_k = f - Y'y)
+#if SRBD_P_HK
+  // diagnostic build: the textbook form F + K'H (VL: f + K'g), as oracle/ocp_qp_oracle.c
+  // riccati_factor forms it (H'K there; equal after the averaged symmetrization)
+  tmul_acc(o.Kc, Hs, o.F);
+#else
   {
     T Hn[12];
     sfor<0, 12>([&](auto i) { Hn[decltype(i)::value] = -o.H[decltype(i)::value]; });
     tmul_acc(o.H, Hn, o.F);
   }
+#endif
   SRBD_PHASE_FENCE();
   tstamp(9);
   tstamp(10);
