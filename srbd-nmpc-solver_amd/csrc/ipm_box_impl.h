@@ -11,9 +11,11 @@ using real = SRBD_REAL;
 #ifndef SRBD_ITREF_CHECK_ONLY
 #define SRBD_ITREF_CHECK_ONLY 0
 #endif
-// diagnostic builds: P_k of the square-root RB averaged-symmetrized before its factor is taken
-#ifndef SRBD_SQRT_AVG
-#define SRBD_SQRT_AVG 0
+// ric_alg 1's fp64 RB: P_k in the symmetrized textbook form of riccati.h SYMP before its
+// factor is taken (as the oracle's square-root variant forms it) instead of F - Y'Y: 53 vs 48
+// of 64 on the degenerate endgame family in Speed
+#ifndef SRBD_SQRT_SYMP
+#define SRBD_SQRT_SYMP 1
 #endif
 
 constexpr real kThr0 = real(0.1);     // minimum initial slack (HPIPM init_var)
@@ -1259,9 +1261,12 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         tstamp(22);
         StageFactor<real> f;
         if constexpr (SQRT) {
-          riccati_step_sqrt<1, false, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f);
+          riccati_step_sqrt<1, SRBD_SQRT_SYMP != 0 && sizeof(real) == 8, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f, NoMid{},
+                                                           ldsB + lane * 12);
         } else {
-          riccati_step<1, true, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f);  // P_k symmetrized
+          // P_k = F + K'H, symmetrized (riccati.h SYMP); H waits in the group's B block (dead
+          // since the residual products; the record image overwrites it only afterwards)
+          riccati_step<1, true, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f, NoMid{}, ldsB + lane * 12);
         }
         // The factor record goes through the group's LDS image (its A, B, S blocks are
         // dead by now) and leaves as whole 16-byte pieces instead of ~40 scattered
@@ -1283,7 +1288,6 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           P[I] = f.F[I];
         });
         if constexpr (SQRT) {
-          if constexpr (SRBD_SQRT_AVG) symmetrize_avg(P, lane);
           sqrt_factor(P, lane);
           if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
         }

@@ -255,35 +255,38 @@ __device__ __forceinline__ void symmetrize_avg(T (&M)[12], const int lane) {
   });
 }
 
-#ifndef SRBD_SYM_AVG
-#define SRBD_SYM_AVG 0
-#endif
-#ifndef SRBD_P_HK
-#define SRBD_P_HK 0
-#endif
 
 // The common tail of both step variants: given L = chol(G) and the column-owned
 // H (VL: g) and F (VL: f) of the stage,
 //   Y = L^-1 H, K = -L^-T Y, P_k = F - Y'Y (VL: p_k = f - Y'y).
 // `mid` runs before the triangular solves (MidAt = 1) or after them (MidAt = 2).
-// SYMP: P_k is made exactly symmetric from its lower triangle before it continues the
-// recursion.  The column-wise products leave rounding-level asymmetry in F - Y'Y, while
-// the stage record keeps the lower triangle only: with the IPM's barrier Hessians of
-// ~1e12 the next stage's factorization (register P) and the sweeps that read the record P
-// then solve systems that differ far above the factorization's own error, which stalled
-// degenerate endgames.  (The square-root step needs no such step: its
-// Hessian terms are sums of squares, symmetric by construction.)
+// SYMP (the IPM's factorizations): P_k leaves exactly symmetric.  The stage record keeps P's
+// lower triangle only, and with the IPM's barrier Hessians of ~1e12 the next stage's
+// factorization (register P) and the sweeps that read the record P then solve systems that
+// differ far above the factorization's own error.  fp64: P_k in the textbook form F + K'H
+// (VL: f + K'g, as the oracle's riccati_factor / riccati_vectors form it), averaged with its
+// transpose.  Of the forms measured on the degenerate endgame family of DESIGN.md 4.4 (Speed,
+// 64 copies, ric_alg 0) F - Y'Y with its lower triangle converged on 58, F - Y'Y averaged on
+// 62, F + K'H with its lower triangle on 49 and F + K'H averaged on 64 (the oracle's 63-64).
+// H waits for the product in `hstash` (12 reals per lane, e.g. the caller's dead LDS block) or
+// in registers.  fp32 (the config-5 kernels, at fp32 tolerances): F - Y'Y, lower triangle
+// copied up (the fp64 form measured +0.8% on config 5 for no change in its iterates' reach).
 template <int MidAt, bool SYMP, typename T, typename Mid>
-__device__ __forceinline__ void riccati_tail(const int lane, StageFactor<T>& o, Mid&& mid) {
+__device__ __forceinline__ void riccati_tail(const int lane, StageFactor<T>& o, Mid&& mid, T* hstash) {
   if constexpr (MidAt == 1) {
     mid();
     SRBD_PHASE_FENCE();
   }
+  constexpr bool kHK = SYMP && sizeof(T) == 8;
+  T Hs[kHK ? 12 : 1];
+  if constexpr (kHK) {
+    if (hstash) {
+      store12(hstash, o.H);
+    } else {
+      sfor<0, 12>([&](auto i) { Hs[decltype(i)::value] = o.H[decltype(i)::value]; });
+    }
+  }
   // ---- Y = L^-1 H, K = -L^-T Y
-#if SRBD_P_HK
-  T Hs[12];  // (diagnostic form, below)
-  sfor<0, 12>([&](auto i) { Hs[decltype(i)::value] = o.H[decltype(i)::value]; });
-#endif
   trsv_lower(o.Lc, o.rs, o.H);
   SRBD_PHASE_FENCE();
   tstamp(7);
@@ -295,29 +298,25 @@ __device__ __forceinline__ void riccati_tail(const int lane, StageFactor<T>& o, 
     mid();
     SRBD_PHASE_FENCE();
   }
-  // ---- P_k = F - Y'Y (VL: p_k = f - Y'y)
-#if SRBD_P_HK
-  // diagnostic build: the textbook form F + K'H (VL: f + K'g), as oracle/ocp_qp_oracle.c
-  // riccati_factor forms it (H'K there; equal after the averaged symmetrization)
-  tmul_acc(o.Kc, Hs, o.F);
-#else
-  {
+  if constexpr (kHK) {
+    // ---- P_k = F + K'H (VL: p_k = f + K'g), averaged with its transpose
+    if (hstash) load12(hstash, Hs);
+    tmul_acc(o.Kc, Hs, o.F);
+    SRBD_PHASE_FENCE();
+    symmetrize_avg(o.F, lane);
+  } else {
+    // ---- P_k = F - Y'Y (VL: p_k = f - Y'y)
     T Hn[12];
     sfor<0, 12>([&](auto i) { Hn[decltype(i)::value] = -o.H[decltype(i)::value]; });
     tmul_acc(o.H, Hn, o.F);
+    if constexpr (SYMP) {
+      SRBD_PHASE_FENCE();
+      symmetrize_lower(o.F, lane);
+    }
   }
-#endif
   SRBD_PHASE_FENCE();
   tstamp(9);
   tstamp(10);
-  if constexpr (SYMP) {
-    SRBD_PHASE_FENCE();
-    if constexpr (SRBD_SYM_AVG) {
-      symmetrize_avg(o.F, lane);
-    } else {
-      symmetrize_lower(o.F, lane);  // (B dead here: fewer live registers)
-    }
-  }
 }
 
 // One backward Riccati step.  `P` holds P_{k+1} (VL: p_{k+1}) on entry.
@@ -330,7 +329,8 @@ template <int MidAt = 1, bool SYMP = false, typename TGin = void, typename T, ty
           typename LoadSQ, typename Mid = NoMid>
 __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&B_)[12],
                                              LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
-                                             const T reg, StageFactor<T>& o, Mid&& mid = Mid{}) {
+                                             const T reg, StageFactor<T>& o, Mid&& mid = Mid{},
+                                             T* hstash = nullptr) {
   using TG = std::conditional_t<std::is_void_v<TGin>, T, TGin>;
   const bool isv = lane == kVecLane;
   // ---- G = R + B'(P B), L = chol(G)  (loadR fills a TG column)
@@ -375,7 +375,7 @@ __device__ __forceinline__ void riccati_step(const T (&P)[12], T (&A_)[12], T (&
   }
   SRBD_PHASE_FENCE();
   tstamp(6);
-  riccati_tail<MidAt, SYMP>(lane, o, mid);
+  riccati_tail<MidAt, SYMP>(lane, o, mid, hstash);
 }
 
 // Square-root step (ric_alg = 1).  `Lp` holds the factor of P_{k+1} (lane l: column l,
@@ -389,7 +389,7 @@ template <int MidAt = 1, bool SYMP = false, typename TGin = void, typename T, ty
 __device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12], T (&B_)[12],
                                                   LoadR&& loadR, LoadSQ&& loadSQ, const int lane,
                                                   const T reg, StageFactor<T>& o,
-                                                  Mid&& mid = Mid{}) {
+                                                  Mid&& mid = Mid{}, T* hstash = nullptr) {
   using TG = std::conditional_t<std::is_void_v<TGin>, T, TGin>;
   const bool isv = lane == kVecLane;
   // ---- MB = Lp'B (VL: 0, its B_ column is 0); G = R + MB'MB, L = chol(G)
@@ -420,7 +420,7 @@ __device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12]
     tmul_acc(MA, MA, o.F);
   }
   SRBD_PHASE_FENCE();
-  riccati_tail<MidAt, SYMP>(lane, o, mid);
+  riccati_tail<MidAt, SYMP>(lane, o, mid, hstash);
 }
 
 // P (lane l: column l of P_k; VL: p_k) -> its square-root form for the next
