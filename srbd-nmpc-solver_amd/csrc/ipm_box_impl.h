@@ -17,6 +17,11 @@ using real = SRBD_REAL;
 #ifndef SRBD_SQRT_SYMP
 #define SRBD_SQRT_SYMP 1
 #endif
+// ric_alg 1: the stage records keep P itself (the sweeps apply it as ric_alg 0's do) instead of
+// its factor Lp (applied as Lp (Lp' x)); the factorization still carries Lp from stage to stage
+#ifndef SRBD_SQRT_EXPLICIT_P
+#define SRBD_SQRT_EXPLICIT_P 0
+#endif
 
 constexpr real kThr0 = real(0.1);     // minimum initial slack (HPIPM init_var)
 
@@ -508,8 +513,10 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   using greal = std::conditional_t<sizeof(real) == 4 && GEN == 1, double, real>;
   // (P x)_col + acc for an element-owned x (lane j holds x_j), P from a stage record's kRecP
   // slot: packed P (ric_alg 0) or its factor Lp (ric_alg 1)
+  // the record's kRecP slot holds the factor Lp (ric_alg 1) or P
+  constexpr bool kRecFactor = SQRT && !SRBD_SQRT_EXPLICIT_P;
   auto rec_P_mul = [&](const real* rec, real xv, real acc) -> real {
-    if constexpr (SQRT) {
+    if constexpr (kRecFactor) {
       real Lv[12];
       load_packed_lcol_d(rec + kRecP, col, Lv);
       const real t = dot_bcast(Lv, xv, real(0.0));  // (Lp' x)_col
@@ -864,7 +871,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       real bxk[12];
       gather12(xel ? c.x()[(size_t)k * nx + li] : real(0.0), bxk);
       real Pc[12];
-      if constexpr (SQRT) {  // P = Lp Lp': column l = sum_K Lp[:, K] Lp[l][K]
+      if constexpr (kRecFactor) {  // P = Lp Lp': column l = sum_K Lp[:, K] Lp[l][K]
         real Lr[12];
         load_packed_lrow_d(stk + kRecP, col, Lr);
         sfor<0, 12>([&](auto i) { Pc[decltype(i)::value] = real(0.0); });
@@ -1182,8 +1189,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           if (c.isv) P[I] = qv[I];
         });
         if (c.isv) store12(rec + kRecPv, P);
-        if constexpr (SQRT) sqrt_factor(P, lane);  // (the record keeps the factor)
-        if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
+        if constexpr (SQRT && !kRecFactor)
+          if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
+        if constexpr (SQRT) sqrt_factor(P, lane);  // (kRecFactor: the record keeps the factor)
+        if constexpr (!SQRT || kRecFactor)
+          if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
       } else {
         // ---- A, B (kept by the factorization), S (kept in LDS): residual products ----
         real A_[12], B_[12], Sh[12], Rh[12];
@@ -1276,7 +1286,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         if (lane < kMaxDim) {
           store_packed_col(img + kRecL, lane, f.Lc);
           store12(img + kRecK + lane * 12, f.Kc);
-          if constexpr (!SQRT) store_packed_col(img + kRecP, lane, f.F);
+          if constexpr (!kRecFactor) store_packed_col(img + kRecP, lane, f.F);
           img[kRecRs + lane] = f.rs;
         }
         if (c.isv) {
@@ -1289,7 +1299,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         });
         if constexpr (SQRT) {
           sqrt_factor(P, lane);
-          if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
+          if constexpr (kRecFactor)
+            if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
         }
         lds_wave_fence();
         if constexpr (kRecImg<GEN>) rec_copy(rec, img, lane);
