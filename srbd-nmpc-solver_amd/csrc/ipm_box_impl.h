@@ -11,11 +11,13 @@ using real = SRBD_REAL;
 #ifndef SRBD_ITREF_CHECK_ONLY
 #define SRBD_ITREF_CHECK_ONLY 0
 #endif
-// ric_alg 1's fp64 RB: P_k in the symmetrized textbook form of riccati.h SYMP before its
-// factor is taken (as the oracle's square-root variant forms it) instead of F - Y'Y: 53 vs 48
-// of 64 on the degenerate endgame family in Speed
+// diagnostic builds: ric_alg 1's fp64 RB with P_k in the symmetrized textbook form of riccati.h
+// SYMP before its factor is taken (as the oracle's square-root variant forms it) instead of
+// F - Y'Y.  On the degenerate endgame family in Speed it converges on 53 instead of 48 of 64,
+// but a copy it stops at min step lands ~2e-3 from the oracle's solution (F - Y'Y: 3.3e-5), so
+// it is not the default
 #ifndef SRBD_SQRT_SYMP
-#define SRBD_SQRT_SYMP 1
+#define SRBD_SQRT_SYMP 0
 #endif
 // ric_alg 1: the stage records keep P itself (the sweeps apply it as ric_alg 0's do) instead of
 // its factor Lp (applied as Lp (Lp' x)); the factorization still carries Lp from stage to stage
