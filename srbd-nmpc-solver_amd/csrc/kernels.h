@@ -75,9 +75,6 @@ struct ProblemArgsT {
   // qp_list[g] if g < count.
   int* qp_buf;
   const int* qp_list;
-  // Element buffers of the parallel-in-time single-QP kernel (unconstrained fp64 handles:
-  // srbd_qp_create allocates unconstr_scan_bytes; null = that kernel is not used)
-  T* scan;
 };
 // iterations of the live-QP counter arrays (iter_max >= this runs without the control)
 constexpr int kCtlCap = 257;
@@ -140,9 +137,6 @@ bool unconstr_fused_residuals(const ProblemArgsT<T>& a);
 // (the single-QP kernel's copy into LDS): the data may then live in mapped host memory
 template <typename T>
 bool unconstr_reads_once(const ProblemArgsT<T>& a);
-// bytes of the parallel-in-time kernel's element buffers for a handle of these dims and
-// capacity (0: the handle's solves never take that kernel)
-size_t unconstr_scan_bytes(int N, int nx, int nu, int capacity);
 
 // nx < 12 or nu < 12: embed the problem in 12 x 12 stages (pad.hip).  pad_elems
 // is the pad buffer size (elements of T); pad_problem fills it from `a` and

@@ -38,17 +38,6 @@ namespace srbd {
 
 size_t ws_doubles_unconstr(int N) { return (size_t)(N + 1) * kWsStage; }
 
-size_t unconstr_scan_bytes(int N, int nx, int nu, int capacity) {
-#if !SRBD_SCAN
-  (void)N, (void)nx, (void)nu, (void)capacity;
-  return 0;
-#else
-  if (nx != 12 || nu != 12 || N < 1 || N > ric_f64::kScanNMax) return 0;
-  const int b = capacity < ric_f64::kScanBatchMax ? capacity : ric_f64::kScanBatchMax;
-  return (size_t)b * ric_f64::scan_doubles_per_qp(N) * sizeof(double);
-#endif
-}
-
 hipError_t prepare_riccati_device() {
   hipError_t e = ric_f64::prepare_device();
   return e == hipSuccess ? ric_f32::prepare_device() : e;

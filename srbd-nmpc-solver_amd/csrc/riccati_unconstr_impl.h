@@ -374,12 +374,11 @@ __device__ __forceinline__ const real* img_source(const ProblemArgsT<real>& a, i
 
 // The QP's blocks into the LDS image by every thread of the workgroup (global->LDS DMA;
 // the source may be device memory or mapped host memory), waited for and fenced.
-template <int NT = kLdsCopyThreads>
 __device__ __forceinline__ void lds_copy_qp(const ProblemArgsT<real>& a, real* img, int qp) {
   const int lane = threadIdx.x;
   const int total = (a.N + 1) * kImgStage;
   const int wave_off = (lane >> 6) * 64 * kRealsPerDma;  // this wave's 1 KiB of each round
-  for (int c0 = 0; c0 < total; c0 += NT * kRealsPerDma) {
+  for (int c0 = 0; c0 < total; c0 += kLdsCopyThreads * kRealsPerDma) {
     const int e = c0 + lane * kRealsPerDma;
     const real* g = e < total ? img_source(a, qp, e) : nullptr;
     if (g)
@@ -751,21 +750,6 @@ bool lat_eligible(const ProblemArgsT<real>& a) { return use_lds_kernel(a) && lat
 #else
 bool lat_eligible(const ProblemArgsT<real>&) { return false; }
 #endif
-// ... and batches of at most kScanBatchMax QPs with a scan buffer (srbd_qp_create allocates it
-// for unconstrained 12 x 12 handles) on the parallel-in-time kernel (riccati_scan_impl.h;
-// -DSRBD_SCAN=0 builds without it)
-#ifndef SRBD_SCAN
-#define SRBD_SCAN 0
-#endif
-#if SRBD_WITH_LATENCY && SRBD_SCAN
-#include "riccati_scan_impl.h"
-bool scan_eligible(const ProblemArgsT<real>& a) {
-  return a.scan && a.nx == 12 && a.nu == 12 && a.batch <= kScanBatchMax && a.N <= kScanNMax &&
-         use_lds_kernel(a) && lds_res_bytes(a.N) + kLdsResStatic <= kLdsBytesMax;
-}
-#else
-bool scan_eligible(const ProblemArgsT<real>&) { return false; }
-#endif
 
 // the single-QP kernel computes the residuals itself (one launch, one read of the data)
 bool fused_residuals(const ProblemArgsT<real>& a) {
@@ -780,18 +764,6 @@ bool reads_once(const ProblemArgsT<real>& a) {
 
 template <bool SQRT>
 static hipError_t launch_alg(const ProblemArgsT<real>& a, hipStream_t stream) {
-#if SRBD_WITH_LATENCY && SRBD_SCAN
-  if (!SQRT && scan_eligible(a)) {
-    if (fused_residuals(a)) {
-      hipLaunchKernelGGL(riccati_scan_kernel<true>, dim3((unsigned)a.batch), dim3(kScanThreads),
-                         lds_res_bytes(a.N), stream, a);
-    } else {
-      hipLaunchKernelGGL(riccati_scan_kernel<false>, dim3((unsigned)a.batch), dim3(kScanThreads),
-                         lds_res_bytes(a.N), stream, a);
-    }
-    return hipGetLastError();
-  }
-#endif
 #if SRBD_WITH_LATENCY && SRBD_LATENCY_MFMA
   if (!SQRT && lat_eligible(a)) {
     if (fused_residuals(a)) {
@@ -840,14 +812,6 @@ hipError_t prepare_device() {
   if (e == hipSuccess)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_unconstr_lds_res_kernel<true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
-#if SRBD_WITH_LATENCY && SRBD_SCAN
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_scan_kernel<false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_scan_kernel<true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
-#endif
 #if SRBD_WITH_LATENCY && SRBD_LATENCY_MFMA
   if (e == hipSuccess)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_latency_kernel<false>),

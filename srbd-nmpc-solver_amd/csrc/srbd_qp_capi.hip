@@ -44,9 +44,6 @@ struct srbd_qp_handle_s {
   double* ws = nullptr;
   size_t ws_qp = 0;  // doubles per QP
   size_t ws_bytes = 0;
-  // element buffers of the parallel-in-time single-QP kernel (unconstrained 12 x 12 handles)
-  double* scan = nullptr;
-  size_t scan_bytes = 0;
   // host-solve staging (device)
   double* stage = nullptr;
   size_t stage_bytes = 0;
@@ -194,11 +191,6 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srb
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = srbd::prepare_riccati_device();  // per-device kernel attributes
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&h->ws), h->ws_bytes);
-  if (e == hipSuccess && !constrained(*dims)) {
-    h->scan_bytes = srbd::unconstr_scan_bytes(dims->N, dims->nx, dims->nu, batch_capacity);
-    if (h->scan_bytes) e = hipMalloc(reinterpret_cast<void**>(&h->scan), h->scan_bytes);
-    if (e != hipSuccess) h->scan_bytes = 0;
-  }
   if (e == hipSuccess && constrained(*dims)) {
     e = hipMalloc(reinterpret_cast<void**>(&h->ctl), sizeof(int) * srbd::kCtlInts);
     if (e == hipSuccess) e = hipMemset(h->ctl, 0, sizeof(int) * srbd::kCtlInts);
@@ -221,7 +213,6 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->ws) hipFree(h->ws);
-  if (h->scan) hipFree(h->scan);
   if (h->stage) hipFree(h->stage);
   if (h->pinned) hipHostFree(h->pinned);
   if (h->pad) hipFree(h->pad);
@@ -245,7 +236,7 @@ size_t srbd_qp_workspace_bytes(srbd_qp_handle h) { return h ? h->ws_bytes : 0; }
 
 size_t srbd_qp_memory_bytes(srbd_qp_handle h) {
   if (!h) return 0;
-  return h->ws_bytes + h->scan_bytes + h->stage_bytes + h->pinned_bytes + h->pad_bytes + h->nmpc_bytes +
+  return h->ws_bytes + h->stage_bytes + h->pinned_bytes + h->pad_bytes + h->nmpc_bytes +
          (h->ctl ? sizeof(int) * srbd::kCtlInts : 0) +
          (h->qp_buf ? sizeof(int) * ((size_t)h->capacity + 1) : 0) +
          h->resc_bytes + h->resc2_bytes + h->mixed_bytes +
@@ -343,7 +334,6 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   a.status = status; a.iter = s->iter; a.res = s->res; a.obj = s->obj;
   a.stat = s->stat;
   a.ws = reinterpret_cast<T*>(h->ws);
-  if constexpr (std::is_same_v<T, double>) a.scan = h->scan;  // (fp64 only)
   a.ws_qp = h->ws_qp;
   a.reg = st->reg_prim;
   a.iter_max = st->iter_max;
