@@ -32,5 +32,14 @@ mode = sys.argv[2] if len(sys.argv) > 2 else "Speed"
 for ra in [int(v) for v in sys.argv[1].split(",")]:
     out = pkg.capi.solve(fam, xb, dict(iter_max=50, mode=mode, ric_alg=ra))
     st = out["status"]
+    worst = 0.0
+    if len(sys.argv) > 3:  # distance of every copy to the oracle's solution (converged copies)
+        sys.path.insert(0, str(REPO / "oracle"))
+        ref = helpers.load_oracle().solve(fam, dict(iter_max=50, mode=mode, ric_alg=ra), x0=xb)
+        for i in range(M):
+            if ref["status"][i] == 0:
+                for key in ("x", "u"):
+                    d = np.linalg.norm(out[key][i] - ref[key][i]) / np.linalg.norm(ref[key][i])
+                    worst = max(worst, d)
     print(f"{mode} ric_alg {ra}: converged {(st == 0).sum()}/{M}, statuses {np.bincount(st, minlength=4).tolist()}, "
-          f"iters {np.bincount(out['iter'][st == 0]).nonzero()[0].tolist()}", flush=True)
+          f"iters {np.bincount(out['iter'][st == 0]).nonzero()[0].tolist()}, worst rel dist to oracle {worst:.1e}", flush=True)

@@ -24,6 +24,14 @@ using real = SRBD_REAL;
 #ifndef SRBD_SQRT_EXPLICIT_P
 #define SRBD_SQRT_EXPLICIT_P 0
 #endif
+// fp64 box RB (12 x 12 blocks): Q_k reaches the group's LDS by LDS-DMA issued before the
+// Cholesky of G instead of by register loads after it (one memory round trip less on the
+// stage's chain, no VGPRs held across the Cholesky).  Measured slower (box-u 78.90 vs 78.05 ms
+// same box, profiles/round4/ab_qdma_box_u.log: the exec / M0 set-up of four groups' pieces
+// and 12 more bytes of spills outweigh the round trip), so off by default
+#ifndef SRBD_Q_DMA
+#define SRBD_Q_DMA 0
+#endif
 
 constexpr real kThr0 = real(0.1);     // minimum initial slack (HPIPM init_var)
 
@@ -344,6 +352,47 @@ __device__ __forceinline__ void lds_put_col(real* blk, int lane, const real (&v)
 }
 __device__ __forceinline__ void lds_get_col(const real* blk, int c, real (&v)[12]) {
   load12(blk + c * 12, v);
+}
+// One 12 x 12 fp64 block (1152 contiguous, 16-byte aligned bytes of each group's QP) into
+// the group's LDS block by LDS-DMA (global_load_lds_dwordx4): no VGPR destination, retired by
+// the memory counter.  An LDS-DMA writes at a wave-uniform base (M0) + 16 B x (lane in the
+// wave), so each of the wave's four groups issues its own five 256-byte pieces under an exec
+// mask of its 16 lanes, M0 offset by the group's position in the wave.  One asm statement for
+// the whole wave: with the intrinsic under per-group branches the compiler merged the arms'
+// last pieces into one block and took M0 from the first active lane for all four groups.
+// The fifth piece is whole (bytes 1152..1279 of the source are the next stage's block, and
+// land in the group's dead B block).  The caller waits (vmcnt(0)) before reading the block;
+// the compiler does not see these loads.  `blk0`: the LDS byte address of the wave's first
+// group block (wave-uniform); `stride`: the group blocks' byte stride.
+template <unsigned kStride>
+__device__ __forceinline__ void dma_block144(const real* src, unsigned blk0, int lane) {
+  const real* g = src + 2 * lane;
+  unsigned km;
+  unsigned long long ke;
+  asm volatile(
+      "s_mov_b32 %[km], m0\n\t"
+      "s_mov_b64 %[ke], exec\n\t"
+#define SRBD_DMA_GROUP(G, MASK)                                  \
+      "s_and_b64 exec, %[ke], " MASK "\n\t"                    \
+      "s_add_u32 m0, %[b], %[o" #G "]\n\t"                     \
+      "s_nop 1\n\t"                                            \
+      "global_load_lds_dwordx4 %[g], off\n\t"                  \
+      "global_load_lds_dwordx4 %[g], off offset:256\n\t"       \
+      "global_load_lds_dwordx4 %[g], off offset:512\n\t"       \
+      "global_load_lds_dwordx4 %[g], off offset:768\n\t"       \
+      "global_load_lds_dwordx4 %[g], off offset:1024\n\t"
+      SRBD_DMA_GROUP(0, "%[m0]")
+      SRBD_DMA_GROUP(1, "%[m1]")
+      SRBD_DMA_GROUP(2, "%[m2]")
+      SRBD_DMA_GROUP(3, "%[m3]")
+#undef SRBD_DMA_GROUP
+      "s_mov_b64 exec, %[ke]\n\t"
+      "s_mov_b32 m0, %[km]"
+      : [km] "=&s"(km), [ke] "=&s"(ke)
+      : [g] "v"(g), [b] "s"(blk0), [o0] "i"(0), [o1] "i"(kStride - 256), [o2] "i"(2 * (kStride - 256)),
+        [o3] "i"(3 * (kStride - 256)), [m0] "s"(0xffffull), [m1] "s"(0xffffull << 16),
+        [m2] "s"(0xffffull << 32), [m3] "s"(0xffffull << 48)
+      : "memory", "scc");
 }
 __device__ __forceinline__ void lds_get_row(const real* blk, int r, real (&v)[12]) {
   sfor<0, 12>([&](auto j) {
@@ -1206,6 +1255,10 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         // at their register limit, when the factorization asks for it (cone +0.7% otherwise)
         constexpr bool kEarlyR = GEN == 0;
         if constexpr (kEarlyR) c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, Rh);
+        // Q_k by LDS-DMA into the A block (free once the residual products have read it),
+        // issued at the end of loadR: R's registers are consumed by then, so no ordinary load
+        // result is waited for while the DMA is in flight (such a wait drains it)
+        constexpr bool kQDma = SRBD_Q_DMA && FULL && GEN == 0 && sizeof(real) == 8;
         const real bk = c.el(c.b() + (size_t)k * nx, nx, li);
         rgx = dot_bcast(A_, pin, rgx);  // + A'pi_{k+1}
         rgu = dot_bcast(B_, pin, rgu);  // + B'pi_{k+1}
@@ -1252,10 +1305,24 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             if (lane == I) Rc[I] += (I < nu) ? greal(Gu) : greal(1.0);  // padded inputs: R = 1
             if (c.isv) Rc[I] = greal(0.0);
           });
+          if constexpr (kQDma) {
+            // the wave's first group block (the same on every lane of the wave)
+            const real* b0 = ldsA - ((threadIdx.x / kGroup) & 3) * kGroupLds<GEN>;
+            const unsigned blk0 = __builtin_amdgcn_readfirstlane(
+                (unsigned)(size_t)(const __attribute__((address_space(3))) real*)b0);
+            dma_block144<kGroupLds<GEN> * sizeof(real)>(c.Q() + (size_t)k * 144, blk0, lane);
+          }
         };
         auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
           lds_get_col(ldsS, col, Sc);
-          c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
+          if constexpr (kQDma) {
+            // the compiler does not order this LDS read after the DMA's write: wait by hand
+            // (the DMA is the wave's last memory instruction, so nothing else is waited for)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_get_col(ldsA, col, Qc);
+          } else {
+            c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
+          }
           const real qx = dot_bcast(Qc, xk, real(0.0));
           if (k > 0) objl += xk * (real(0.5) * qx + qk);
           const real qt = finish_x(rgx + qx);
