@@ -140,6 +140,7 @@ typedef struct {
   double rd_l, rd_u, rm_l, rm_u; /* res_d, res_m                            */
   double dlam_l, dlam_u, dt_l, dt_u;
   double aff_l, aff_u;           /* dlam_aff * dt_aff                        */
+  double G;                      /* this iteration's barrier Hessian weight  */
 } row_t;
 
 typedef struct {
@@ -335,6 +336,116 @@ static int riccati_factor(const dims_t* d, ric_ws_t* w, double reg, int sqrt_alg
   return 0;
 }
 
+/* LQ factorization with a positive diagonal of the n x m matrix M (column-major, ld n), in
+ * place: afterwards the lower triangle of M[:, 0:n] holds L with M = L Q (Q orthogonal, not
+ * formed).  One Householder reflection from the right per row maps row i's entries i..m-1 to
+ * (||.||, 0, ..., 0): LAPACK's dgelqf with dlarfgp's positive beta, as HPIPM's dgelqf_pd
+ * (restated: HPIPM / BLASFEO are not vendored).  A zero row stays zero.        */
+static void lq_pd(int n, int m, double* M) {
+  double v[512];
+  for (int i = 0; i < n; ++i) {
+    const double alpha = M_(M, n, i, i);
+    double sigma = 0.0;
+    for (int j = i + 1; j < m; ++j) sigma += M_(M, n, i, j) * M_(M, n, i, j);
+    if (sigma == 0.0) {
+      if (alpha < 0.0)
+        for (int r = i; r < n; ++r) M_(M, n, r, i) = -M_(M, n, r, i);
+      continue;
+    }
+    const double norm = sqrt(alpha * alpha + sigma);
+    v[0] = alpha <= 0.0 ? alpha - norm : -sigma / (alpha + norm);
+    for (int j = i + 1; j < m; ++j) v[j - i] = M_(M, n, i, j);
+    const double vtv = v[0] * v[0] + sigma;
+    for (int r = i; r < n; ++r) {
+      double dot = 0.0;
+      for (int j = i; j < m; ++j) dot += M_(M, n, r, j) * v[j - i];
+      const double f = 2.0 * dot / vtv;
+      for (int j = i; j < m; ++j) M_(M, n, r, j) -= f * v[j - i];
+    }
+    M_(M, n, i, i) = norm;
+    for (int j = i + 1; j < m; ++j) M_(M, n, i, j) = 0.0;
+  }
+}
+
+/* HPIPM's lq_fact factorization (d_ocp_qp_fact_lq_solve_kkt_step, restated): the stage's
+ * barrier-augmented Hessian is never formed.  Stage k factors
+ *   M_k = [ chol(RSQ_k) | sqrt(reg) e_i (inputs) | sqrt(G_r) row_r (every bound / general
+ *           row) | [B'; A'] Lx_{k+1} ]
+ * as M_k = L_k Q with L_k = [Lu 0; Lxu Lx] lower ([u; x] order), so L_k L_k' = RSQ_k + Gamma_k
+ * + reg + [B'; A'] P_{k+1} [B A] -- riccati_factor's matrix -- with Gamma entering as its
+ * square root beside the data instead of being added to it.  Then chol(G) = Lu, K = -G^-1 H
+ * with H = Lu Lxu', P_k = Lx Lx' (the record riccati_vectors reads).  Stage N: L_N from
+ * [chol(Q_N) | sqrt(G_r) row_r], P_N = L_N L_N'.                                            */
+static void fill_stage_H(const dims_t* d, int k, double* Ht, double* gt);
+static int riccati_factor_lq(const dims_t* d, ric_ws_t* w, const stage_rows_t* st, double reg) {
+  const int nx = d->nx, nu = d->nu, N = d->N;
+  double* M = (double*)malloc(sizeof(double) * 64 * 512);
+  double Lx[32 * 32], Hd[64 * 64], gdum[64], vrow[64];
+  if (!M) return -1;
+  for (int k = N; k >= 0; --k) {
+    const int nu_k = st[k].nu_k, ns = nu_k + nx;
+    int m = 0;
+    fill_stage_H(d, k, Hd, gdum);
+    chol(ns, Hd);
+    for (int j = 0; j < ns; ++j, ++m)
+      for (int i = 0; i < ns; ++i) M_(M, ns, i, m) = M_(Hd, ns, i, j);
+    if (reg > 0.0)
+      for (int j = 0; j < nu_k; ++j, ++m)
+        for (int i = 0; i < ns; ++i) M_(M, ns, i, m) = i == j ? sqrt(reg) : 0.0;
+    for (int r = 0; r < st[k].nrow; ++r) {
+      const row_t* rw = &st[k].rows[r];
+      if (!(rw->G > 0.0)) continue;
+      for (int i = 0; i < ns; ++i) vrow[i] = 0.0;
+      row_axpy(d, rw, nu_k, sqrt(rw->G), vrow, vrow + nu_k);
+      for (int i = 0; i < ns; ++i) M_(M, ns, i, m) = vrow[i];
+      ++m;
+    }
+    if (k < N) {
+      const double* A = qA(d, k);
+      const double* B = qB(d, k);
+      for (int j = 0; j < nx; ++j, ++m) {
+        for (int i = 0; i < nu; ++i) {
+          double acc = 0.0;
+          for (int l = 0; l < nx; ++l) acc += M_(B, nx, l, i) * M_(Lx, nx, l, j);
+          M_(M, ns, i, m) = acc;
+        }
+        for (int i = 0; i < nx; ++i) {
+          double acc = 0.0;
+          for (int l = 0; l < nx; ++l) acc += M_(A, nx, l, i) * M_(Lx, nx, l, j);
+          M_(M, ns, nu + i, m) = acc;
+        }
+      }
+    }
+    lq_pd(ns, m, M);
+    double* P = w->P + (size_t)k * nx * nx;
+    for (int j = 0; j < nx; ++j)
+      for (int i = 0; i < nx; ++i) M_(Lx, nx, i, j) = i >= j ? M_(M, ns, nu_k + i, nu_k + j) : 0.0;
+    for (int j = 0; j < nx; ++j)
+      for (int i = 0; i < nx; ++i) {
+        double acc = 0.0;
+        for (int l = 0; l < nx; ++l) acc += M_(Lx, nx, i, l) * M_(Lx, nx, j, l);
+        M_(P, nx, i, j) = acc;
+      }
+    if (k == N) continue;
+    double* L = w->Lg + (size_t)k * nu * nu;
+    for (int j = 0; j < nu; ++j)
+      for (int i = 0; i < nu; ++i) M_(L, nu, i, j) = i >= j ? M_(M, ns, i, j) : 0.0;
+    double* K = w->K + (size_t)k * nu * nx;
+    for (int j = 0; j < nx; ++j) {
+      double col[32];
+      for (int i = 0; i < nu; ++i) {  /* H[:, j] = Lu Lxu'[:, j] */
+        double acc = 0.0;
+        for (int l = 0; l <= i; ++l) acc += M_(L, nu, i, l) * M_(M, ns, nu + j, l);
+        col[i] = acc;
+      }
+      chol_solve(nu, L, col);
+      for (int i = 0; i < nu; ++i) M_(K, nu, i, j) = -col[i];
+    }
+  }
+  free(M);
+  return 0;
+}
+
 /* p-vector recursion: p_N = gt_N; k_k = -G^-1 (r~ + B'(P b~ + p));
  * p_k = q~ + A'(P b~ + p) + K' (r~ + B'(P b~ + p)).                   */
 static void riccati_vectors(const dims_t* d, ric_ws_t* w) {
@@ -414,6 +525,57 @@ static void fill_stage_H(const dims_t* d, int k, double* Ht, double* gt) {
     for (int i = 0; i < nx; ++i) M_(Ht, n, nu + i, nu + j) = M_(Q, nx, i, j);
   memcpy(gt, qr(d, k), sizeof(double) * nu);
   memcpy(gt + nu, qq(d, k), sizeof(double) * nx);
+}
+
+/* The linear residual of the Newton system at the step (du, dx, dpi and the rows' dt, dlam), in
+ * its full form: QP Hessian, the rows' multiplier steps, dynamics (HPIPM d_ocp_qp_res_compute_lin,
+ * restated); the dt / dlam rows hold exactly by construction and are not formed.  Fills itg / itb
+ * and returns the infinity norms of the stationarity and equality parts.                      */
+static void lin_res(const dims_t* d, const stage_rows_t* st, const ric_ws_t* w, const double* rg,
+                    const double* rb, const double* du, const double* dx, const double* dpi,
+                    double* itg, double* itb, double* ng_out, double* nb_out) {
+  const int nx = d->nx, nu = d->nu, N = d->N;
+  double ng = 0.0, nb = 0.0;
+  for (int s = 0; s <= N; ++s) {
+    int nu_k = st[s].nu_k, ns = nu_k + nx;
+    double H[64 * 64], gdum[64], v[64], r1[64];
+    fill_stage_H(d, s, H, gdum);
+    for (int i = 0; i < nu_k; ++i) v[i] = du[(size_t)s * nu + i];
+    for (int i = 0; i < nx; ++i) v[nu_k + i] = dx[(size_t)s * nx + i];
+    for (int i = 0; i < ns; ++i) {
+      double acc = rg[(size_t)s * w->gstride + i];
+      for (int j = 0; j < ns; ++j) acc += M_(H, ns, i, j) * v[j];
+      r1[i] = acc;
+    }
+    for (int i = 0; i < st[s].nrow; ++i) {
+      row_t* rw = &st[s].rows[i];
+      double c = (rw->has_u ? rw->dlam_u : 0.0) - (rw->has_l ? rw->dlam_l : 0.0);
+      row_axpy(d, rw, nu_k, c, r1, r1 + nu_k);
+    }
+    if (s < N) {
+      double t[32];
+      mtv(nx, nu, qB(d, s), dpi + (size_t)(s + 1) * nx, t);
+      for (int i = 0; i < nu; ++i) r1[i] += t[i];
+      mtv(nx, nx, qA(d, s), dpi + (size_t)(s + 1) * nx, t);
+      for (int i = 0; i < nx; ++i) r1[nu_k + i] += t[i];
+    }
+    if (s > 0) for (int i = 0; i < nx; ++i) r1[nu_k + i] -= dpi[(size_t)s * nx + i];
+    else for (int i = 0; i < nx; ++i) r1[nu_k + i] = 0.0;  /* x_0 fixed */
+    for (int i = 0; i < ns; ++i) ng = fmax(ng, fabs(r1[i]));
+    memcpy(itg + (size_t)s * w->gstride, r1, sizeof(double) * ns);
+    if (s < N) {
+      double t1[32], t2[32];
+      mv(nx, nx, qA(d, s), dx + (size_t)s * nx, t1);
+      mv(nx, nu, qB(d, s), du + (size_t)s * nu, t2);
+      for (int i = 0; i < nx; ++i) {
+        double rbi = rb[(size_t)s * nx + i] + t1[i] + t2[i] - dx[(size_t)(s + 1) * nx + i];
+        itb[(size_t)s * nx + i] = rbi;
+        nb = fmax(nb, fabs(rbi));
+      }
+    }
+  }
+  *ng_out = ng;
+  *nb_out = nb;
 }
 
 /* ------------------------------------------------------------------ */
@@ -646,6 +808,7 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
 
   double alpha_prim = 1.0, alpha_dual = 1.0;
   int iter = 0;
+  int force_lq = set->lq_fact == 2;  /* lq_fact 1 switches for the rest of the solve */
   for (;;) {
     compute_residuals(&d, st, x, u, pi, rg, rb, res->res, &res->obj, w.gstride);
     double mu = 0.0;
@@ -677,12 +840,14 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
         double G = 0.0, gam = 0.0;
         if (rw->has_l) { G += rw->lam_l / rw->t_l; gam += (rw->rm_l + rw->lam_l * rw->rd_l) / rw->t_l; }
         if (rw->has_u) { G += rw->lam_u / rw->t_u; gam -= (rw->rm_u + rw->lam_u * rw->rd_u) / rw->t_u; }
+        rw->G = G;
         row_syr(&d, rw, nu_k, G, Ht);
         row_axpy(&d, rw, nu_k, gam, gt, gt + nu_k);
       }
       if (s < N) memcpy(w.bt + (size_t)s * nx, rb + (size_t)s * nx, sizeof(double) * nx);
     }
-    if (riccati_factor(&d, &w, set->reg_prim, set->ric_alg)) { res->status = 3; break; }
+    if (force_lq ? riccati_factor_lq(&d, &w, st, set->reg_prim)
+                 : riccati_factor(&d, &w, set->reg_prim, set->ric_alg)) { res->status = 3; break; }
     riccati_vectors(&d, &w);
     riccati_forward(&d, &w, zero, dx, du, dpi);
 #ifdef ORACLE_DEBUG
@@ -720,6 +885,20 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
     for (int s = 0; s <= N; ++s)
       for (int i = 0; i < st[s].nrow; ++i) { st[s].rows[i].aff_l = 0.0; st[s].rows[i].aff_u = 0.0; }
     STEP_TLAM();
+    if (set->lq_fact == 1 && !force_lq) {
+      /* HPIPM lq_fact 1: the predictor step's linear residual decides; above 1e-5 (or NaN) the
+       * factorization is redone by LQ, and LQ stays for the rest of the solve */
+      double ng = 0.0, nb = 0.0;
+      lin_res(&d, st, &w, rg, rb, du, dx, dpi, itg, itb, &ng, &nb);
+      if (!(ng <= 1e-5) || !(nb <= 1e-5)) {
+        force_lq = 1;
+        if (riccati_factor_lq(&d, &w, st, set->reg_prim)) { res->status = 3; break; }
+        riccati_vectors(&d, &w);
+        riccati_forward(&d, &w, zero, dx, du, dpi);
+        STEP_TLAM();
+      }
+    }
+    res->lq_iters += force_lq;
 
     if (set->pred_corr) {
       /* alpha_aff, mu_aff, sigma = (mu_aff/mu)^3 */
@@ -784,44 +963,7 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
       double n0g = 0.0, n0b = 0.0;
       for (int ir = 0; ir < set->itref_corr_max; ++ir) {
         double ng = 0.0, nb = 0.0;
-        for (int s = 0; s <= N; ++s) {
-          int nu_k = st[s].nu_k, ns = nu_k + nx;
-          double H[64 * 64], gdum[64], v[64], r1[64];
-          fill_stage_H(&d, s, H, gdum);
-          for (int i = 0; i < nu_k; ++i) v[i] = du[(size_t)s * nu + i];
-          for (int i = 0; i < nx; ++i) v[nu_k + i] = dx[(size_t)s * nx + i];
-          for (int i = 0; i < ns; ++i) {
-            double acc = rg[(size_t)s * w.gstride + i];
-            for (int j = 0; j < ns; ++j) acc += M_(H, ns, i, j) * v[j];
-            r1[i] = acc;
-          }
-          for (int i = 0; i < st[s].nrow; ++i) {
-            row_t* rw = &st[s].rows[i];
-            double c = (rw->has_u ? rw->dlam_u : 0.0) - (rw->has_l ? rw->dlam_l : 0.0);
-            row_axpy(&d, rw, nu_k, c, r1, r1 + nu_k);
-          }
-          if (s < N) {
-            double t[32];
-            mtv(nx, nu, qB(&d, s), dpi + (size_t)(s + 1) * nx, t);
-            for (int i = 0; i < nu; ++i) r1[i] += t[i];
-            mtv(nx, nx, qA(&d, s), dpi + (size_t)(s + 1) * nx, t);
-            for (int i = 0; i < nx; ++i) r1[nu_k + i] += t[i];
-          }
-          if (s > 0) for (int i = 0; i < nx; ++i) r1[nu_k + i] -= dpi[(size_t)s * nx + i];
-          else for (int i = 0; i < nx; ++i) r1[nu_k + i] = 0.0;  /* x_0 fixed */
-          for (int i = 0; i < ns; ++i) ng = fmax(ng, fabs(r1[i]));
-          memcpy(itg + (size_t)s * w.gstride, r1, sizeof(double) * ns);
-          if (s < N) {
-            double t1[32], t2[32];
-            mv(nx, nx, qA(&d, s), dx + (size_t)s * nx, t1);
-            mv(nx, nu, qB(&d, s), du + (size_t)s * nu, t2);
-            for (int i = 0; i < nx; ++i) {
-              double rbi = rb[(size_t)s * nx + i] + t1[i] + t2[i] - dx[(size_t)(s + 1) * nx + i];
-              itb[(size_t)s * nx + i] = rbi;
-              nb = fmax(nb, fabs(rbi));
-            }
-          }
-        }
+        lin_res(&d, st, &w, rg, rb, du, dx, dpi, itg, itb, &ng, &nb);
         if (ir == 0) { n0g = ng; n0b = nb; }
         if ((ng < set->tol_stat || ng < 1e-3 * n0g) && (nb < set->tol_eq || nb < 1e-3 * n0b)) break;
         /* correction: same factors, right-hand side = the residual */
@@ -914,7 +1056,16 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
         row_syr(&d, rw, nu_k, G, Ht);
       }
     }
-    if (riccati_factor(&d, &w, set->reg_prim, set->ric_alg) != 0) res->status = 3;
+    if (set->lq_fact == 2) {
+      for (int s = 0; s <= N; ++s)
+        for (int i = 0; i < st[s].nrow; ++i) {
+          row_t* rw = &st[s].rows[i];
+          rw->G = (rw->has_l ? rw->lam_l / rw->t_l : 0.0) + (rw->has_u ? rw->lam_u / rw->t_u : 0.0);
+        }
+      if (riccati_factor_lq(&d, &w, st, set->reg_prim) != 0) res->status = 3;
+    } else if (riccati_factor(&d, &w, set->reg_prim, set->ric_alg) != 0) {
+      res->status = 3;
+    }
   }
   write_outputs(&d, &w, x, u, pi, P, p, K, k);
   goto done;

@@ -59,6 +59,11 @@ typedef struct oracle_settings {
   int ric_alg;  /* 0 classical Riccati; else square root: P_k = Lx Lx', with the
                  * stage products formed from chol(P_{k+1}) (HPIPM square_root_alg) */
   int itref_corr_max; /* iterative refinement steps of the final (corrector) step        */
+  int lq_fact;  /* HPIPM lq_fact: 0 Cholesky; 2 LQ factorization of every stage (square-root
+                 * form, Gamma as its square root beside the data); 1 Cholesky until a
+                 * predictor step's linear residual exceeds 1e-5, LQ from then on.  HPIPM's
+                 * Balance / Robust select 1 / 2; the oracle takes it only when asked (the HIP
+                 * library does not build it: DESIGN.md 9)                                     */
 } oracle_settings;
 
 typedef struct oracle_result {
@@ -66,6 +71,7 @@ typedef struct oracle_result {
   int iter;
   double res[4];     /* max |res_stat|, |res_eq|, |res_ineq|, |res_comp|    */
   double obj;
+  int lq_iters;      /* iterations whose step came from the LQ factorization */
 } oracle_result;
 
 /* Solve one QP.  x ((N+1)*nx), u (N*nu): in = warm start (if enabled), out =

@@ -36,11 +36,12 @@ class _Settings(C.Structure):
                 ("tol_stat", C.c_double), ("tol_eq", C.c_double), ("tol_ineq", C.c_double),
                 ("tol_comp", C.c_double), ("reg_prim", C.c_double), ("warm_start", C.c_int),
                 ("pred_corr", C.c_int), ("split_step", C.c_int), ("ric_alg", C.c_int),
-                ("itref_corr_max", C.c_int)]
+                ("itref_corr_max", C.c_int), ("lq_fact", C.c_int)]
 
 
 class _Result(C.Structure):
-    _fields_ = [("status", C.c_int), ("iter", C.c_int), ("res", C.c_double * 4), ("obj", C.c_double)]
+    _fields_ = [("status", C.c_int), ("iter", C.c_int), ("res", C.c_double * 4), ("obj", C.c_double),
+                ("lq_iters", C.c_int)]
 
 
 _lib = None
@@ -77,7 +78,8 @@ def _ptr(a: Optional[np.ndarray]):
 
 DEFAULT_SETTINGS = dict(iter_max=15, alpha_min=1e-8, mu0=1e2, tol_stat=1e-8, tol_eq=1e-8,
                         tol_ineq=1e-8, tol_comp=1e-8, reg_prim=1e-12, warm_start=0, pred_corr=1,
-                        split_step=0, ric_alg=1, itref_corr_max=0)  # hpipm-cpp defaults (settings.hpp:26-86)
+                        split_step=0, ric_alg=1, itref_corr_max=0,  # hpipm-cpp defaults (settings.hpp:26-86)
+                        lq_fact=0)  # (HPIPM's Balance / Robust: 1 / 2 -- only when asked)
 
 
 # HPIPM's mode-dependent itref_corr_max (d_ocp_qp_ipm_arg_set_default; the HIP library
@@ -117,7 +119,7 @@ def solve(batch, settings: Optional[Dict] = None, x0: Optional[np.ndarray] = Non
         "P": np.zeros((nb, N + 1, nx, nx)), "p": np.zeros((nb, N + 1, nx)),
         "K": np.zeros((nb, N, nu, nx)), "k": np.zeros((nb, N, nu)),
         "status": np.zeros(nb, dtype=np.int32), "iter": np.zeros(nb, dtype=np.int32),
-        "res": np.zeros((nb, 4)), "obj": np.zeros(nb),
+        "res": np.zeros((nb, 4)), "obj": np.zeros(nb), "lq_iters": np.zeros(nb, dtype=np.int32),
     }
     if x_init is not None:
         out["x"][:] = x_init
@@ -152,6 +154,7 @@ def solve(batch, settings: Optional[Dict] = None, x0: Optional[np.ndarray] = Non
         out["status"][i], out["iter"][i] = r.status, r.iter
         out["res"][i] = list(r.res)
         out["obj"][i] = r.obj
+        out["lq_iters"][i] = r.lq_iters
     return out
 
 

@@ -133,3 +133,63 @@ def test_itref_oracle(OcpQpBatch, oracle, ng):
     plain = oracle.solve(qp, dict(tiny, itref_corr_max=0), x0=x0)
     for i in range(qp.batch):
         assert helpers.is_approx(ref["u"][i], plain["u"][i], 1e-6), i
+
+
+@pytest.mark.parametrize("ric_alg", [0, 1])
+@pytest.mark.parametrize("dims", [(12, 12, 0), (6, 4, 3), (12, 12, 4)])
+def test_lq_fact_oracle(OcpQpBatch, oracle, dims, ric_alg):
+    """The oracle's restatement of HPIPM's lq_fact (the stage factor by an LQ
+    factorization of [chol(RSQ) | sqrt(Gamma) rows | [B'; A'] Lx_{k+1}], Gamma never added to
+    the data).  lq_fact 2 takes the same iterations as the Cholesky and lands on its solution
+    at rounding level; lq_fact 1 keeps the Cholesky while the predictor's linear residual stays
+    below 1e-5, which it does on these regular QPs.  (HPIPM is not vendored: parity against
+    HPIPM itself is unpinned; the HIP library does not build lq_fact.)"""
+    nx, nu, ng = dims
+    qp, x0 = helpers.random_constrained(8, 10, nx, nu, ng, 5, OcpQpBatch)
+    base = dict(iter_max=30, ric_alg=ric_alg)
+    chol = oracle.solve(qp, base, x0=x0)
+    assert np.all(chol["status"] == 0) and np.all(chol["lq_iters"] == 0)
+    lq = oracle.solve(qp, dict(base, lq_fact=2), x0=x0)
+    assert np.array_equal(lq["status"], chol["status"]) and np.array_equal(lq["iter"], chol["iter"])
+    assert np.array_equal(lq["lq_iters"], lq["iter"])
+    # x, u agree to ~1e-11 (measured); pi, the dynamics multipliers, only to the stationarity
+    # tolerance scaled by the active bounds' barrier weights (measured up to 3e-6)
+    for i in range(qp.batch):
+        for key, tol in (("x", 1e-9), ("u", 1e-9), ("pi", 1e-5)):
+            assert helpers.is_approx(lq[key][i], chol[key][i], tol), (key, i)
+    mix = oracle.solve(qp, dict(base, lq_fact=1), x0=x0)
+    assert np.all(mix["lq_iters"] == 0)
+    assert np.array_equal(mix["u"], chol["u"])
+
+
+def test_lq_fact_oracle_degenerate_endgame(OcpQpBatch, oracle):
+    """The near-degenerate family of tests/test_gpu_ipm.py test_degenerate_endgame_family (QP
+    #12 of (12, 4, 14) seed 200, 64 copies perturbed at 1e-15) in Speed with the square-root
+    Riccati: the Cholesky converges on 63 of 64 (measured), the LQ factorization, which never
+    forms the ~1e13 barrier sums, on all 64; lq_fact 1 switches on the copies whose predictor
+    residual exceeds 1e-5."""
+    qp, x0 = helpers.random_constrained(20, 12, 12, 4, 14, 200, OcpQpBatch)
+    M = 64
+    rng = np.random.default_rng(7)
+    fields = {}
+    for name in ("Q", "R", "S", "A", "B", "q", "r", "b", "C", "D", "lg", "ug", "lbu", "ubu", "lbx",
+                 "ubx", "lg_mask", "ug_mask", "lbu_mask", "ubu_mask", "lbx_mask", "ubx_mask"):
+        a = getattr(qp, name, None)
+        if a is None:
+            continue
+        a = np.repeat(np.asarray(a)[12:13], M, axis=0)
+        if name in ("Q", "R", "S", "A", "B", "q", "r", "b"):
+            a = a * (1 + 1e-15 * rng.standard_normal(a.shape))
+        fields[name] = a
+    fam = OcpQpBatch(N=qp.N, nx=qp.nx, nu=qp.nu, ng=qp.ng, **fields)
+    xb = np.repeat(np.asarray(x0)[12:13], M, axis=0)
+    st = dict(iter_max=50, mode="Speed", ric_alg=1)
+    chol = oracle.solve(fam, st, x0=xb)
+    lq = oracle.solve(fam, dict(st, lq_fact=2), x0=xb)
+    mix = oracle.solve(fam, dict(st, lq_fact=1), x0=xb)
+    assert (chol["status"] == 0).sum() >= 63
+    assert (lq["status"] == 0).sum() == 64
+    assert (mix["status"] == 0).sum() >= 63 and mix["lq_iters"].sum() > 0
+    for i in range(M):
+        if chol["status"][i] == 0:
+            assert helpers.is_approx(lq["u"][i], chol["u"][i], 1e-6), i
