@@ -24,6 +24,15 @@ using real = SRBD_REAL;
 #ifndef SRBD_SQRT_EXPLICIT_P
 #define SRBD_SQRT_EXPLICIT_P 0
 #endif
+// diagnostic builds: ric_alg 1 carries P_k as the oracle's riccati_factor does -- Lp = chol(P_k),
+// then P_k := Lp Lp' (explicit, for the record with SRBD_SQRT_EXPLICIT_P) and the next stage's
+// factor is chol(Lp Lp') -- instead of Lp itself (equal in exact arithmetic).  On the
+// degenerate endgame family in Speed: 51 / 48 / 46 of 64 (alone / with SRBD_SQRT_SYMP / with
+// both and SRBD_SQRT_EXPLICIT_P), against the product's 48, and further from the oracle
+// (profiles/round4/endgame_counts_ric1_recon.log)
+#ifndef SRBD_SQRT_RECON
+#define SRBD_SQRT_RECON 0
+#endif
 // fp64 box RB (12 x 12 blocks): Q_k reaches the group's LDS by LDS-DMA issued before the
 // Cholesky of G instead of by register loads after it (one memory round trip less on the
 // stage's chain, no VGPRs held across the Cholesky).  Measured slower (box-u 78.90 vs 78.05 ms
@@ -1368,6 +1377,26 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         });
         if constexpr (SQRT) {
           sqrt_factor(P, lane);
+          if constexpr (SRBD_SQRT_RECON != 0) {
+            // P_k := Lp Lp' (rows of Lp through a free LDS slot: behind the record image in the
+            // box kernels, the dead A block in the general-row ones), p_k kept; Lp := chol(P_k)
+            static_assert(kRecSize + 78 <= kGroupLds<GEN>, "scratch slot");
+            real* const scr = ldsA + (kRecImg<GEN> ? kRecSize : 0);
+            lds_wave_fence();
+            if (lane < kMaxDim) store_packed_col(scr, lane, P);
+            lds_wave_fence();
+            real Lr[12];
+            load_packed_lrow_d(scr, col, Lr);
+            sfor<0, 12>([&](auto i) { P[decltype(i)::value] = real(0.0); });
+            tmul_acc(Lr, Lr, P);
+            sfor<0, 12>([&](auto i) {
+              constexpr int I = decltype(i)::value;
+              if (lane >= kMaxDim) P[I] = f.F[I];  // p_k on VL; the pad lanes as before
+            });
+            if constexpr (!kRecFactor)
+              if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
+            sqrt_factor(P, lane);
+          }
           if constexpr (kRecFactor)
             if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
         }
