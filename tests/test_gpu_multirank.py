@@ -87,3 +87,39 @@ def test_two_ranks_config4_shard_solve_gather(tmp_path):
     assert res["rank0_ok"] == PER_RANK and res["global_ok"] == world * PER_RANK
     assert res["t_max"] == 2.0  # the slowest rank's time
     assert res["bitwise_equal"], res["max_abs_diff"]
+
+
+def _rccl_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    try:
+        bench = _bench()
+        pkg = bench.import_pkg()
+        device = torch.device("cuda", 0)
+        h, dt, sol_t = _solve_shard(bench, pkg, 4096, rank, device)
+        dist.barrier()
+        got = bench.gather_solutions(pkg, sol_t, world, rank, cpu_staged=False)
+        torch.cuda.synchronize()
+        walls = [None] * world
+        dist.all_gather_object(walls, 1.5)
+        want = pkg.dist.solution_payload(sol_t["x"], sol_t["u"], sol_t["pi"])
+        res = {"n": len(got), "device": str(got[0].device), "equal": bool(torch.equal(got[0], want)),
+               "walls": walls, "backend": dist.get_backend()}
+        (Path(out_dir) / "rccl.json").write_text(json.dumps(res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_single_rank_gather(tmp_path):
+    """bench.py's RCCL branch (the nccl process group, dist.gather of device tensors in
+    gather_solutions, barrier, all_gather_object) executed for real with one rank on cuda:0 --
+    one GPU cannot hold two RCCL ranks; the config-4 collective across 8 devices is the
+    driver's run."""
+    import torch.multiprocessing as mp
+    mp.spawn(_rccl_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
+    res = json.loads((tmp_path / "rccl.json").read_text())
+    assert res["backend"] == "nccl" and res["n"] == 1 and res["device"] == "cuda:0"
+    assert res["equal"] and res["walls"] == [1.5]
