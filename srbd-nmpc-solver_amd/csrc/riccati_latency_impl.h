@@ -61,12 +61,21 @@ size_t lat_lds_bytes(int N) { return (size_t)(lat_scr_off(N) + lat_scr_size(N)) 
 // (3 dependent FMAs instead of the IEEE division's ~10 instructions on the stage's critical
 // path); otherwise chol_cols (riccati.h): `reg` on each pivot, a non-positive pivot zeroes
 // its column (BLASFEO dpotrf_l).
+// (one Newton step, -DSRBD_LAT_NEWTON=1: the riccati GPU tests pass and the call pattern moves
+// 99.0 / 99.8 vs 100.2 / 99.9 us on one box, within its noise -- kept at two;
+// profiles/round4/newton_call_pattern.log)
+#ifndef SRBD_LAT_NEWTON
+#define SRBD_LAT_NEWTON 2
+#endif
 __device__ __forceinline__ double lat_recip(double d) {
   double r = __builtin_amdgcn_rcp(d);
   double e = __builtin_fma(-d, r, 1.0);
   r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-d, r, 1.0);
-  return __builtin_fma(r, e, r);
+  if constexpr (SRBD_LAT_NEWTON >= 2) {
+    e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+  }
+  return r;
 }
 // `hook(ic<K>)` runs at the top of pivot K: the caller issues its independent matrix-core
 // work there, one MFMA per pivot, so the MFMA pipe runs beside the pivots' VALU chain
