@@ -374,18 +374,22 @@ __device__ __forceinline__ const real* img_source(const ProblemArgsT<real>& a, i
 
 // The QP's blocks into the LDS image by every thread of the workgroup (global->LDS DMA;
 // the source may be device memory or mapped host memory), waited for and fenced.
-__device__ __forceinline__ void lds_copy_qp(const ProblemArgsT<real>& a, real* img, int qp) {
-  const int lane = threadIdx.x;
-  const int total = (a.N + 1) * kImgStage;
-  const int wave_off = (lane >> 6) * 64 * kRealsPerDma;  // this wave's 1 KiB of each round
-  for (int c0 = 0; c0 < total; c0 += kLdsCopyThreads * kRealsPerDma) {
-    const int e = c0 + lane * kRealsPerDma;
-    const real* g = e < total ? img_source(a, qp, e) : nullptr;
+// Image elements [e0, e1) (e0 even) issued by nthr threads (whole waves; t = 0..nthr-1 the
+// thread's rank among them); not waited for.
+__device__ __forceinline__ void lds_copy_range(const ProblemArgsT<real>& a, real* img, int qp, int e0, int e1,
+                                               int t, int nthr) {
+  const int wave_off = (t >> 6) * 64 * kRealsPerDma;  // this wave's 1 KiB of each round
+  for (int c0 = e0; c0 < e1; c0 += nthr * kRealsPerDma) {
+    const int e = c0 + t * kRealsPerDma;
+    const real* g = e < e1 ? img_source(a, qp, e) : nullptr;
     if (g)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                        (__attribute__((address_space(3))) void*)(img + c0 + wave_off), 16,
                                        0, 0);
   }
+}
+__device__ __forceinline__ void lds_copy_qp(const ProblemArgsT<real>& a, real* img, int qp) {
+  lds_copy_range(a, img, qp, 0, (a.N + 1) * kImgStage, threadIdx.x, kLdsCopyThreads);
   tstamp(14);  // (kernel entry is the first stamp of a launch: the copy into LDS ends here)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
