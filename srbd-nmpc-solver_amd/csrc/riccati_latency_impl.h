@@ -68,7 +68,8 @@ size_t lat_lds_bytes(int N) { return (size_t)(lat_scr_off(N) + lat_scr_size(N)) 
 // (1), or all before it (0).  Streaming measured 103.6 / 104.0 vs 102.3 / 103.1 us per call on
 // one box (profiles/round4/stream_call_pattern.log): each stage's mapped-host read waits a
 // PCIe round trip, longer than the stage it hides behind, and __syncthreads drains any deeper
-// lookahead.  Off.
+// lookahead.  A two-stage lookahead (inline-asm LDS-DMA, raw barriers in the sweep) measured
+// 113.6-124.0 vs 101.4-106.2 us (profiles/round4/stream_call_pattern.log).  Off.
 #ifndef SRBD_LAT_STREAM
 #define SRBD_LAT_STREAM 0
 #endif
