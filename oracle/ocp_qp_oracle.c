@@ -27,9 +27,7 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
-#ifdef ORACLE_DEBUG
 #include <stdio.h>
-#endif
 
 #define IPM_THR0 0.1      /* minimum initial slack (HPIPM init_var)          */
 #define IPM_STEP_TAU 0.995 /* fraction-to-boundary factor                     */
@@ -334,6 +332,293 @@ static int riccati_factor(const dims_t* d, ric_ws_t* w, double reg, int sqrt_alg
     }
   }
   return 0;
+}
+
+/* EXPERIMENT (env ORACLE_SQRT_HPIPM=1): HPIPM's square-root factor and solve as its kkt
+ * routines form them -- the stage factor L_k = chol(Ht_k + AL AL'), AL = [B'; A'] Lx_{k+1}, is
+ * carried (never re-formed from an explicit P), the vectors follow d_ocp_qp_solve_kkt_step
+ * (Pb = Lx (Lx' b), l = g + [B'; A'](Pb + p), y = Lu^-1 l_u, p_k = l_x - Lxu y) and the forward
+ * sweep du = -Lu^-T (y + Lxu' dx), dpi = Lx (Lx' dx) + p: no explicit K or P on the solve path. */
+static double* g_Lfull; /* (N+1) n x n stage factors [Lu 0; Lxu Lx] ([u; x] order)            */
+static double* g_yv;    /* N x nu */
+static int g_classical;
+static int sqrt_factor_hpipm(const dims_t* d, ric_ws_t* w, double reg) {
+  const int nx = d->nx, nu = d->nu, n = nx + nu, N = d->N;
+  double M[64 * 64], AL[64 * 32];
+  {
+    double* LN = g_Lfull + (size_t)N * n * n;
+    memcpy(LN, w->Ht + (size_t)N * w->hstride, sizeof(double) * nx * nx);
+    chol(nx, LN);
+  }
+  for (int k = N - 1; k >= 0; --k) {
+    const double* A = qA(d, k);
+    const double* B = qB(d, k);
+    const double* Ln = g_Lfull + (size_t)(k + 1) * n * n; /* stage k+1 */
+    const int nun = k + 1 < N ? nu : 0;
+    const int ldn = nun + nx;
+    /* Lx_{k+1} = Ln[nun:, nun:] */
+    if (g_classical) {
+      /* HPIPM classical: AL = [B'; A'] P_{k+1} with P_{k+1} = Lx Lx' formed, M = Ht + AL [B A] */
+      double P1[32 * 32], BA[64 * 32];
+      for (int j = 0; j < nx; ++j)
+        for (int i = 0; i < nx; ++i) {
+          double s = 0.0;
+          for (int l = 0; l < nx; ++l) s += M_(Ln, ldn, nun + i, nun + l) * M_(Ln, ldn, nun + j, nun + l);
+          M_(P1, nx, i, j) = s;
+        }
+      for (int j = 0; j < nx; ++j) { /* BA' = [B'; A'] (n x nx) */
+        for (int i = 0; i < nu; ++i) M_(BA, n, i, j) = M_(B, nx, j, i);
+        for (int i = 0; i < nx; ++i) M_(BA, n, nu + i, j) = M_(A, nx, j, i);
+      }
+      for (int j = 0; j < nx; ++j)
+        for (int i = 0; i < n; ++i) {
+          double s = 0.0;
+          for (int l = 0; l < nx; ++l) s += M_(BA, n, i, l) * M_(P1, nx, l, j);
+          M_(AL, n, i, j) = s;
+        }
+      const double* Ht = w->Ht + (size_t)k * w->hstride;
+      for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i) {
+          double s = M_(Ht, n, i, j);
+          for (int l = 0; l < nx; ++l) s += M_(AL, n, i, l) * M_(BA, n, j, l);
+          M_(M, n, i, j) = s;
+        }
+      for (int i = 0; i < nu; ++i) M_(M, n, i, i) += reg;
+      chol(n, M);
+      memcpy(g_Lfull + (size_t)k * n * n, M, sizeof(double) * n * n);
+      continue;
+    }
+    for (int j = 0; j < nx; ++j) {
+      for (int i = 0; i < nu; ++i) {
+        double s = 0.0;
+        for (int l = j; l < nx; ++l) s += M_(B, nx, l, i) * M_(Ln, ldn, nun + l, nun + j);
+        M_(AL, n, i, j) = s;
+      }
+      for (int i = 0; i < nx; ++i) {
+        double s = 0.0;
+        for (int l = j; l < nx; ++l) s += M_(A, nx, l, i) * M_(Ln, ldn, nun + l, nun + j);
+        M_(AL, n, nu + i, j) = s;
+      }
+    }
+    const double* Ht = w->Ht + (size_t)k * w->hstride;
+    for (int j = 0; j < n; ++j)
+      for (int i = 0; i < n; ++i) {
+        double s = M_(Ht, n, i, j);
+        for (int l = 0; l < nx; ++l) s += M_(AL, n, i, l) * M_(AL, n, j, l);
+        M_(M, n, i, j) = s;
+      }
+    for (int i = 0; i < nu; ++i) M_(M, n, i, i) += reg;
+    if (getenv("ORACLE_SCHUR_TEXTBOOK")) {
+      /* Lx = chol(F + H'K), K = -G^-1 H (two triangular solves), averaged with its transpose */
+      double Lu[32 * 32], Kt[32 * 32], Pk[32 * 32];
+      for (int j = 0; j < nu; ++j) for (int i = 0; i < nu; ++i) M_(Lu, nu, i, j) = M_(M, n, i, j);
+      chol(nu, Lu);
+      for (int j = 0; j < nx; ++j) {
+        double col[32];
+        for (int i = 0; i < nu; ++i) col[i] = M_(M, n, i, nu + j);
+        chol_solve(nu, Lu, col);
+        for (int i = 0; i < nu; ++i) M_(Kt, nu, i, j) = -col[i];
+      }
+      for (int j = 0; j < nx; ++j)
+        for (int i = 0; i < nx; ++i) {
+          double s = M_(M, n, nu + i, nu + j);
+          for (int l = 0; l < nu; ++l) s += M_(M, n, l, nu + i) * M_(Kt, nu, l, j);
+          M_(Pk, nx, i, j) = s;
+        }
+      for (int j = 0; j < nx; ++j)
+        for (int i = j + 1; i < nx; ++i) {
+          double s = 0.5 * (M_(Pk, nx, i, j) + M_(Pk, nx, j, i));
+          M_(Pk, nx, i, j) = s; M_(Pk, nx, j, i) = s;
+        }
+      chol(nx, Pk);
+      chol(n, M); /* Lu, Lxu as the joint factor has them */
+      for (int j = 0; j < nx; ++j) for (int i = 0; i < nx; ++i) M_(M, n, nu + i, nu + j) = M_(Pk, nx, i, j);
+    } else {
+      chol(n, M);
+    }
+    if (getenv("ORACLE_REFACTOR")) { /* Lx := chol(Lx Lx') */
+      double Pk[32 * 32];
+      for (int j = 0; j < nx; ++j)
+        for (int i = 0; i < nx; ++i) {
+          double s = 0.0;
+          for (int l = 0; l < nx; ++l) s += M_(M, n, nu + i, nu + l) * M_(M, n, nu + j, nu + l);
+          M_(Pk, nx, i, j) = s;
+        }
+      chol(nx, Pk);
+      for (int j = 0; j < nx; ++j) for (int i = 0; i < nx; ++i) M_(M, n, nu + i, nu + j) = M_(Pk, nx, i, j);
+    }
+    memcpy(g_Lfull + (size_t)k * n * n, M, sizeof(double) * n * n);
+  }
+  /* P, K, Lg for the getters */
+  for (int k = 0; k <= N; ++k) {
+    const int nuk = k < N ? nu : 0, ld = nuk + nx;
+    const double* L = g_Lfull + (size_t)k * n * n;
+    double* P = w->P + (size_t)k * nx * nx;
+    for (int j = 0; j < nx; ++j)
+      for (int i = 0; i < nx; ++i) {
+        double s = 0.0;
+        for (int l = 0; l < nx; ++l) s += M_(L, ld, nuk + i, nuk + l) * M_(L, ld, nuk + j, nuk + l);
+        M_(P, nx, i, j) = s;
+      }
+    if (k == N) continue;
+    double* Lg = w->Lg + (size_t)k * nu * nu;
+    for (int j = 0; j < nu; ++j)
+      for (int i = 0; i < nu; ++i) M_(Lg, nu, i, j) = M_(L, ld, i, j);
+    double* K = w->K + (size_t)k * nu * nx;
+    for (int j = 0; j < nx; ++j) { /* K[:, j] = -Lu^-T Lxu[j, :]' */
+      double col[32];
+      for (int i = 0; i < nu; ++i) col[i] = M_(L, ld, nu + j, i);
+      for (int i = nu - 1; i >= 0; --i) {
+        double s = col[i];
+        for (int l = i + 1; l < nu; ++l) s -= M_(L, ld, l, i) * col[l];
+        const double dd = M_(L, ld, i, i);
+        col[i] = dd > 0.0 ? s / dd : 0.0;
+      }
+      for (int i = 0; i < nu; ++i) M_(K, nu, i, j) = -col[i];
+    }
+  }
+  return 0;
+}
+static int g_sform; /* 1: the vectors travel as s = Lx^-1 p (fact_solve's last factor row) */
+/* x := Lx^-1 x (stage factor L, x part), zero pivots give zero */
+static void lx_solve(const double* L, int ld, int off, int nx, double* x) {
+  for (int i = 0; i < nx; ++i) {
+    double s = x[i];
+    for (int l = 0; l < i; ++l) s -= M_(L, ld, off + i, off + l) * x[l];
+    const double dd = M_(L, ld, off + i, off + i);
+    x[i] = dd > 0.0 ? s / dd : 0.0;
+  }
+}
+static void sqrt_vectors_hpipm_s(const dims_t* d, ric_ws_t* w) {
+  const int nx = d->nx, nu = d->nu, n = nx + nu, N = d->N;
+  double* pN = w->p + (size_t)N * nx;
+  memcpy(pN, w->gt + (size_t)N * w->gstride, sizeof(double) * nx);
+  lx_solve(g_Lfull + (size_t)N * n * n, nx, 0, nx, pN);
+  for (int k = N - 1; k >= 0; --k) {
+    const double* Ln = g_Lfull + (size_t)(k + 1) * n * n;
+    const int nun = k + 1 < N ? nu : 0, ldn = nun + nx;
+    const double* bt = w->bt + (size_t)k * nx;
+    double m[32];
+    for (int j = 0; j < nx; ++j) { /* m = Lx' b + s */
+      double sacc = 0.0;
+      for (int l = j; l < nx; ++l) sacc += M_(Ln, ldn, nun + l, nun + j) * bt[l];
+      m[j] = sacc + w->p[(size_t)(k + 1) * nx + j];
+    }
+    const double* A = qA(d, k);
+    const double* B = qB(d, k);
+    const double* gt = w->gt + (size_t)k * w->gstride;
+    double l_[64];
+    for (int i = 0; i < n; ++i) { /* l = g + AL m, AL = [B'; A'] Lx */
+      double acc = gt[i];
+      for (int j = 0; j < nx; ++j) {
+        double al = 0.0;
+        for (int q = j; q < nx; ++q)
+          al += (i < nu ? M_(B, nx, q, i) : M_(A, nx, q, i - nu)) * M_(Ln, ldn, nun + q, nun + j);
+        acc += al * m[j];
+      }
+      l_[i] = acc;
+    }
+    const double* L = g_Lfull + (size_t)k * n * n;
+    double* y = g_yv + (size_t)k * nu;
+    for (int i = 0; i < nu; ++i) {
+      double sacc = l_[i];
+      for (int q = 0; q < i; ++q) sacc -= M_(L, n, i, q) * y[q];
+      const double dd = M_(L, n, i, i);
+      y[i] = dd > 0.0 ? sacc / dd : 0.0;
+    }
+    double* sk = w->p + (size_t)k * nx;
+    for (int i = 0; i < nx; ++i) {
+      double sacc = l_[nu + i];
+      for (int q = 0; q < nu; ++q) sacc -= M_(L, n, nu + i, q) * y[q];
+      sk[i] = sacc;
+    }
+    lx_solve(L, n, nu, nx, sk);
+  }
+}
+static void sqrt_vectors_hpipm(const dims_t* d, ric_ws_t* w) {
+  const int nx = d->nx, nu = d->nu, n = nx + nu, N = d->N;
+  if (g_sform) { sqrt_vectors_hpipm_s(d, w); return; }
+  memcpy(w->p + (size_t)N * nx, w->gt + (size_t)N * w->gstride, sizeof(double) * nx);
+  for (int k = N - 1; k >= 0; --k) {
+    const double* Ln = g_Lfull + (size_t)(k + 1) * n * n;
+    const int nun = k + 1 < N ? nu : 0, ldn = nun + nx;
+    const double* bt = w->bt + (size_t)k * nx;
+    double t[32], tmp[32];
+    for (int j = 0; j < nx; ++j) { /* Lx' b */
+      double s = 0.0;
+      for (int l = j; l < nx; ++l) s += M_(Ln, ldn, nun + l, nun + j) * bt[l];
+      t[j] = s;
+    }
+    for (int i = 0; i < nx; ++i) { /* Lx (Lx' b) + p */
+      double s = 0.0;
+      for (int l = 0; l <= i; ++l) s += M_(Ln, ldn, nun + i, nun + l) * t[l];
+      tmp[i] = s + w->p[(size_t)(k + 1) * nx + i];
+    }
+    const double* gt = w->gt + (size_t)k * w->gstride;
+    double lu[32], lx[32];
+    mtv(nx, nu, qB(d, k), tmp, lu);
+    mtv(nx, nx, qA(d, k), tmp, lx);
+    for (int i = 0; i < nu; ++i) lu[i] += gt[i];
+    for (int i = 0; i < nx; ++i) lx[i] += gt[nu + i];
+    const double* L = g_Lfull + (size_t)k * n * n;
+    double* y = g_yv + (size_t)k * nu;
+    for (int i = 0; i < nu; ++i) {
+      double s = lu[i];
+      for (int l = 0; l < i; ++l) s -= M_(L, n, i, l) * y[l];
+      const double dd = M_(L, n, i, i);
+      y[i] = dd > 0.0 ? s / dd : 0.0;
+    }
+    for (int i = 0; i < nx; ++i) {
+      double s = lx[i];
+      for (int l = 0; l < nu; ++l) s -= M_(L, n, nu + i, l) * y[l];
+      w->p[(size_t)k * nx + i] = s;
+    }
+  }
+}
+static void sqrt_forward_hpipm(const dims_t* d, const ric_ws_t* w, const double* xinit, double* x,
+                               double* u, double* pi) {
+  const int nx = d->nx, nu = d->nu, n = nx + nu, N = d->N;
+  memcpy(x, xinit, sizeof(double) * nx);
+  for (int k = 0; k < N; ++k) {
+    const double* L = g_Lfull + (size_t)k * n * n;
+    const double* xk = x + (size_t)k * nx;
+    double* uk = u + (size_t)k * nu;
+    double v[32];
+    for (int i = 0; i < nu; ++i) { /* y + Lxu' x */
+      double s = g_yv[(size_t)k * nu + i];
+      for (int l = 0; l < nx; ++l) s += M_(L, n, nu + l, i) * xk[l];
+      v[i] = -s;
+    }
+    for (int i = nu - 1; i >= 0; --i) {
+      double s = v[i];
+      for (int l = i + 1; l < nu; ++l) s -= M_(L, n, l, i) * v[l];
+      const double dd = M_(L, n, i, i);
+      v[i] = dd > 0.0 ? s / dd : 0.0;
+    }
+    memcpy(uk, v, sizeof(double) * nu);
+    double t1[32], t2[32];
+    mv(nx, nx, qA(d, k), xk, t1);
+    mv(nx, nu, qB(d, k), uk, t2);
+    double* x1 = x + (size_t)(k + 1) * nx;
+    for (int i = 0; i < nx; ++i) x1[i] = t1[i] + t2[i] + w->bt[(size_t)k * nx + i];
+  }
+  for (int k = 1; k <= N; ++k) {
+    const double* L = g_Lfull + (size_t)k * n * n;
+    const int nuk = k < N ? nu : 0, ld = nuk + nx;
+    const double* xk = x + (size_t)k * nx;
+    double t[32];
+    for (int j = 0; j < nx; ++j) {
+      double s = 0.0;
+      for (int l = j; l < nx; ++l) s += M_(L, ld, nuk + l, nuk + j) * xk[l];
+      t[j] = s;
+    }
+    if (g_sform) for (int j = 0; j < nx; ++j) t[j] += w->p[(size_t)k * nx + j];
+    for (int i = 0; i < nx; ++i) {
+      double s = 0.0;
+      for (int l = 0; l <= i; ++l) s += M_(L, ld, nuk + i, nuk + l) * t[l];
+      pi[(size_t)k * nx + i] = s + (g_sform ? 0.0 : w->p[(size_t)k * nx + i]);
+    }
+  }
 }
 
 /* LQ factorization with a positive diagonal of the n x m matrix M (column-major, ld n), in
@@ -808,6 +1093,15 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
 
   double alpha_prim = 1.0, alpha_dual = 1.0;
   int iter = 0;
+  const int hp = !set->lq_fact && getenv("ORACLE_SQRT_HPIPM") && getenv("ORACLE_SQRT_HPIPM")[0] == '1';
+  g_classical = !set->ric_alg;
+  if (hp) {
+    g_Lfull = (double*)calloc((size_t)(N + 1) * n * n, sizeof(double));
+    g_yv = (double*)calloc((size_t)N * nu + 1, sizeof(double));
+  }
+  const int hps = hp && !getenv("ORACLE_SQRT_CLASSIC");
+#define VECTORS() do { if (hps) sqrt_vectors_hpipm(&d, &w); else riccati_vectors(&d, &w); } while (0)
+#define FORWARD(X, U, PI) do { if (hps) sqrt_forward_hpipm(&d, &w, zero, X, U, PI); else riccati_forward(&d, &w, zero, X, U, PI); } while (0)
   int force_lq = set->lq_fact == 2;  /* lq_fact 1 switches for the rest of the solve */
   for (;;) {
     compute_residuals(&d, st, x, u, pi, rg, rb, res->res, &res->obj, w.gstride);
@@ -847,9 +1141,12 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
       if (s < N) memcpy(w.bt + (size_t)s * nx, rb + (size_t)s * nx, sizeof(double) * nx);
     }
     if (force_lq ? riccati_factor_lq(&d, &w, st, set->reg_prim)
-                 : riccati_factor(&d, &w, set->reg_prim, set->ric_alg)) { res->status = 3; break; }
-    riccati_vectors(&d, &w);
-    riccati_forward(&d, &w, zero, dx, du, dpi);
+                 : (hp ? sqrt_factor_hpipm(&d, &w, set->reg_prim)
+                       : riccati_factor(&d, &w, set->reg_prim, set->ric_alg))) { res->status = 3; break; }
+    g_sform = hp && getenv("ORACLE_SQRT_SFORM") != NULL;
+    VECTORS();
+    FORWARD(dx, du, dpi);
+    g_sform = 0;
 #ifdef ORACLE_DEBUG
     {
       double tmin = 1e300, lmax = 0;
@@ -947,9 +1244,14 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
           row_axpy(&d, rw, nu_k, gam, gt, gt + nu_k);
         }
       }
-      riccati_vectors(&d, &w);
-      riccati_forward(&d, &w, zero, dx, du, dpi);
+      VECTORS();
+      FORWARD(dx, du, dpi);
       STEP_TLAM();
+    }
+    if (getenv("ORACLE_LINRES_DIAG")) {
+      double ng = 0.0, nb = 0.0;
+      lin_res(&d, st, &w, rg, rb, du, dx, dpi, itg, itb, &ng, &nb);
+      fprintf(stderr, "LINRES %d %.3e %.3e %.3e\n", iter, mu, ng, res->res[0]);
     }
     /* iterative refinement of the final step (HPIPM itref_corr_max: Balance 2, Robust 4;
      * restated from HPIPM's d_ocp_qp_ipm_solve / d_ocp_qp_res_compute_lin, not vendored):
@@ -969,8 +1271,8 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
         /* correction: same factors, right-hand side = the residual */
         double* gkeep = w.gt; double* bkeep = w.bt;
         w.gt = itg; w.bt = itb;
-        riccati_vectors(&d, &w);
-        riccati_forward(&d, &w, zero, cdx, cdu, cdpi);
+        VECTORS();
+        FORWARD(cdx, cdu, cdpi);
         w.gt = gkeep; w.bt = bkeep;
         for (size_t i = 0; i < (size_t)(N + 1) * nx; ++i) { dx[i] += cdx[i]; if (i >= (size_t)nx) dpi[i] += cdpi[i]; }
         for (size_t i = 0; i < (size_t)N * nu; ++i) du[i] += cdu[i];
@@ -1036,6 +1338,9 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
     ++iter;
   }
   res->iter = iter;
+#undef VECTORS
+#undef FORWARD
+  if (hp) { free(g_Lfull); free(g_yv); g_Lfull = NULL; g_yv = NULL; }
 
   /* Riccati outputs (P, K) are those of the last factorization performed by
    * the IPM (the last step's barrier-augmented KKT system), as HPIPM's
