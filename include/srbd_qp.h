@@ -257,7 +257,10 @@ int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* 
  * others set NULL.  A caller that packs its QPs there and then passes the same
  * two structs to srbd_qp_solve_host_f64 saves both staging copies (the solve
  * skips a copy whose source already is its place); the outputs are left there.
- * Valid until the handle stages a larger call or is destroyed; SRBD_QP_ECAPACITY
+ * The pointers are invalidated by the handle's destruction and by ANY later
+ * srbd_qp_solve_host_* or srbd_qp_host_staging_* call on the handle that needs a
+ * larger staging buffer (the old pinned buffer is freed): re-stage after such a
+ * call, as the hpipm-cpp shim does on every solve.  SRBD_QP_ECAPACITY
  * when the call's buffers exceed the pinned staging size (8 MiB).  Replaces the
  * Eigen-pointer marshalling of ocp_qp_ipm_solver.cpp:226-289 for the shim.
  * (ABI 10)                                                                  */

@@ -27,7 +27,9 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef ORACLE_DEBUG
 #include <stdio.h>
+#endif
 
 #define IPM_THR0 0.1      /* minimum initial slack (HPIPM init_var)          */
 #define IPM_STEP_TAU 0.995 /* fraction-to-boundary factor                     */
@@ -254,41 +256,33 @@ typedef struct {
   double* kk;  /* N nu        */
   double* Lg;  /* N nu*nu (chol of G)                                     */
   size_t hstride, gstride;
+  /* ric_alg != 0 (square root, HPIPM's form): the stage factors and y = Lu^-1 l_u    */
+  double* Lf;  /* (N+1) n*n: stage k < N [Lu 0; Lxu Lx] (ld n), stage N Lx (ld nx)   */
+  double* yv;  /* N nu                                                               */
+  int sq;      /* 1 once the last factorization was the square-root one              */
+  int sform;   /* 1: the vectors travel as s = Lx^-1 p (fact_solve), 0: p           */
 } ric_ws_t;
 
-/* ric_alg = 0: the textbook recursion (test/ocp_qp_ipm_solver.cpp:67-90).
- * ric_alg != 0: HPIPM's square-root variant (square_root_alg, hpipm-cpp default
- * ocp_qp_ipm_solver_settings.hpp:81): with Lp = chol(P_{k+1}), the stage terms are
- * sums of squares, G = R + (Lp'B)'(Lp'B), H = S + (Lp'B)'(Lp'A), F = Q + (Lp'A)'(Lp'A),
- * and P_k = Lx Lx' with Lx = chol(F - H'G^-1 H) (the trailing factor of the
- * stage's dsyrk_dpotrf); equal to the textbook P_k in exact arithmetic.        */
-static int riccati_factor(const dims_t* d, ric_ws_t* w, double reg, int sqrt_alg) {
+/* ric_alg = 0: the textbook recursion (test/ocp_qp_ipm_solver.cpp:67-90): F, H, G from
+ * P_{k+1}, K = -G^-1 H, P_k = F + H'K symmetrised (the square-root variant is
+ * sqrt_factor below).                                                               */
+static int riccati_factor(const dims_t* d, ric_ws_t* w, double reg) {
   const int nx = d->nx, nu = d->nu, n = nx + nu, N = d->N;
-  double PA[32 * 32], PB[32 * 32], G[32 * 32], Hm[32 * 32], F[32 * 32], Lp[32 * 32];
+  double PA[32 * 32], PB[32 * 32], G[32 * 32], Hm[32 * 32], F[32 * 32];
   double* PN = w->P + (size_t)N * nx * nx;
   const double* HtN = w->Ht + (size_t)N * w->hstride;
   memcpy(PN, HtN, sizeof(double) * nx * nx);
+  w->sq = 0;
   for (int k = N - 1; k >= 0; --k) {
     const double* A = qA(d, k);
     const double* B = qB(d, k);
     const double* P1 = w->P + (size_t)(k + 1) * nx * nx;
     const double* Ht = w->Ht + (size_t)k * w->hstride;
-    if (sqrt_alg) {
-      /* PA := Lp'A, PB := Lp'B; G = PB'PB, H = PB'PA, F = PA'PA */
-      memcpy(Lp, P1, sizeof(double) * nx * nx);
-      chol(nx, Lp);
-      mtm(nx, nx, nx, Lp, A, PA);
-      mtm(nx, nu, nx, Lp, B, PB);
-      mtm(nu, nu, nx, PB, PB, G);
-      mtm(nu, nx, nx, PB, PA, Hm);
-      mtm(nx, nx, nx, PA, PA, F);
-    } else {
-      mm(nx, nx, nx, P1, A, PA);
-      mm(nx, nu, nx, P1, B, PB);
-      mtm(nu, nu, nx, B, PB, G);
-      mtm(nu, nx, nx, B, PA, Hm);
-      mtm(nx, nx, nx, A, PA, F);
-    }
+    mm(nx, nx, nx, P1, A, PA);
+    mm(nx, nu, nx, P1, B, PB);
+    mtm(nu, nu, nx, B, PB, G);
+    mtm(nu, nx, nx, B, PA, Hm);
+    mtm(nx, nx, nx, A, PA, F);
     for (int j = 0; j < nu; ++j)
       for (int i = 0; i < nu; ++i) M_(G, nu, i, j) += M_(Ht, n, i, j);
     for (int i = 0; i < nu; ++i) M_(G, nu, i, i) += reg;
@@ -320,74 +314,43 @@ static int riccati_factor(const dims_t* d, ric_ws_t* w, double reg, int sqrt_alg
         double s = 0.5 * (M_(P, nx, i, j) + M_(P, nx, j, i));
         M_(P, nx, i, j) = s; M_(P, nx, j, i) = s;
       }
-    if (sqrt_alg) { /* P_k = Lx Lx' */
-      memcpy(Lp, P, sizeof(double) * nx * nx);
-      chol(nx, Lp);
-      for (int j = 0; j < nx; ++j)
-        for (int i = 0; i < nx; ++i) {
-          double s = 0.0;
-          for (int l = 0; l < nx; ++l) s += M_(Lp, nx, i, l) * M_(Lp, nx, j, l);
-          M_(P, nx, i, j) = s;
-        }
-    }
   }
   return 0;
 }
 
-/* EXPERIMENT (env ORACLE_SQRT_HPIPM=1): HPIPM's square-root factor and solve as its kkt
- * routines form them -- the stage factor L_k = chol(Ht_k + AL AL'), AL = [B'; A'] Lx_{k+1}, is
- * carried (never re-formed from an explicit P), the vectors follow d_ocp_qp_solve_kkt_step
- * (Pb = Lx (Lx' b), l = g + [B'; A'](Pb + p), y = Lu^-1 l_u, p_k = l_x - Lxu y) and the forward
- * sweep du = -Lu^-T (y + Lxu' dx), dpi = Lx (Lx' dx) + p: no explicit K or P on the solve path. */
-static double* g_Lfull; /* (N+1) n x n stage factors [Lu 0; Lxu Lx] ([u; x] order)            */
-static double* g_yv;    /* N x nu */
-static int g_classical;
-static int sqrt_factor_hpipm(const dims_t* d, ric_ws_t* w, double reg) {
+/* ric_alg != 0: HPIPM's square-root Riccati (square_root_alg, the hpipm-cpp default
+ * ocp_qp_ipm_solver_settings.hpp:81) as its kkt routines form it (hpipm_d_ocp_qp_kkt.h:54-60;
+ * restated, the source is not vendored).  The stage factor is carried, never re-formed from an
+ * explicit P: with AL = [B'; A'] Lx_{k+1},
+ *     L_k = [Lu 0; Lxu Lx] = chol(Ht_k + AL AL')           (dsyrk_dpotrf_ln_mn, one 24 x 24 factor)
+ * so G = Lu Lu', H = Lxu Lu', P_k = Lx Lx' with Lx the trailing factor of the same elimination.
+ * The Riccati vector travels in the two forms HPIPM's ws->valid_ric_p names
+ * (hpipm_d_ocp_qp_ipm.h:134, "0 p*inv(L), 1 p"):
+ *   sform 1 (d_ocp_qp_fact_solve_kkt_step / _unconstr: the factor's last row):
+ *     m = Lx_{k+1}' b + s_{k+1}, l = g + AL m, y = Lu^-1 l_u, s_k = Lx^-1 (l_x - Lxu y)
+ *   sform 0 (d_ocp_qp_solve_kkt_step: the corrector and the refinement):
+ *     l = g + [B'; A'] (Lx_{k+1} (Lx_{k+1}' b) + p_{k+1}), y = Lu^-1 l_u, p_k = l_x - Lxu y
+ * and the forward substitution never forms K or P:
+ *     du = -Lu^-T (y + Lxu' dx), dx+ = A dx + B du + b, dpi = Lx (Lx' dx + s) | Lx (Lx' dx) + p.
+ * The HIP library's square-root kernels (riccati.h riccati_step_sqrt, ipm_box_impl.h SQRT)
+ * follow the same forms.                                                                     */
+static const double* sq_L(const ric_ws_t* w, const dims_t* d, int k) {
+  return w->Lf + (size_t)k * (size_t)d->n * d->n;
+}
+static int sqrt_factor(const dims_t* d, ric_ws_t* w, double reg) {
   const int nx = d->nx, nu = d->nu, n = nx + nu, N = d->N;
   double M[64 * 64], AL[64 * 32];
+  w->sq = 1;
   {
-    double* LN = g_Lfull + (size_t)N * n * n;
+    double* LN = w->Lf + (size_t)N * n * n;
     memcpy(LN, w->Ht + (size_t)N * w->hstride, sizeof(double) * nx * nx);
     chol(nx, LN);
   }
   for (int k = N - 1; k >= 0; --k) {
     const double* A = qA(d, k);
     const double* B = qB(d, k);
-    const double* Ln = g_Lfull + (size_t)(k + 1) * n * n; /* stage k+1 */
-    const int nun = k + 1 < N ? nu : 0;
-    const int ldn = nun + nx;
-    /* Lx_{k+1} = Ln[nun:, nun:] */
-    if (g_classical) {
-      /* HPIPM classical: AL = [B'; A'] P_{k+1} with P_{k+1} = Lx Lx' formed, M = Ht + AL [B A] */
-      double P1[32 * 32], BA[64 * 32];
-      for (int j = 0; j < nx; ++j)
-        for (int i = 0; i < nx; ++i) {
-          double s = 0.0;
-          for (int l = 0; l < nx; ++l) s += M_(Ln, ldn, nun + i, nun + l) * M_(Ln, ldn, nun + j, nun + l);
-          M_(P1, nx, i, j) = s;
-        }
-      for (int j = 0; j < nx; ++j) { /* BA' = [B'; A'] (n x nx) */
-        for (int i = 0; i < nu; ++i) M_(BA, n, i, j) = M_(B, nx, j, i);
-        for (int i = 0; i < nx; ++i) M_(BA, n, nu + i, j) = M_(A, nx, j, i);
-      }
-      for (int j = 0; j < nx; ++j)
-        for (int i = 0; i < n; ++i) {
-          double s = 0.0;
-          for (int l = 0; l < nx; ++l) s += M_(BA, n, i, l) * M_(P1, nx, l, j);
-          M_(AL, n, i, j) = s;
-        }
-      const double* Ht = w->Ht + (size_t)k * w->hstride;
-      for (int j = 0; j < n; ++j)
-        for (int i = 0; i < n; ++i) {
-          double s = M_(Ht, n, i, j);
-          for (int l = 0; l < nx; ++l) s += M_(AL, n, i, l) * M_(BA, n, j, l);
-          M_(M, n, i, j) = s;
-        }
-      for (int i = 0; i < nu; ++i) M_(M, n, i, i) += reg;
-      chol(n, M);
-      memcpy(g_Lfull + (size_t)k * n * n, M, sizeof(double) * n * n);
-      continue;
-    }
+    const double* Ln = sq_L(w, d, k + 1);
+    const int nun = k + 1 < N ? nu : 0, ldn = nun + nx; /* Lx_{k+1} = Ln[nun:, nun:] */
     for (int j = 0; j < nx; ++j) {
       for (int i = 0; i < nu; ++i) {
         double s = 0.0;
@@ -408,51 +371,13 @@ static int sqrt_factor_hpipm(const dims_t* d, ric_ws_t* w, double reg) {
         M_(M, n, i, j) = s;
       }
     for (int i = 0; i < nu; ++i) M_(M, n, i, i) += reg;
-    if (getenv("ORACLE_SCHUR_TEXTBOOK")) {
-      /* Lx = chol(F + H'K), K = -G^-1 H (two triangular solves), averaged with its transpose */
-      double Lu[32 * 32], Kt[32 * 32], Pk[32 * 32];
-      for (int j = 0; j < nu; ++j) for (int i = 0; i < nu; ++i) M_(Lu, nu, i, j) = M_(M, n, i, j);
-      chol(nu, Lu);
-      for (int j = 0; j < nx; ++j) {
-        double col[32];
-        for (int i = 0; i < nu; ++i) col[i] = M_(M, n, i, nu + j);
-        chol_solve(nu, Lu, col);
-        for (int i = 0; i < nu; ++i) M_(Kt, nu, i, j) = -col[i];
-      }
-      for (int j = 0; j < nx; ++j)
-        for (int i = 0; i < nx; ++i) {
-          double s = M_(M, n, nu + i, nu + j);
-          for (int l = 0; l < nu; ++l) s += M_(M, n, l, nu + i) * M_(Kt, nu, l, j);
-          M_(Pk, nx, i, j) = s;
-        }
-      for (int j = 0; j < nx; ++j)
-        for (int i = j + 1; i < nx; ++i) {
-          double s = 0.5 * (M_(Pk, nx, i, j) + M_(Pk, nx, j, i));
-          M_(Pk, nx, i, j) = s; M_(Pk, nx, j, i) = s;
-        }
-      chol(nx, Pk);
-      chol(n, M); /* Lu, Lxu as the joint factor has them */
-      for (int j = 0; j < nx; ++j) for (int i = 0; i < nx; ++i) M_(M, n, nu + i, nu + j) = M_(Pk, nx, i, j);
-    } else {
-      chol(n, M);
-    }
-    if (getenv("ORACLE_REFACTOR")) { /* Lx := chol(Lx Lx') */
-      double Pk[32 * 32];
-      for (int j = 0; j < nx; ++j)
-        for (int i = 0; i < nx; ++i) {
-          double s = 0.0;
-          for (int l = 0; l < nx; ++l) s += M_(M, n, nu + i, nu + l) * M_(M, n, nu + j, nu + l);
-          M_(Pk, nx, i, j) = s;
-        }
-      chol(nx, Pk);
-      for (int j = 0; j < nx; ++j) for (int i = 0; i < nx; ++i) M_(M, n, nu + i, nu + j) = M_(Pk, nx, i, j);
-    }
-    memcpy(g_Lfull + (size_t)k * n * n, M, sizeof(double) * n * n);
+    chol(n, M);
+    memcpy(w->Lf + (size_t)k * n * n, M, sizeof(double) * n * n);
   }
-  /* P, K, Lg for the getters */
+  /* P = Lx Lx', Lg = Lu, K = -Lu^-T Lxu' for the getters (ocp_qp_ipm_solver.cpp:337-346) */
   for (int k = 0; k <= N; ++k) {
     const int nuk = k < N ? nu : 0, ld = nuk + nx;
-    const double* L = g_Lfull + (size_t)k * n * n;
+    const double* L = sq_L(w, d, k);
     double* P = w->P + (size_t)k * nx * nx;
     for (int j = 0; j < nx; ++j)
       for (int i = 0; i < nx; ++i) {
@@ -465,7 +390,7 @@ static int sqrt_factor_hpipm(const dims_t* d, ric_ws_t* w, double reg) {
     for (int j = 0; j < nu; ++j)
       for (int i = 0; i < nu; ++i) M_(Lg, nu, i, j) = M_(L, ld, i, j);
     double* K = w->K + (size_t)k * nu * nx;
-    for (int j = 0; j < nx; ++j) { /* K[:, j] = -Lu^-T Lxu[j, :]' */
+    for (int j = 0; j < nx; ++j) {
       double col[32];
       for (int i = 0; i < nu; ++i) col[i] = M_(L, ld, nu + j, i);
       for (int i = nu - 1; i >= 0; --i) {
@@ -479,8 +404,7 @@ static int sqrt_factor_hpipm(const dims_t* d, ric_ws_t* w, double reg) {
   }
   return 0;
 }
-static int g_sform; /* 1: the vectors travel as s = Lx^-1 p (fact_solve's last factor row) */
-/* x := Lx^-1 x (stage factor L, x part), zero pivots give zero */
+/* x := Lx^-1 x (the x block of a stage factor, ld ld, offset off); zero pivots give zero */
 static void lx_solve(const double* L, int ld, int off, int nx, double* x) {
   for (int i = 0; i < nx; ++i) {
     double s = x[i];
@@ -489,113 +413,86 @@ static void lx_solve(const double* L, int ld, int off, int nx, double* x) {
     x[i] = dd > 0.0 ? s / dd : 0.0;
   }
 }
-static void sqrt_vectors_hpipm_s(const dims_t* d, ric_ws_t* w) {
+static void sqrt_vectors(const dims_t* d, ric_ws_t* w) {
   const int nx = d->nx, nu = d->nu, n = nx + nu, N = d->N;
   double* pN = w->p + (size_t)N * nx;
   memcpy(pN, w->gt + (size_t)N * w->gstride, sizeof(double) * nx);
-  lx_solve(g_Lfull + (size_t)N * n * n, nx, 0, nx, pN);
+  if (w->sform) lx_solve(sq_L(w, d, N), nx, 0, nx, pN);
   for (int k = N - 1; k >= 0; --k) {
-    const double* Ln = g_Lfull + (size_t)(k + 1) * n * n;
-    const int nun = k + 1 < N ? nu : 0, ldn = nun + nx;
-    const double* bt = w->bt + (size_t)k * nx;
-    double m[32];
-    for (int j = 0; j < nx; ++j) { /* m = Lx' b + s */
-      double sacc = 0.0;
-      for (int l = j; l < nx; ++l) sacc += M_(Ln, ldn, nun + l, nun + j) * bt[l];
-      m[j] = sacc + w->p[(size_t)(k + 1) * nx + j];
-    }
     const double* A = qA(d, k);
     const double* B = qB(d, k);
-    const double* gt = w->gt + (size_t)k * w->gstride;
-    double l_[64];
-    for (int i = 0; i < n; ++i) { /* l = g + AL m, AL = [B'; A'] Lx */
-      double acc = gt[i];
-      for (int j = 0; j < nx; ++j) {
-        double al = 0.0;
-        for (int q = j; q < nx; ++q)
-          al += (i < nu ? M_(B, nx, q, i) : M_(A, nx, q, i - nu)) * M_(Ln, ldn, nun + q, nun + j);
-        acc += al * m[j];
-      }
-      l_[i] = acc;
-    }
-    const double* L = g_Lfull + (size_t)k * n * n;
-    double* y = g_yv + (size_t)k * nu;
-    for (int i = 0; i < nu; ++i) {
-      double sacc = l_[i];
-      for (int q = 0; q < i; ++q) sacc -= M_(L, n, i, q) * y[q];
-      const double dd = M_(L, n, i, i);
-      y[i] = dd > 0.0 ? sacc / dd : 0.0;
-    }
-    double* sk = w->p + (size_t)k * nx;
-    for (int i = 0; i < nx; ++i) {
-      double sacc = l_[nu + i];
-      for (int q = 0; q < nu; ++q) sacc -= M_(L, n, nu + i, q) * y[q];
-      sk[i] = sacc;
-    }
-    lx_solve(L, n, nu, nx, sk);
-  }
-}
-static void sqrt_vectors_hpipm(const dims_t* d, ric_ws_t* w) {
-  const int nx = d->nx, nu = d->nu, n = nx + nu, N = d->N;
-  if (g_sform) { sqrt_vectors_hpipm_s(d, w); return; }
-  memcpy(w->p + (size_t)N * nx, w->gt + (size_t)N * w->gstride, sizeof(double) * nx);
-  for (int k = N - 1; k >= 0; --k) {
-    const double* Ln = g_Lfull + (size_t)(k + 1) * n * n;
+    const double* Ln = sq_L(w, d, k + 1);
     const int nun = k + 1 < N ? nu : 0, ldn = nun + nx;
     const double* bt = w->bt + (size_t)k * nx;
-    double t[32], tmp[32];
+    const double* pn = w->p + (size_t)(k + 1) * nx;
+    const double* gt = w->gt + (size_t)k * w->gstride;
+    double t[32], l_[64];
     for (int j = 0; j < nx; ++j) { /* Lx' b */
       double s = 0.0;
       for (int l = j; l < nx; ++l) s += M_(Ln, ldn, nun + l, nun + j) * bt[l];
       t[j] = s;
     }
-    for (int i = 0; i < nx; ++i) { /* Lx (Lx' b) + p */
-      double s = 0.0;
-      for (int l = 0; l <= i; ++l) s += M_(Ln, ldn, nun + i, nun + l) * t[l];
-      tmp[i] = s + w->p[(size_t)(k + 1) * nx + i];
+    if (w->sform) {
+      /* l = g + AL m, m = Lx' b + s, AL = [B'; A'] Lx */
+      for (int j = 0; j < nx; ++j) t[j] += pn[j];
+      for (int i = 0; i < n; ++i) {
+        double acc = gt[i];
+        for (int j = 0; j < nx; ++j) {
+          double al = 0.0;
+          for (int q = j; q < nx; ++q)
+            al += (i < nu ? M_(B, nx, q, i) : M_(A, nx, q, i - nu)) * M_(Ln, ldn, nun + q, nun + j);
+          acc += al * t[j];
+        }
+        l_[i] = acc;
+      }
+    } else {
+      /* l = g + [B'; A'] (Lx (Lx' b) + p) */
+      double tmp[32];
+      for (int i = 0; i < nx; ++i) {
+        double s = 0.0;
+        for (int l = 0; l <= i; ++l) s += M_(Ln, ldn, nun + i, nun + l) * t[l];
+        tmp[i] = s + pn[i];
+      }
+      mtv(nx, nu, B, tmp, l_);
+      mtv(nx, nx, A, tmp, l_ + nu);
+      for (int i = 0; i < n; ++i) l_[i] += gt[i];
     }
-    const double* gt = w->gt + (size_t)k * w->gstride;
-    double lu[32], lx[32];
-    mtv(nx, nu, qB(d, k), tmp, lu);
-    mtv(nx, nx, qA(d, k), tmp, lx);
-    for (int i = 0; i < nu; ++i) lu[i] += gt[i];
-    for (int i = 0; i < nx; ++i) lx[i] += gt[nu + i];
-    const double* L = g_Lfull + (size_t)k * n * n;
-    double* y = g_yv + (size_t)k * nu;
+    const double* L = sq_L(w, d, k);
+    double* y = w->yv + (size_t)k * nu;
     for (int i = 0; i < nu; ++i) {
-      double s = lu[i];
-      for (int l = 0; l < i; ++l) s -= M_(L, n, i, l) * y[l];
+      double s = l_[i];
+      for (int q = 0; q < i; ++q) s -= M_(L, n, i, q) * y[q];
       const double dd = M_(L, n, i, i);
       y[i] = dd > 0.0 ? s / dd : 0.0;
     }
+    double* pk = w->p + (size_t)k * nx;
     for (int i = 0; i < nx; ++i) {
-      double s = lx[i];
-      for (int l = 0; l < nu; ++l) s -= M_(L, n, nu + i, l) * y[l];
-      w->p[(size_t)k * nx + i] = s;
+      double s = l_[nu + i];
+      for (int q = 0; q < nu; ++q) s -= M_(L, n, nu + i, q) * y[q];
+      pk[i] = s;
     }
+    if (w->sform) lx_solve(L, n, nu, nx, pk);
   }
 }
-static void sqrt_forward_hpipm(const dims_t* d, const ric_ws_t* w, const double* xinit, double* x,
-                               double* u, double* pi) {
+static void sqrt_forward(const dims_t* d, const ric_ws_t* w, const double* xinit, double* x,
+                         double* u, double* pi) {
   const int nx = d->nx, nu = d->nu, n = nx + nu, N = d->N;
   memcpy(x, xinit, sizeof(double) * nx);
   for (int k = 0; k < N; ++k) {
-    const double* L = g_Lfull + (size_t)k * n * n;
+    const double* L = sq_L(w, d, k);
     const double* xk = x + (size_t)k * nx;
     double* uk = u + (size_t)k * nu;
-    double v[32];
-    for (int i = 0; i < nu; ++i) { /* y + Lxu' x */
-      double s = g_yv[(size_t)k * nu + i];
+    for (int i = 0; i < nu; ++i) { /* -(y + Lxu' x) */
+      double s = w->yv[(size_t)k * nu + i];
       for (int l = 0; l < nx; ++l) s += M_(L, n, nu + l, i) * xk[l];
-      v[i] = -s;
+      uk[i] = -s;
     }
-    for (int i = nu - 1; i >= 0; --i) {
-      double s = v[i];
-      for (int l = i + 1; l < nu; ++l) s -= M_(L, n, l, i) * v[l];
+    for (int i = nu - 1; i >= 0; --i) { /* Lu^-T */
+      double s = uk[i];
+      for (int l = i + 1; l < nu; ++l) s -= M_(L, n, l, i) * uk[l];
       const double dd = M_(L, n, i, i);
-      v[i] = dd > 0.0 ? s / dd : 0.0;
+      uk[i] = dd > 0.0 ? s / dd : 0.0;
     }
-    memcpy(uk, v, sizeof(double) * nu);
     double t1[32], t2[32];
     mv(nx, nx, qA(d, k), xk, t1);
     mv(nx, nu, qB(d, k), uk, t2);
@@ -603,20 +500,20 @@ static void sqrt_forward_hpipm(const dims_t* d, const ric_ws_t* w, const double*
     for (int i = 0; i < nx; ++i) x1[i] = t1[i] + t2[i] + w->bt[(size_t)k * nx + i];
   }
   for (int k = 1; k <= N; ++k) {
-    const double* L = g_Lfull + (size_t)k * n * n;
+    const double* L = sq_L(w, d, k);
     const int nuk = k < N ? nu : 0, ld = nuk + nx;
     const double* xk = x + (size_t)k * nx;
+    const double* pk = w->p + (size_t)k * nx;
     double t[32];
-    for (int j = 0; j < nx; ++j) {
+    for (int j = 0; j < nx; ++j) { /* Lx' x (+ s) */
       double s = 0.0;
       for (int l = j; l < nx; ++l) s += M_(L, ld, nuk + l, nuk + j) * xk[l];
-      t[j] = s;
+      t[j] = s + (w->sform ? pk[j] : 0.0);
     }
-    if (g_sform) for (int j = 0; j < nx; ++j) t[j] += w->p[(size_t)k * nx + j];
     for (int i = 0; i < nx; ++i) {
       double s = 0.0;
       for (int l = 0; l <= i; ++l) s += M_(L, ld, nuk + i, nuk + l) * t[l];
-      pi[(size_t)k * nx + i] = s + (g_sform ? 0.0 : w->p[(size_t)k * nx + i]);
+      pi[(size_t)k * nx + i] = s + (w->sform ? 0.0 : pk[i]);
     }
   }
 }
@@ -667,6 +564,7 @@ static int riccati_factor_lq(const dims_t* d, ric_ws_t* w, const stage_rows_t* s
   double* M = (double*)malloc(sizeof(double) * 64 * 512);
   double Lx[32 * 32], Hd[64 * 64], gdum[64], vrow[64];
   if (!M) return -1;
+  w->sq = 1;
   for (int k = N; k >= 0; --k) {
     const int nu_k = st[k].nu_k, ns = nu_k + nx;
     int m = 0;
@@ -702,6 +600,11 @@ static int riccati_factor_lq(const dims_t* d, ric_ws_t* w, const stage_rows_t* s
       }
     }
     lq_pd(ns, m, M);
+    /* the stage factor for the square-root vector and forward routines (HPIPM's lq path
+     * solves with L exactly as the Cholesky square root does) */
+    double* Lk = w->Lf + (size_t)k * (size_t)d->n * d->n;
+    for (int j = 0; j < ns; ++j)
+      for (int i = 0; i < ns; ++i) M_(Lk, ns, i, j) = i >= j ? M_(M, ns, i, j) : 0.0;
     double* P = w->P + (size_t)k * nx * nx;
     for (int j = 0; j < nx; ++j)
       for (int i = 0; i < nx; ++i) M_(Lx, nx, i, j) = i >= j ? M_(M, ns, nu_k + i, nu_k + j) : 0.0;
@@ -998,6 +901,19 @@ static void compute_residuals(const dims_t* d, stage_rows_t* st, const double* x
   if (obj) *obj = ob;
 }
 
+/* the factorization / vector / forward routines of the Riccati variant (ric_alg) */
+static int factor(const dims_t* d, ric_ws_t* w, double reg, int ric_alg) {
+  return ric_alg ? sqrt_factor(d, w, reg) : riccati_factor(d, w, reg);
+}
+static void vectors(const dims_t* d, ric_ws_t* w, int sform) {
+  w->sform = sform;
+  if (w->sq) sqrt_vectors(d, w); else riccati_vectors(d, w);
+}
+static void forward(const dims_t* d, const ric_ws_t* w, const double* xinit, double* x, double* u,
+                    double* pi) {
+  if (w->sq) sqrt_forward(d, w, xinit, x, u, pi); else riccati_forward(d, w, xinit, x, u, pi);
+}
+
 /* ------------------------------------------------------------------ */
 /* main entry                                                          */
 /* ------------------------------------------------------------------ */
@@ -1020,6 +936,10 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
   w.K = (double*)calloc((size_t)N * nu * nx, sizeof(double));
   w.kk = (double*)calloc((size_t)N * nu, sizeof(double));
   w.Lg = (double*)calloc((size_t)N * nu * nu, sizeof(double));
+  w.Lf = (double*)calloc((size_t)(N + 1) * n * n, sizeof(double));
+  w.yv = (double*)calloc((size_t)N * nu + 1, sizeof(double));
+  w.sq = 0;
+  w.sform = 0;
   double* rg = (double*)calloc((size_t)(N + 1) * w.gstride, sizeof(double));
   double* rb = (double*)calloc((size_t)N * nx, sizeof(double));
   double* dx = (double*)calloc((size_t)(N + 1) * nx, sizeof(double));
@@ -1041,9 +961,10 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
      * (pinned by test/ocp_qp_ipm_solver.cpp:55-56)                   */
     for (int s = 0; s <= N; ++s) fill_stage_H(&d, s, w.Ht + s * w.hstride, w.gt + s * w.gstride);
     memcpy(w.bt, qp->b, sizeof(double) * N * nx);
-    if (riccati_factor(&d, &w, set->reg_prim, set->ric_alg)) { res->status = 3; rc = 0; goto done_nan; }
-    riccati_vectors(&d, &w);
-    riccati_forward(&d, &w, x0, x, u, pi);
+    /* (d_ocp_qp_fact_solve_kkt_unconstr: the square root carries s = Lx^-1 p) */
+    if (factor(&d, &w, set->reg_prim, set->ric_alg)) { res->status = 3; rc = 0; goto done_nan; }
+    vectors(&d, &w, 1);
+    forward(&d, &w, x0, x, u, pi);
     compute_residuals(&d, st, x, u, pi, rg, rb, res->res, &res->obj, w.gstride);
     write_outputs(&d, &w, x, u, pi, P, p, K, k);
     res->iter = 0;
@@ -1093,15 +1014,6 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
 
   double alpha_prim = 1.0, alpha_dual = 1.0;
   int iter = 0;
-  const int hp = !set->lq_fact && getenv("ORACLE_SQRT_HPIPM") && getenv("ORACLE_SQRT_HPIPM")[0] == '1';
-  g_classical = !set->ric_alg;
-  if (hp) {
-    g_Lfull = (double*)calloc((size_t)(N + 1) * n * n, sizeof(double));
-    g_yv = (double*)calloc((size_t)N * nu + 1, sizeof(double));
-  }
-  const int hps = hp && !getenv("ORACLE_SQRT_CLASSIC");
-#define VECTORS() do { if (hps) sqrt_vectors_hpipm(&d, &w); else riccati_vectors(&d, &w); } while (0)
-#define FORWARD(X, U, PI) do { if (hps) sqrt_forward_hpipm(&d, &w, zero, X, U, PI); else riccati_forward(&d, &w, zero, X, U, PI); } while (0)
   int force_lq = set->lq_fact == 2;  /* lq_fact 1 switches for the rest of the solve */
   for (;;) {
     compute_residuals(&d, st, x, u, pi, rg, rb, res->res, &res->obj, w.gstride);
@@ -1141,12 +1053,10 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
       if (s < N) memcpy(w.bt + (size_t)s * nx, rb + (size_t)s * nx, sizeof(double) * nx);
     }
     if (force_lq ? riccati_factor_lq(&d, &w, st, set->reg_prim)
-                 : (hp ? sqrt_factor_hpipm(&d, &w, set->reg_prim)
-                       : riccati_factor(&d, &w, set->reg_prim, set->ric_alg))) { res->status = 3; break; }
-    g_sform = hp && getenv("ORACLE_SQRT_SFORM") != NULL;
-    VECTORS();
-    FORWARD(dx, du, dpi);
-    g_sform = 0;
+                 : factor(&d, &w, set->reg_prim, set->ric_alg)) { res->status = 3; break; }
+    /* predictor: d_ocp_qp_fact_solve_kkt_step (square root: s-form) */
+    vectors(&d, &w, 1);
+    forward(&d, &w, zero, dx, du, dpi);
 #ifdef ORACLE_DEBUG
     {
       double tmin = 1e300, lmax = 0;
@@ -1190,8 +1100,8 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
       if (!(ng <= 1e-5) || !(nb <= 1e-5)) {
         force_lq = 1;
         if (riccati_factor_lq(&d, &w, st, set->reg_prim)) { res->status = 3; break; }
-        riccati_vectors(&d, &w);
-        riccati_forward(&d, &w, zero, dx, du, dpi);
+        vectors(&d, &w, 1);
+        forward(&d, &w, zero, dx, du, dpi);
         STEP_TLAM();
       }
     }
@@ -1244,14 +1154,10 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
           row_axpy(&d, rw, nu_k, gam, gt, gt + nu_k);
         }
       }
-      VECTORS();
-      FORWARD(dx, du, dpi);
+      /* corrector: d_ocp_qp_solve_kkt_step, same factors (square root: p-form) */
+      vectors(&d, &w, 0);
+      forward(&d, &w, zero, dx, du, dpi);
       STEP_TLAM();
-    }
-    if (getenv("ORACLE_LINRES_DIAG")) {
-      double ng = 0.0, nb = 0.0;
-      lin_res(&d, st, &w, rg, rb, du, dx, dpi, itg, itb, &ng, &nb);
-      fprintf(stderr, "LINRES %d %.3e %.3e %.3e\n", iter, mu, ng, res->res[0]);
     }
     /* iterative refinement of the final step (HPIPM itref_corr_max: Balance 2, Robust 4;
      * restated from HPIPM's d_ocp_qp_ipm_solve / d_ocp_qp_res_compute_lin, not vendored):
@@ -1271,8 +1177,8 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
         /* correction: same factors, right-hand side = the residual */
         double* gkeep = w.gt; double* bkeep = w.bt;
         w.gt = itg; w.bt = itb;
-        VECTORS();
-        FORWARD(cdx, cdu, cdpi);
+        vectors(&d, &w, 0);
+        forward(&d, &w, zero, cdx, cdu, cdpi);
         w.gt = gkeep; w.bt = bkeep;
         for (size_t i = 0; i < (size_t)(N + 1) * nx; ++i) { dx[i] += cdx[i]; if (i >= (size_t)nx) dpi[i] += cdpi[i]; }
         for (size_t i = 0; i < (size_t)N * nu; ++i) du[i] += cdu[i];
@@ -1338,9 +1244,6 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
     ++iter;
   }
   res->iter = iter;
-#undef VECTORS
-#undef FORWARD
-  if (hp) { free(g_Lfull); free(g_yv); g_Lfull = NULL; g_yv = NULL; }
 
   /* Riccati outputs (P, K) are those of the last factorization performed by
    * the IPM (the last step's barrier-augmented KKT system), as HPIPM's
@@ -1368,7 +1271,7 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
           rw->G = (rw->has_l ? rw->lam_l / rw->t_l : 0.0) + (rw->has_u ? rw->lam_u / rw->t_u : 0.0);
         }
       if (riccati_factor_lq(&d, &w, st, set->reg_prim) != 0) res->status = 3;
-    } else if (riccati_factor(&d, &w, set->reg_prim, set->ric_alg) != 0) {
+    } else if (factor(&d, &w, set->reg_prim, set->ric_alg) != 0) {
       res->status = 3;
     }
   }
@@ -1380,6 +1283,7 @@ done_nan:
 done:
   free_rows(&d, st);
   free(w.Ht); free(w.gt); free(w.bt); free(w.P); free(w.p); free(w.K); free(w.kk); free(w.Lg);
+  free(w.Lf); free(w.yv);
   free(rg); free(rb); free(dx); free(du); free(dpi); free(zero);
   free(itg); free(itb); free(cdx); free(cdu); free(cdpi);
   return rc;

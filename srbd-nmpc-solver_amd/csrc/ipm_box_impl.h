@@ -8,40 +8,6 @@ namespace SRBD_NS {
 
 using real = SRBD_REAL;
 
-#ifndef SRBD_ITREF_CHECK_ONLY
-#define SRBD_ITREF_CHECK_ONLY 0
-#endif
-// diagnostic builds: ric_alg 1's fp64 RB with P_k in the symmetrized textbook form of riccati.h
-// SYMP before its factor is taken (as the oracle's square-root variant forms it) instead of
-// F - Y'Y.  On the degenerate endgame family in Speed it converges on 53 instead of 48 of 64,
-// but a copy it stops at min step lands ~2e-3 from the oracle's solution (F - Y'Y: 3.3e-5), so
-// it is not the default
-#ifndef SRBD_SQRT_SYMP
-#define SRBD_SQRT_SYMP 0
-#endif
-// ric_alg 1: the stage records keep P itself (the sweeps apply it as ric_alg 0's do) instead of
-// its factor Lp (applied as Lp (Lp' x)); the factorization still carries Lp from stage to stage
-#ifndef SRBD_SQRT_EXPLICIT_P
-#define SRBD_SQRT_EXPLICIT_P 0
-#endif
-// diagnostic builds: ric_alg 1 carries P_k as the oracle's riccati_factor does -- Lp = chol(P_k),
-// then P_k := Lp Lp' (explicit, for the record with SRBD_SQRT_EXPLICIT_P) and the next stage's
-// factor is chol(Lp Lp') -- instead of Lp itself (equal in exact arithmetic).  On the
-// degenerate endgame family in Speed: 51 / 48 / 46 of 64 (alone / with SRBD_SQRT_SYMP / with
-// both and SRBD_SQRT_EXPLICIT_P), against the product's 48, and further from the oracle
-// (profiles/round4/endgame_counts_ric1_recon.log)
-#ifndef SRBD_SQRT_RECON
-#define SRBD_SQRT_RECON 0
-#endif
-// fp64 box RB (12 x 12 blocks): Q_k reaches the group's LDS by LDS-DMA issued before the
-// Cholesky of G instead of by register loads after it (one memory round trip less on the
-// stage's chain, no VGPRs held across the Cholesky).  Measured slower (box-u 78.90 vs 78.05 ms
-// same box, profiles/round4/ab_qdma_box_u.log: the exec / M0 set-up of four groups' pieces
-// and 12 more bytes of spills outweigh the round trip), so off by default
-#ifndef SRBD_Q_DMA
-#define SRBD_Q_DMA 0
-#endif
-
 constexpr real kThr0 = real(0.1);     // minimum initial slack (HPIPM init_var)
 
 // phase kernels (one launch each, per IPM iteration; see launch_ipm_box)
@@ -362,47 +328,6 @@ __device__ __forceinline__ void lds_put_col(real* blk, int lane, const real (&v)
 __device__ __forceinline__ void lds_get_col(const real* blk, int c, real (&v)[12]) {
   load12(blk + c * 12, v);
 }
-// One 12 x 12 fp64 block (1152 contiguous, 16-byte aligned bytes of each group's QP) into
-// the group's LDS block by LDS-DMA (global_load_lds_dwordx4): no VGPR destination, retired by
-// the memory counter.  An LDS-DMA writes at a wave-uniform base (M0) + 16 B x (lane in the
-// wave), so each of the wave's four groups issues its own five 256-byte pieces under an exec
-// mask of its 16 lanes, M0 offset by the group's position in the wave.  One asm statement for
-// the whole wave: with the intrinsic under per-group branches the compiler merged the arms'
-// last pieces into one block and took M0 from the first active lane for all four groups.
-// The fifth piece is whole (bytes 1152..1279 of the source are the next stage's block, and
-// land in the group's dead B block).  The caller waits (vmcnt(0)) before reading the block;
-// the compiler does not see these loads.  `blk0`: the LDS byte address of the wave's first
-// group block (wave-uniform); `stride`: the group blocks' byte stride.
-template <unsigned kStride>
-__device__ __forceinline__ void dma_block144(const real* src, unsigned blk0, int lane) {
-  const real* g = src + 2 * lane;
-  unsigned km;
-  unsigned long long ke;
-  asm volatile(
-      "s_mov_b32 %[km], m0\n\t"
-      "s_mov_b64 %[ke], exec\n\t"
-#define SRBD_DMA_GROUP(G, MASK)                                  \
-      "s_and_b64 exec, %[ke], " MASK "\n\t"                    \
-      "s_add_u32 m0, %[b], %[o" #G "]\n\t"                     \
-      "s_nop 1\n\t"                                            \
-      "global_load_lds_dwordx4 %[g], off\n\t"                  \
-      "global_load_lds_dwordx4 %[g], off offset:256\n\t"       \
-      "global_load_lds_dwordx4 %[g], off offset:512\n\t"       \
-      "global_load_lds_dwordx4 %[g], off offset:768\n\t"       \
-      "global_load_lds_dwordx4 %[g], off offset:1024\n\t"
-      SRBD_DMA_GROUP(0, "%[m0]")
-      SRBD_DMA_GROUP(1, "%[m1]")
-      SRBD_DMA_GROUP(2, "%[m2]")
-      SRBD_DMA_GROUP(3, "%[m3]")
-#undef SRBD_DMA_GROUP
-      "s_mov_b64 exec, %[ke]\n\t"
-      "s_mov_b32 m0, %[km]"
-      : [km] "=&s"(km), [ke] "=&s"(ke)
-      : [g] "v"(g), [b] "s"(blk0), [o0] "i"(0), [o1] "i"(kStride - 256), [o2] "i"(2 * (kStride - 256)),
-        [o3] "i"(3 * (kStride - 256)), [m0] "s"(0xffffull), [m1] "s"(0xffffull << 16),
-        [m2] "s"(0xffffull << 32), [m3] "s"(0xffffull << 48)
-      : "memory", "scc");
-}
 __device__ __forceinline__ void lds_get_row(const real* blk, int r, real (&v)[12]) {
   sfor<0, 12>([&](auto j) {
     constexpr int J = decltype(j)::value;
@@ -574,7 +499,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   // (P x)_col + acc for an element-owned x (lane j holds x_j), P from a stage record's kRecP
   // slot: packed P (ric_alg 0) or its factor Lp (ric_alg 1)
   // the record's kRecP slot holds the factor Lp (ric_alg 1) or P
-  constexpr bool kRecFactor = SQRT && !SRBD_SQRT_EXPLICIT_P;
+  constexpr bool kRecFactor = SQRT;
   auto rec_P_mul = [&](const real* rec, real xv, real acc) -> real {
     if constexpr (kRecFactor) {
       real Lv[12];
@@ -1264,10 +1189,6 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         // at their register limit, when the factorization asks for it (cone +0.7% otherwise)
         constexpr bool kEarlyR = GEN == 0;
         if constexpr (kEarlyR) c.col(c.R() + (size_t)k * c.nuu(), nu, col, uel, Rh);
-        // Q_k by LDS-DMA into the A block (free once the residual products have read it),
-        // issued at the end of loadR: R's registers are consumed by then, so no ordinary load
-        // result is waited for while the DMA is in flight (such a wait drains it)
-        constexpr bool kQDma = SRBD_Q_DMA && FULL && GEN == 0 && sizeof(real) == 8;
         const real bk = c.el(c.b() + (size_t)k * nx, nx, li);
         rgx = dot_bcast(A_, pin, rgx);  // + A'pi_{k+1}
         rgu = dot_bcast(B_, pin, rgu);  // + B'pi_{k+1}
@@ -1314,24 +1235,10 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             if (lane == I) Rc[I] += (I < nu) ? greal(Gu) : greal(1.0);  // padded inputs: R = 1
             if (c.isv) Rc[I] = greal(0.0);
           });
-          if constexpr (kQDma) {
-            // the wave's first group block (the same on every lane of the wave)
-            const real* b0 = ldsA - ((threadIdx.x / kGroup) & 3) * kGroupLds<GEN>;
-            const unsigned blk0 = __builtin_amdgcn_readfirstlane(
-                (unsigned)(size_t)(const __attribute__((address_space(3))) real*)b0);
-            dma_block144<kGroupLds<GEN> * sizeof(real)>(c.Q() + (size_t)k * 144, blk0, lane);
-          }
         };
         auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
           lds_get_col(ldsS, col, Sc);
-          if constexpr (kQDma) {
-            // the compiler does not order this LDS read after the DMA's write: wait by hand
-            // (the DMA is the wave's last memory instruction, so nothing else is waited for)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_get_col(ldsA, col, Qc);
-          } else {
-            c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
-          }
+          c.col(c.Q() + (size_t)k * c.nxx(), nx, col, xel, Qc);
           const real qx = dot_bcast(Qc, xk, real(0.0));
           if (k > 0) objl += xk * (real(0.5) * qx + qk);
           const real qt = finish_x(rgx + qx);
@@ -1349,8 +1256,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         tstamp(22);
         StageFactor<real> f;
         if constexpr (SQRT) {
-          riccati_step_sqrt<1, SRBD_SQRT_SYMP != 0 && sizeof(real) == 8, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f, NoMid{},
-                                                           ldsB + lane * 12);
+          // (HPIPM's square-root form: P_k = F - Y'Y as the trailing block of the joint factor)
+          riccati_step_sqrt<1, false, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f);
         } else {
           // P_k = F + K'H, symmetrized (riccati.h SYMP); H waits in the group's B block (dead
           // since the residual products; the record image overwrites it only afterwards)
@@ -1377,26 +1284,6 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         });
         if constexpr (SQRT) {
           sqrt_factor(P, lane);
-          if constexpr (SRBD_SQRT_RECON != 0) {
-            // P_k := Lp Lp' (rows of Lp through a free LDS slot: behind the record image in the
-            // box kernels, the dead A block in the general-row ones), p_k kept; Lp := chol(P_k)
-            static_assert(kRecSize + 78 <= kGroupLds<GEN>, "scratch slot");
-            real* const scr = ldsA + (kRecImg<GEN> ? kRecSize : 0);
-            lds_wave_fence();
-            if (lane < kMaxDim) store_packed_col(scr, lane, P);
-            lds_wave_fence();
-            real Lr[12];
-            load_packed_lrow_d(scr, col, Lr);
-            sfor<0, 12>([&](auto i) { P[decltype(i)::value] = real(0.0); });
-            tmul_acc(Lr, Lr, P);
-            sfor<0, 12>([&](auto i) {
-              constexpr int I = decltype(i)::value;
-              if (lane >= kMaxDim) P[I] = f.F[I];  // p_k on VL; the pad lanes as before
-            });
-            if constexpr (!kRecFactor)
-              if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
-            sqrt_factor(P, lane);
-          }
           if constexpr (kRecFactor)
             if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
         }
@@ -1585,11 +1472,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
       const real nga = gmax(ng), nba = gmax(nb);
       const int cnt = (int)qs[kQsItCnt];
       const real n0g = cnt == 0 ? nga : qs[kQsItN0g], n0b = cnt == 0 ? nba : qs[kQsItN0b];
-      // (diagnostic builds, -DSRBD_ITREF_CHECK_ONLY=1: the check records the unrefined step's
-      // linear residual in the stat table and never corrects -- Speed's iterates)
-      const bool small = SRBD_ITREF_CHECK_ONLY ||
-                         ((nga < a.tol_stat || nga < real(1e-3) * n0g) &&
-                          (nba < a.tol_eq || nba < real(1e-3) * n0b));
+      const bool small = (nga < a.tol_stat || nga < real(1e-3) * n0g) &&
+                         (nba < a.tol_eq || nba < real(1e-3) * n0b);
       if (lane == 0) {
         if (cnt == 0) {
           qs[kQsItN0g] = nga;
@@ -2132,8 +2016,7 @@ __global__ void __launch_bounds__(256) compact_running_kernel(const real* __rest
   if (run) buf[base + __popcll(m & ((1ull << lane) - 1))] = q;
 }
 
-// diagnostic builds (-DSRBD_IPM_SPLIT=1, profiling only): every sweep its own launch
-// (SRBD_ITREF_CHECK_ONLY: see kPhIS)
+// diagnostic builds (-DSRBD_IPM_SPLIT=1, scripts/profile_ipm.sh): every sweep its own launch
 #ifndef SRBD_IPM_SPLIT
 #define SRBD_IPM_SPLIT 0
 #endif

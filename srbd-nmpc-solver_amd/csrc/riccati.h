@@ -84,30 +84,16 @@ __device__ __forceinline__ void tmul_acc(const T (&X)[12], const T (&Y)[12], T (
   });
 }
 
-// How a triangular solve applies a diagonal entry of L: by default `rs` holds 1 / L_ll and
-// the solves multiply by it; -DSRBD_TRSV_DIV=1 (diagnostic builds) keeps L_ll itself and
-// divides, as the oracle's chol_solve does (0 stays 0 for a zeroed pivot).
-#ifndef SRBD_TRSV_DIV
-#define SRBD_TRSV_DIV 0
-#endif
+// A triangular solve applies a diagonal entry of L as rs = 1 / L_ll (0 for a zeroed pivot).
 template <typename T>
 __device__ __forceinline__ T apply_rs(T x, T rs) {
-  if constexpr (SRBD_TRSV_DIV) {
-    return rs != T(0) ? x / rs : T(0);
-  } else {
-    return x * rs;
-  }
+  return x * rs;
 }
 // rs of a pivot d (> 0, else the zeroed direction) and 1 / L_ll for scaling L's column
 template <typename T>
 __device__ __forceinline__ void pivot_rs(T d, T& rs, T& inv_l) {
-  if constexpr (SRBD_TRSV_DIV) {
-    rs = d > T(0) ? __builtin_sqrt(d) : T(0);
-    inv_l = rs > T(0) ? T(1) / rs : T(0);
-  } else {
-    rs = d > T(0) ? T(1) / __builtin_sqrt(d) : T(0);
-    inv_l = rs;
-  }
+  rs = d > T(0) ? T(1) / __builtin_sqrt(d) : T(0);
+  inv_l = rs;
 }
 
 // Right-looking Cholesky of the column-owned symmetric G (lane l holds

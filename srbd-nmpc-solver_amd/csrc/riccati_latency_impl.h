@@ -61,29 +61,14 @@ size_t lat_lds_bytes(int N) { return (size_t)(lat_scr_off(N) + lat_scr_size(N)) 
 // (3 dependent FMAs instead of the IEEE division's ~10 instructions on the stage's critical
 // path); otherwise chol_cols (riccati.h): `reg` on each pivot, a non-positive pivot zeroes
 // its column (BLASFEO dpotrf_l).
-// (one Newton step, -DSRBD_LAT_NEWTON=1: the riccati GPU tests pass and the call pattern moves
-// 99.0 / 99.8 vs 100.2 / 99.9 us on one box, within its noise -- kept at two;
-// profiles/round4/newton_call_pattern.log)
-// the QP's stages reach the LDS image during the backward sweep, one stage ahead, by waves 2..7
-// (1), or all before it (0).  Streaming measured 103.6 / 104.0 vs 102.3 / 103.1 us per call on
-// one box (profiles/round4/stream_call_pattern.log): each stage's mapped-host read waits a
-// PCIe round trip, longer than the stage it hides behind, and __syncthreads drains any deeper
-// lookahead.  A two-stage lookahead (inline-asm LDS-DMA, raw barriers in the sweep) measured
-// 113.6-124.0 vs 101.4-106.2 us (profiles/round4/stream_call_pattern.log).  Off.
-#ifndef SRBD_LAT_STREAM
-#define SRBD_LAT_STREAM 0
-#endif
-#ifndef SRBD_LAT_NEWTON
-#define SRBD_LAT_NEWTON 2
-#endif
+// (one Newton step measured within the call pattern's noise, 99.0 / 99.8 vs 100.2 / 99.9 us;
+// streaming the stages into LDS during the sweep measured slower: DESIGN.md 9.1)
 __device__ __forceinline__ double lat_recip(double d) {
   double r = __builtin_amdgcn_rcp(d);
   double e = __builtin_fma(-d, r, 1.0);
   r = __builtin_fma(r, e, r);
-  if constexpr (SRBD_LAT_NEWTON >= 2) {
-    e = __builtin_fma(-d, r, 1.0);
-    r = __builtin_fma(r, e, r);
-  }
+  e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
   return r;
 }
 // `hook(ic<K>)` runs at the top of pivot K: the caller issues its independent matrix-core
@@ -133,16 +118,7 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
   const int cc = cv ? c : 11;       // clamped column for addressing
   auto rec = [&](int k) { return a.ws + ((size_t)k * a.batch + qp) * kWsStage; };
   tstamp(16);
-#if SRBD_LAT_STREAM
-  // stages N - 1 and N by every thread; the rest streamed one stage ahead of the backward sweep
-  // by waves 2..7 (idle there), so the mapped-host read overlaps the stage chain
-  lds_copy_range(a, img, qp, (N > 0 ? N - 1 : 0) * kImgStage, (N + 1) * kImgStage, threadIdx.x,
-                 kLatThreads);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-#else
   lds_copy_qp(a, img, qp);
-#endif
 
   // ---------------- backward sweep ----------------
   lat_d4 Pt;  // [P | p]_k+1 (wave 0)
@@ -194,12 +170,6 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
   };
 #pragma unroll 1
   for (int k = N - 1; k >= 0; --k) {
-#if SRBD_LAT_STREAM
-    if (wave >= 2 && k >= 1) {  // stage k - 1 into the image while stage k is factorized
-      lds_copy_range(a, img, qp, (k - 1) * kImgStage, k * kImgStage, threadIdx.x - 128, kLatThreads - 128);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-#endif
     if (wave == 0) {
       tstamp(0);
       const double* sl = img + k * kImgStage;

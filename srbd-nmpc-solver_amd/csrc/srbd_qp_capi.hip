@@ -15,7 +15,9 @@
 
 #include <cmath>
 #include <cstdio>
+#include <chrono>
 #include <cstring>
+#include <thread>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -724,10 +726,19 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
 // ---------------------------------------------------------------------------
 // host-buffer convenience path
 // ---------------------------------------------------------------------------
-#ifndef SRBD_SPIN_WAIT
-#define SRBD_SPIN_WAIT 1
-#endif
 namespace {
+// one polling step of the zero-copy wait: a pause hint where the host has one
+inline void spin_pause() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#else
+  std::this_thread::yield();
+#endif
+}
+// The single-QP launch is a few tens of microseconds: the zero-copy host solve polls for it
+// (the blocking wait's wake-up costs about as much as the kernel), for at most this long; a
+// longer solve (or a hung one) falls back to the blocking wait, so no host core spins for more.
+constexpr auto kSpinBudget = std::chrono::milliseconds(2);
 // host solves whose staged bytes fit this go through the handle's pinned buffer
 constexpr size_t kPinnedMaxBytes = size_t(8) << 20;
 struct Field {
@@ -923,12 +934,13 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
   if (small) {
     if (e == hipSuccess && in_end < off && !zero_copy)
       e = hipMemcpyAsync(pin + in_end, base + in_end, off - in_end, hipMemcpyDeviceToHost, h->stream);
-    // The single-QP launch is a few tens of microseconds: poll for it instead of the blocking
-    // wait, whose wake-up costs about as much as the kernel (-DSRBD_SPIN_WAIT=0: block).
-    if (e == hipSuccess && zero_copy && SRBD_SPIN_WAIT) {
+    // poll for the single-QP launch for at most kSpinBudget, then block (spin_pause above)
+    if (e == hipSuccess && zero_copy) {
+      const auto t_end = std::chrono::steady_clock::now() + kSpinBudget;
       hipError_t q;
-      while ((q = hipStreamQuery(h->stream)) == hipErrorNotReady) __builtin_ia32_pause();
-      if (q != hipSuccess) e = q;
+      while ((q = hipStreamQuery(h->stream)) == hipErrorNotReady && std::chrono::steady_clock::now() < t_end)
+        spin_pause();
+      if (q != hipSuccess && q != hipErrorNotReady) e = q;
     }
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)

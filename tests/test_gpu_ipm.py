@@ -192,14 +192,15 @@ def test_general_constraints_vs_oracle(pkg, oracle, dims, ric_alg):
                                                  (0, "Balance", 64), (1, "Balance", 64)])
 def test_degenerate_endgame_family(pkg, oracle, ric_alg, mode, min_ok):
     """The near-degenerate QP above (#12 of (12, 4, 14) seed 200) as 64 copies with Q, R, S,
-    A, B, q, r, b perturbed at 1e-15 relative.  Without iterative refinement (Speed) the
-    oracle converges on 63-64 of them; the GPU on 64 (ric_alg 0, whose fp64 factorization
-    forms P_k = F + K'H symmetrized as the oracle does, riccati.h SYMP; 58 before round 4) and
-    48 (ric_alg 1), the rest stopping at min step with x, u within 3.3e-5 of the oracle's and
-    the stationarity residual O(1) (barrier Hessians ~1e13).  With
-    HPIPM's refinement of the corrector (Balance: 2 corrections at most) both
-    converge on 64 / 64 (measured r03: every copy in 13 iterations, GPU and oracle).  The
-    x, u of every copy are held to the oracle's at 1e-6 (converged) or 1e-3 (min step)."""
+    A, B, q, r, b perturbed at 1e-15 relative.  Without iterative refinement (Speed) whether a
+    copy converges is a race between res_comp falling and the unrefined step's linear residual
+    (~eps x the 1e13 barrier Hessians) rising past tol_stat.  The oracle, in
+    HPIPM's own forms, converges on 64 (ric_alg 0) and 48 (ric_alg 1: the carried joint stage
+    factor, s-form predictor, p-form corrector -- ws->valid_ric_p, hpipm_d_ocp_qp_ipm.h:134); the
+    GPU on 64 and 48.  The count of the square-root variant is held to the oracle's within 8
+    (equivalent summation orders move it by about that much).  With HPIPM's refinement of the
+    corrector (Balance: 2 corrections at most) both converge on 64 / 64.  The x, u
+    of every copy are held to the oracle's at 1e-6 (converged) or 1e-3 (min step)."""
     qp, x0 = helpers.random_constrained(20, 12, 12, 4, 14, 200, pkg.OcpQpBatch)
     M = 64
     rng = np.random.default_rng(7)
@@ -218,8 +219,9 @@ def test_degenerate_endgame_family(pkg, oracle, ric_alg, mode, min_ok):
     st = dict(iter_max=50, mode=mode, ric_alg=ric_alg)
     out = pkg.capi.solve(fam, xb, st)
     ref = oracle.solve(fam, st, x0=xb)
-    assert (ref["status"] == 0).sum() >= (63 if mode == "Speed" else 64), ref["status"]
-    assert (out["status"] == 0).sum() >= min_ok, out["status"]
+    n_ref, n_out = (ref["status"] == 0).sum(), (out["status"] == 0).sum()
+    assert n_ref >= min_ok, ref["status"]
+    assert n_out >= min_ok and abs(int(n_out) - int(n_ref)) <= 8, (n_out, n_ref, out["status"])
     assert set(np.unique(out["status"])) <= {0, 2}, out["status"]
     for i in range(M):
         if ref["status"][i] != 0:

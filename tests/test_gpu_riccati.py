@@ -309,6 +309,37 @@ def test_latency_kernel_bit_identical(pkg, dtype, N, ric_alg):
     assert np.all(big["status"] == 0)
 
 
+def test_latency_kernel_nan_and_singular_r(pkg):
+    """The matrix-core single-QP kernel (batch <= 256, fp64, ric_alg 0, N <= 20: the
+    reference's own call) against the streaming kernel on the same QPs with bad data: a NaN in
+    one QP's R -> NaNDetected with a NaN stationarity residual in both; an input that is absent
+    from another QP (its R row / column, S row, B column and r entry zero at every stage, so
+    G's pivot is exactly 0: BLASFEO's dpotrf_l zeroes the direction) -> that input is 0,
+    Success, and the residuals, the objective and x, u agree with the streaming kernel."""
+    qp, x0 = pkg.srbd_model.generate_batch(300, N=20, seed=515, constraints="none")
+    qp.R[3, 7, 4, 4] = np.nan
+    i = 5
+    qp.R[10, :, i, :] = 0.0
+    qp.R[10, :, :, i] = 0.0
+    qp.S[10, :, i, :] = 0.0
+    qp.B[10, :, :, i] = 0.0
+    qp.r[10, :, i] = 0.0
+    st = dict(ric_alg=0)
+    big = pkg.capi.solve(qp, x0, st)                                     # streaming kernel
+    small = pkg.capi.solve(qp.subset(slice(0, 16)), x0[:16], st)         # matrix-core kernel
+    for out in (big, small):
+        assert out["status"][3] == 3 and np.isnan(out["res"][3, 0]), out["status"][:16]
+        ok = np.arange(16) != 3
+        assert np.all(out["status"][:16][ok] == 0)
+        assert np.all(out["u"][10, :, i] == 0.0)
+    for j in (0, 1):
+        assert np.all(np.abs(small["res"][ok, j] - big["res"][:16][ok, j]) <= 1e-10 + 1e-6 * np.abs(big["res"][:16][ok, j]))
+    np.testing.assert_allclose(small["obj"][ok], big["obj"][:16][ok], rtol=1e-11)
+    for key in ("x", "u"):
+        for q in np.nonzero(ok)[0]:
+            assert helpers.is_approx(small[key][q], big[key][q], 1e-11), (key, q)
+
+
 @pytest.mark.parametrize("ric_alg", [0, 1])
 def test_streaming_kernel_partial_waves(pkg, oracle, ric_alg):
     """N = 30 (over the LDS image cap: the streaming kernel at every batch size) with

@@ -165,9 +165,13 @@ def test_lq_fact_oracle(OcpQpBatch, oracle, dims, ric_alg):
 def test_lq_fact_oracle_degenerate_endgame(OcpQpBatch, oracle):
     """The near-degenerate family of tests/test_gpu_ipm.py test_degenerate_endgame_family (QP
     #12 of (12, 4, 14) seed 200, 64 copies perturbed at 1e-15) in Speed with the square-root
-    Riccati: the Cholesky converges on 63 of 64 (measured), the LQ factorization, which never
-    forms the ~1e13 barrier sums, on all 64; lq_fact 1 switches on the copies whose predictor
-    residual exceeds 1e-5."""
+    Riccati in HPIPM's form (the carried joint stage factor): the Cholesky converges on 48 of 64
+    (measured; the rest stop at min step once the unrefined step's linear residual, ~eps x the
+    1e13 barrier Hessians, passes tol_stat -- DESIGN.md 4.4), the LQ factorization, which never
+    forms the ~1e13 barrier sums, on all 64 in 13 iterations.  lq_fact 1 switches on the copies
+    whose predictor residual exceeds 1e-5 -- in Speed (no refinement) only once a stalled
+    Cholesky step has already been taken, so it does not rescue them; Balance adds the
+    refinement that does."""
     qp, x0 = helpers.random_constrained(20, 12, 12, 4, 14, 200, OcpQpBatch)
     M = 64
     rng = np.random.default_rng(7)
@@ -187,9 +191,9 @@ def test_lq_fact_oracle_degenerate_endgame(OcpQpBatch, oracle):
     chol = oracle.solve(fam, st, x0=xb)
     lq = oracle.solve(fam, dict(st, lq_fact=2), x0=xb)
     mix = oracle.solve(fam, dict(st, lq_fact=1), x0=xb)
-    assert (chol["status"] == 0).sum() >= 63
-    assert (lq["status"] == 0).sum() == 64
-    assert (mix["status"] == 0).sum() >= 63 and mix["lq_iters"].sum() > 0
+    assert (chol["status"] == 0).sum() >= 44
+    assert (lq["status"] == 0).sum() == 64 and np.all(lq["iter"] == 13)
+    assert mix["lq_iters"].sum() > 0 and np.all(mix["lq_iters"][mix["iter"] <= 13] == 0)
     for i in range(M):
         if chol["status"][i] == 0:
             assert helpers.is_approx(lq["u"][i], chol["u"][i], 1e-6), i
