@@ -76,7 +76,7 @@
 extern "C" {
 #endif
 
-#define SRBD_QP_ABI_VERSION 10
+#define SRBD_QP_ABI_VERSION 11
 #define SRBD_QP_MAX_NX 12
 #define SRBD_QP_MAX_NU 12
 #define SRBD_QP_MAX_NG 64
@@ -169,6 +169,15 @@ typedef struct srbd_qp_settings {
                      * solve's outputs, bit for bit; the call waits once to
                      * count them.  Worst case per QP: iter_max iterations (m of
                      * them fp32) plus iter_max fp64 ones.                  */
+  int lq_fact;      /* HPIPM's lq_fact (d_ocp_qp_ipm_arg_set "lq_fact",
+                     * hpipm_d_ocp_qp_ipm.h:78,147), square-root Riccati only:
+                     * -1 (default) = the mode's, as d_ocp_qp_ipm_arg_set_default
+                     * sets it (Balance 1, Robust 2, else 0); 0 = Cholesky
+                     * factorizations; 1 = Cholesky until a predictor step's
+                     * linear residual exceeds 1e-5, then LQ for the rest of
+                     * the solve; 2 = every stage factorization by LQ (the
+                     * barrier Hessians are absorbed as columns, never summed).
+                     * Ignored with ric_alg = 0. (ABI 11)                    */
 } srbd_qp_settings;
 
 typedef struct srbd_qp_data_f64 {

@@ -141,6 +141,7 @@ typedef struct {
   double dlam_l, dlam_u, dt_l, dt_u;
   double aff_l, aff_u;           /* dlam_aff * dt_aff                        */
   double G;                      /* this iteration's barrier Hessian weight  */
+  int gidx;                      /* general rows: the row's index in 0..ng-1  */
 } row_t;
 
 typedef struct {
@@ -223,6 +224,7 @@ static stage_rows_t* build_rows(const dims_t* d, int* nc_out) {
         if (!hl && !hu) continue;
         row_t* rw = &st[k].rows[nr++];
         rw->kind = 1;
+        rw->gidx = c;
         rw->Drow = (k < d->N && qp->D) ? qp->D + (size_t)k * d->ng * d->nu + c : NULL;
         /* C_0 dropped: hpipm-cpp embeds x0 with nx[0]=0 (ocp_qp_ipm_solver.cpp:128) */
         rw->Crow = (k > 0 && qp->C) ? qp->C + (size_t)k * d->ng * d->nx + c : NULL;
@@ -549,84 +551,92 @@ static void lq_pd(int n, int m, double* M) {
   }
 }
 
-/* HPIPM's lq_fact factorization (d_ocp_qp_fact_lq_solve_kkt_step, restated): the stage's
- * barrier-augmented Hessian is never formed.  Stage k factors
- *   M_k = [ chol(RSQ_k) | sqrt(reg) e_i (inputs) | sqrt(G_r) row_r (every bound / general
- *           row) | [B'; A'] Lx_{k+1} ]
- * as M_k = L_k Q with L_k = [Lu 0; Lxu Lx] lower ([u; x] order), so L_k L_k' = RSQ_k + Gamma_k
- * + reg + [B'; A'] P_{k+1} [B A] -- riccati_factor's matrix -- with Gamma entering as its
- * square root beside the data instead of being added to it.  Then chol(G) = Lu, K = -G^-1 H
- * with H = Lu Lxu', P_k = Lx Lx' (the record riccati_vectors reads).  Stage N: L_N from
- * [chol(Q_N) | sqrt(G_r) row_r], P_N = L_N L_N'.                                            */
+/* HPIPM's lq_fact factorization (d_ocp_qp_fact_lq_solve_kkt_step, hpipm_d_ocp_qp_kkt.h:58,
+ * restated): the stage's barrier-augmented Hessian is never formed.  Stage k's factor
+ * L_k = [Lu 0; Lxu Lx] ([u; x] order) is
+ *   L_k = LQ([ chol(RSQ_k + Gamma_box + reg_u) | [B'; A'] Lx_{k+1} | sqrt(G_r) [D_r'; C_r'] ... ])
+ * so L_k L_k' = RSQ_k + Gamma_k + reg + [B'; A'] P_{k+1} [B A] -- riccati_factor's matrix -- with
+ * the dense terms (the cost-to-go and the general rows) entering as columns beside the data
+ * instead of being added to it.  The columns are absorbed block by block (the cost-to-go, then
+ * the general rows in chunks of 12 by row index), one positive-diagonal LQ (lq_pd) per block,
+ * as the HIP library's riccati_step_lq does.  HPIPM keeps the box Gamma as a diagonal block
+ * beside the Hessian factor (dgelqf_pd_lla); here, as on the GPU, it is added to the Hessian's
+ * diagonal before its Cholesky (a diagonal addition cannot cancel).  The factor feeds the
+ * square-root vector and forward routines (HPIPM's lq path solves with L exactly as the
+ * Cholesky square root does); P, Lg, K are filled for the getters.                         */
 static void fill_stage_H(const dims_t* d, int k, double* Ht, double* gt);
 static int riccati_factor_lq(const dims_t* d, ric_ws_t* w, const stage_rows_t* st, double reg) {
-  const int nx = d->nx, nu = d->nu, N = d->N;
-  double* M = (double*)malloc(sizeof(double) * 64 * 512);
-  double Lx[32 * 32], Hd[64 * 64], gdum[64], vrow[64];
+  const int nx = d->nx, nu = d->nu, N = d->N, ng = d->ng;
+  double* M = (double*)malloc(sizeof(double) * 64 * 128);
+  double Hd[64 * 64], gdum[64], vrow[64];
   if (!M) return -1;
   w->sq = 1;
   for (int k = N; k >= 0; --k) {
     const int nu_k = st[k].nu_k, ns = nu_k + nx;
-    int m = 0;
     fill_stage_H(d, k, Hd, gdum);
-    chol(ns, Hd);
-    for (int j = 0; j < ns; ++j, ++m)
-      for (int i = 0; i < ns; ++i) M_(M, ns, i, m) = M_(Hd, ns, i, j);
-    if (reg > 0.0)
-      for (int j = 0; j < nu_k; ++j, ++m)
-        for (int i = 0; i < ns; ++i) M_(M, ns, i, m) = i == j ? sqrt(reg) : 0.0;
     for (int r = 0; r < st[k].nrow; ++r) {
       const row_t* rw = &st[k].rows[r];
-      if (!(rw->G > 0.0)) continue;
-      for (int i = 0; i < ns; ++i) vrow[i] = 0.0;
-      row_axpy(d, rw, nu_k, sqrt(rw->G), vrow, vrow + nu_k);
-      for (int i = 0; i < ns; ++i) M_(M, ns, i, m) = vrow[i];
-      ++m;
+      if (rw->kind == 0) M_(Hd, ns, rw->var, rw->var) += rw->G;
     }
-    if (k < N) {
+    for (int j = 0; j < nu_k; ++j) M_(Hd, ns, j, j) += reg;
+    chol(ns, Hd);
+    for (int j = 0; j < ns; ++j)
+      for (int i = 0; i < ns; ++i) M_(M, ns, i, j) = M_(Hd, ns, i, j);
+    if (k < N) { /* the cost-to-go [B'; A'] Lx_{k+1} */
       const double* A = qA(d, k);
       const double* B = qB(d, k);
-      for (int j = 0; j < nx; ++j, ++m) {
+      const double* Ln = w->Lf + (size_t)(k + 1) * (size_t)d->n * d->n;
+      const int nun = k + 1 < N ? nu : 0, ldn = nun + nx;
+      for (int j = 0; j < nx; ++j) {
         for (int i = 0; i < nu; ++i) {
           double acc = 0.0;
-          for (int l = 0; l < nx; ++l) acc += M_(B, nx, l, i) * M_(Lx, nx, l, j);
-          M_(M, ns, i, m) = acc;
+          for (int l = j; l < nx; ++l) acc += M_(B, nx, l, i) * M_(Ln, ldn, nun + l, nun + j);
+          M_(M, ns, i, ns + j) = acc;
         }
         for (int i = 0; i < nx; ++i) {
           double acc = 0.0;
-          for (int l = 0; l < nx; ++l) acc += M_(A, nx, l, i) * M_(Lx, nx, l, j);
-          M_(M, ns, nu + i, m) = acc;
+          for (int l = j; l < nx; ++l) acc += M_(A, nx, l, i) * M_(Ln, ldn, nun + l, nun + j);
+          M_(M, ns, nu + i, ns + j) = acc;
         }
       }
+      lq_pd(ns, ns + nx, M);
     }
-    lq_pd(ns, m, M);
-    /* the stage factor for the square-root vector and forward routines (HPIPM's lq path
-     * solves with L exactly as the Cholesky square root does) */
+    for (int c0 = 0; c0 < ng; c0 += 12) { /* the general rows, 12 by row index */
+      int m = ns;
+      for (int r = 0; r < st[k].nrow; ++r) {
+        const row_t* rw = &st[k].rows[r];
+        if (rw->kind != 1 || rw->gidx < c0 || rw->gidx >= c0 + 12 || !(rw->G > 0.0)) continue;
+        for (int i = 0; i < ns; ++i) vrow[i] = 0.0;
+        row_axpy(d, rw, nu_k, sqrt(rw->G), vrow, vrow + nu_k);
+        for (int i = 0; i < ns; ++i) M_(M, ns, i, m) = vrow[i];
+        ++m;
+      }
+      if (m > ns) lq_pd(ns, m, M);
+    }
     double* Lk = w->Lf + (size_t)k * (size_t)d->n * d->n;
     for (int j = 0; j < ns; ++j)
       for (int i = 0; i < ns; ++i) M_(Lk, ns, i, j) = i >= j ? M_(M, ns, i, j) : 0.0;
     double* P = w->P + (size_t)k * nx * nx;
     for (int j = 0; j < nx; ++j)
-      for (int i = 0; i < nx; ++i) M_(Lx, nx, i, j) = i >= j ? M_(M, ns, nu_k + i, nu_k + j) : 0.0;
-    for (int j = 0; j < nx; ++j)
       for (int i = 0; i < nx; ++i) {
         double acc = 0.0;
-        for (int l = 0; l < nx; ++l) acc += M_(Lx, nx, i, l) * M_(Lx, nx, j, l);
+        for (int l = 0; l < nx; ++l) acc += M_(Lk, ns, nu_k + i, nu_k + l) * M_(Lk, ns, nu_k + j, nu_k + l);
         M_(P, nx, i, j) = acc;
       }
     if (k == N) continue;
     double* L = w->Lg + (size_t)k * nu * nu;
     for (int j = 0; j < nu; ++j)
-      for (int i = 0; i < nu; ++i) M_(L, nu, i, j) = i >= j ? M_(M, ns, i, j) : 0.0;
+      for (int i = 0; i < nu; ++i) M_(L, nu, i, j) = M_(Lk, ns, i, j);
     double* K = w->K + (size_t)k * nu * nx;
-    for (int j = 0; j < nx; ++j) {
+    for (int j = 0; j < nx; ++j) { /* K[:, j] = -Lu^-T Lxu[j, :]' */
       double col[32];
-      for (int i = 0; i < nu; ++i) {  /* H[:, j] = Lu Lxu'[:, j] */
-        double acc = 0.0;
-        for (int l = 0; l <= i; ++l) acc += M_(L, nu, i, l) * M_(M, ns, nu + j, l);
-        col[i] = acc;
+      for (int i = 0; i < nu; ++i) col[i] = M_(Lk, ns, nu + j, i);
+      for (int i = nu - 1; i >= 0; --i) {
+        double sacc = col[i];
+        for (int l = i + 1; l < nu; ++l) sacc -= M_(Lk, ns, l, i) * col[l];
+        const double dd = M_(Lk, ns, i, i);
+        col[i] = dd > 0.0 ? sacc / dd : 0.0;
       }
-      chol_solve(nu, L, col);
       for (int i = 0; i < nu; ++i) M_(K, nu, i, j) = -col[i];
     }
   }
@@ -1014,7 +1024,10 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
 
   double alpha_prim = 1.0, alpha_dual = 1.0;
   int iter = 0;
-  int force_lq = set->lq_fact == 2;  /* lq_fact 1 switches for the rest of the solve */
+  /* lq_fact applies to the square-root Riccati only ("for square_root_alg==1",
+   * hpipm_d_ocp_qp_ipm.h:78); 1 switches for the rest of the solve */
+  const int lqf = set->ric_alg ? set->lq_fact : 0;
+  int force_lq = lqf == 2;
   for (;;) {
     compute_residuals(&d, st, x, u, pi, rg, rb, res->res, &res->obj, w.gstride);
     double mu = 0.0;
@@ -1092,7 +1105,7 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
     for (int s = 0; s <= N; ++s)
       for (int i = 0; i < st[s].nrow; ++i) { st[s].rows[i].aff_l = 0.0; st[s].rows[i].aff_u = 0.0; }
     STEP_TLAM();
-    if (set->lq_fact == 1 && !force_lq) {
+    if (lqf == 1 && !force_lq) {
       /* HPIPM lq_fact 1: the predictor step's linear residual decides; above 1e-5 (or NaN) the
        * factorization is redone by LQ, and LQ stays for the rest of the solve */
       double ng = 0.0, nb = 0.0;
@@ -1264,7 +1277,7 @@ int oracle_solve(const oracle_ocp_qp* qp, const oracle_settings* set, const doub
         row_syr(&d, rw, nu_k, G, Ht);
       }
     }
-    if (set->lq_fact == 2) {
+    if (lqf == 2) {
       for (int s = 0; s <= N; ++s)
         for (int i = 0; i < st[s].nrow; ++i) {
           row_t* rw = &st[s].rows[i];

@@ -79,12 +79,17 @@ def _ptr(a: Optional[np.ndarray]):
 DEFAULT_SETTINGS = dict(iter_max=15, alpha_min=1e-8, mu0=1e2, tol_stat=1e-8, tol_eq=1e-8,
                         tol_ineq=1e-8, tol_comp=1e-8, reg_prim=1e-12, warm_start=0, pred_corr=1,
                         split_step=0, ric_alg=1, itref_corr_max=0,  # hpipm-cpp defaults (settings.hpp:26-86)
-                        lq_fact=0)  # (HPIPM's Balance / Robust: 1 / 2 -- only when asked)
+                        lq_fact=0)  # HPIPM: Balance 1, Robust 2 with the square root (MODE_LQ)
 
 
 # HPIPM's mode-dependent itref_corr_max (d_ocp_qp_ipm_arg_set_default; the HIP library
 # derives it from settings.mode the same way, srbd_qp_capi.hip)
 MODE_ITREF = {"SpeedAbs": 0, "Speed": 0, "Balance": 2, "Robust": 4, 0: 0, 1: 0, 2: 2, 3: 4}
+
+
+# and its lq_fact, with the square-root Riccati only (hpipm_d_ocp_qp_ipm.h:78); the HIP library
+# derives it the same way (srbd_qp_capi.hip)
+MODE_LQ = {"SpeedAbs": 0, "Speed": 0, "Balance": 1, "Robust": 2, 0: 0, 1: 0, 2: 1, 3: 2}
 
 
 def _settings(s: Optional[Dict], ng: int = 0) -> _Settings:
@@ -93,6 +98,8 @@ def _settings(s: Optional[Dict], ng: int = 0) -> _Settings:
         d.update({k: v for k, v in s.items() if k in d})
         if "mode" in s and "itref_corr_max" not in s:
             d["itref_corr_max"] = MODE_ITREF[s["mode"]]
+        if s.get("lq_fact", -1) == -1:  # (-1: the mode's, as the C-ABI's srbd_qp_settings)
+            d["lq_fact"] = MODE_LQ[s.get("mode", "Speed")] if d["ric_alg"] else 0
     return _Settings(**d)
 
 

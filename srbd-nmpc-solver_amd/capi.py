@@ -37,7 +37,7 @@ class Settings(C.Structure):
                 ("tol_ineq", C.c_double), ("tol_comp", C.c_double), ("reg_prim", C.c_double),
                 ("warm_start", C.c_int), ("pred_corr", C.c_int), ("ric_alg", C.c_int),
                 ("split_step", C.c_int), ("compute_residuals", C.c_int),
-                ("f64_rescue", C.c_int), ("f32_iters", C.c_int)]
+                ("f64_rescue", C.c_int), ("f32_iters", C.c_int), ("lq_fact", C.c_int)]
 
 
 DATA_FIELDS = ("A", "B", "b", "Q", "S", "R", "q", "r",

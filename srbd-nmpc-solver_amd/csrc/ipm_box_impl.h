@@ -15,13 +15,20 @@ constexpr int kPhInit = 0, kPhRB = 1, kPhF1 = 2, kPhB2 = 3, kPhF2 = 4, kPhOut = 
 // iterative refinement of the corrector step: IR = residual of the step's linear system
 // and the check, IS = the correction's backward recursion, F3 = its forward sweep
 constexpr int kPhIR = 6, kPhF3 = 7, kPhIS = 8;
+// HPIPM lq_fact 1: the predictor step's linear residual (IRP, IR's arithmetic) and the switch
+constexpr int kPhIRP = 9, kPhLqChk = 10;
+constexpr real kLqSwitch = real(1e-5);  // d_ocp_qp_ipm_solve: refactorize by LQ above this
 // per-QP scalar state, kQsSize reals at the head of the QP's workspace
 constexpr int kQsAlphaP = 0, kQsAlphaD = 1, kQsLastAmin = 2, kQsMu = 3, kQsMuSum = 4,
               kQsSigmaMu = 5, kQsStatus = 6, kQsIter = 7, kQsNc = 8, kQsResStat = 9,
               kQsResEq = 10, kQsResIneq = 11, kQsResComp = 12, kQsObj = 13,
               // iterative refinement of this iteration's step: corrections applied, done flag,
               // the first check's linear-residual norms (HPIPM's itref_qp_norm0)
-              kQsItCnt = 14, kQsItDone = 15, kQsItN0g = 16, kQsItN0b = 17, kQsSize = 20;
+              kQsItCnt = 14, kQsItDone = 15, kQsItN0g = 16, kQsItN0b = 17,
+              // HPIPM lq_fact: the stage factorizations are LQ (sticky: lq_fact 2 from the start,
+              // lq_fact 1 once a predictor's linear residual exceeded 1e-5), and the pending redo
+              // of this iteration's factorization + predictor by LQ (lq_fact 1)
+              kQsForceLq = 18, kQsLqRedo = 19, kQsSize = 20;
 constexpr real kStepTau = real(0.995);  // fraction to the boundary
 
 __device__ __forceinline__ real gsum(real v) {
@@ -450,13 +457,15 @@ __device__ __forceinline__ int group_qp(const ProblemArgsT<real>& a) {
   return slot_qp(a, (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4));
 }
 
-template <bool FULL, int GEN, int PH, bool SQRT = false>
+// LQ (ric_alg 1 only): HPIPM's lq_fact -- 0 Cholesky factorizations, 2 LQ (riccati.h
+// riccati_step_lq) in every RB, 1 per QP: Cholesky until the switch (kQsForceLq), then LQ.
+template <bool FULL, int GEN, int PH, bool SQRT = false, int LQ = 0>
 __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   // the refinement check runs stage-parallel: group g on QP slot g / (N + 1), stage
   // g % (N + 1) (its rows are independent across stages); every other phase: one QP per group
   int kst = 0;
   int qp;
-  if constexpr (PH == kPhIR) {
+  if constexpr (PH == kPhIR || PH == kPhIRP) {
     const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4);
     const int slot = g / (a.N + 1);
     kst = g - slot * (a.N + 1);
@@ -804,6 +813,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     qs[kQsStatus] = -real(1.0);
     qs[kQsIter] = real(0.0);
     qs[kQsNc] = nc;
+    qs[kQsForceLq] = a.lq_fact == 2 ? real(1.0) : real(0.0);
+    qs[kQsLqRedo] = real(0.0);
   }
 
     return;
@@ -911,6 +922,9 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     return;
   }
   if (status >= 0) return;  // this QP has exited
+  // the lq_fact 1 redo launch (RB -> F1 by LQ of the QPs whose check switched them)
+  if constexpr (PH == kPhRB || PH == kPhF1)
+    if (a.lq_redo && qs[kQsLqRedo] == real(0.0)) return;
   const int par = iter & 1;  // record written by this iteration's factorization
   const real alpha_p = qs[kQsAlphaP], alpha_d = qs[kQsAlphaD], last_amin = qs[kQsLastAmin];
   if constexpr (PH == kPhRB) {
@@ -945,6 +959,27 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     mg = mb = md = mm = musum = objl = real(0.0);
     real xn = real(0.0), pin = real(0.0);  // updated x_{k+1}, pi_{k+1} (element-owned), from stage k+1
     real P[12];
+    // this QP's factorizations by LQ (HPIPM lq_fact): the general rows' sqrt(Gamma) [D'; C'] and
+    // the cost-to-go are absorbed by reflections instead of summed into the Hessian
+    const bool use_lq = SQRT && (LQ == 2 || (LQ == 1 && qs[kQsForceLq] != real(0.0)));
+    const bool own = lane < kMaxDim;
+    // stage ks's general-row columns sqrt(Gamma_r) [D_r'; C_r'], one 12-row chunk at a time
+    auto absorb_rows = [&](int ks, LqRows<real>& L) {
+      if constexpr (GEN > 0) {
+        for (int ch = 0; ch < c.nch; ++ch) {
+          real G, gg, Gb[12], Cc[12], Dc[12], Au[12], Ax[12];
+          g_gamma(ks, ch, false, real(0.0), G, gg);
+          gather12(__builtin_sqrt(G), Gb);
+          c.g_col(ks, ch, col, Cc, Dc);
+          sfor<0, 12>([&](auto i) {
+            constexpr int I = decltype(i)::value;
+            Au[I] = own ? Dc[I] * Gb[I] : real(0.0);
+            Ax[I] = (GEN == 2 && own) ? Cc[I] * Gb[I] : real(0.0);
+          });
+          lq_absorb(L, Au, Ax, lane);
+        }
+      }
+    };
     for (int k = N; k >= 0; --k) {
       tstamp(20);
       real* stk = c.st(k);
@@ -1074,7 +1109,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             }
             gea = dot_bcast(Dc, e, gea);
           }
-          if constexpr (GEN == 1) {
+          if constexpr (GEN == 1) if (!use_lq) {
             // D'Gamma D from sqrt(Gamma) D: exactly symmetric (see g_hess); formed in greal
             const greal sG = __builtin_sqrt(greal(G));
             greal Dg[12];
@@ -1167,7 +1202,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         const real qt = finish_x(rgx + qx);
         real qv[12];
         gather12(qt, qv);
-        if constexpr (GEN == 2) g_hess(N, 2, P, P);
+        if constexpr (GEN == 2) if (!use_lq) g_hess(N, 2, P, P);
         sfor<0, 12>([&](auto i) {
           constexpr int I = decltype(i)::value;
           if (lane == I) P[I] += Gx;
@@ -1176,7 +1211,34 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         if (c.isv) store12(rec + kRecPv, P);
         if constexpr (SQRT && !kRecFactor)
           if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
-        if constexpr (SQRT) sqrt_factor(P, lane);  // (kRecFactor: the record keeps the factor)
+        if constexpr (SQRT) {  // (kRecFactor: the record keeps the factor)
+          if (GEN == 2 && use_lq) {
+            // L_N = LQ([chol(Q_N + Gamma_x) | sqrt(Gamma) C_N']), s_N = L_N^-1 q~_N
+            LqRows<real> L;
+            real Pm[12], rsx;
+            sfor<0, 12>([&](auto i) {
+              constexpr int I = decltype(i)::value;
+              L.Lu[I] = real(0.0);
+              L.Lxu[I] = real(0.0);
+              Pm[I] = c.isv ? real(0.0) : P[I];
+            });
+            chol_cols(Pm, lane, real(0.0), L.Lx, rsx);
+            group_transpose(ldsB, lane, L.Lx, -1);
+            absorb_rows(N, L);
+            group_transpose(ldsB, lane, L.Lx, 1);
+            real dd = real(0.0);
+            sfor<0, 12>([&](auto i) {
+              if (lane == decltype(i)::value) dd = L.Lx[decltype(i)::value];
+            });
+            rsx = dd > real(0.0) ? real(1.0) / dd : real(0.0);
+            trsv_lower(L.Lx, rsx, P);  // VL: s_N (the matrix lanes' results are replaced)
+            sfor<0, 12>([&](auto i) {
+              if (!c.isv) P[decltype(i)::value] = L.Lx[decltype(i)::value];
+            });
+          } else {
+            sqrt_factor(P, lane);
+          }
+        }
         if constexpr (!SQRT || kRecFactor)
           if (lane < kMaxDim) store_packed_col(rec + kRecP, lane, P);
       } else {
@@ -1227,11 +1289,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           const real ru = dot_bcast(Rr, uk, real(0.0));  // R u, before the barrier Hessian goes in
           objl += uk * (real(0.5) * ru + rk + sxu);
           rt = finish_u(rgu + ru);
-          if constexpr (GEN == 2) g_hess(k, 0, Rr, Rr);
+          if constexpr (GEN == 2) if (!use_lq) g_hess(k, 0, Rr, Rr);
           sfor<0, 12>([&](auto i) {
             constexpr int I = decltype(i)::value;
             Rc[I] = greal(Rr[I]);
-            if constexpr (GEN == 1) Rc[I] += greal(kRgLds ? rg_lds[I * 256 + threadIdx.x] : RG[I]);
+            if constexpr (GEN == 1) if (!use_lq) Rc[I] += greal(kRgLds ? rg_lds[I * 256 + threadIdx.x] : RG[I]);
             if (lane == I) Rc[I] += (I < nu) ? greal(Gu) : greal(1.0);  // padded inputs: R = 1
             if (c.isv) Rc[I] = greal(0.0);
           });
@@ -1242,7 +1304,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           const real qx = dot_bcast(Qc, xk, real(0.0));
           if (k > 0) objl += xk * (real(0.5) * qx + qk);
           const real qt = finish_x(rgx + qx);
-          if constexpr (GEN == 2) g_hess(k, 1, Sc, Qc);  // C = 0: D'Gamma C = C'Gamma C = 0
+          if constexpr (GEN == 2) if (!use_lq) g_hess(k, 1, Sc, Qc);  // C = 0: D'Gamma C = C'Gamma C = 0
           sfor<0, 12>([&](auto i) {
             constexpr int I = decltype(i)::value;
             const real rI = bc<I>(rt), qI = bc<I>(qt);
@@ -1256,8 +1318,18 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         tstamp(22);
         StageFactor<real> f;
         if constexpr (SQRT) {
-          // (HPIPM's square-root form: P_k = F - Y'Y as the trailing block of the joint factor)
-          riccati_step_sqrt<1, false, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f);
+          if (LQ != 0 && use_lq) {
+            auto loadR_lq = [&](real (&Rc)[12]) {
+              greal Rg[12];
+              loadR(Rg);
+              sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = real(Rg[decltype(i)::value]); });
+            };
+            riccati_step_lq(P, A_, B_, loadR_lq, loadSQ, lane, reg, f, ldsB,
+                            [&](LqRows<real>& L, int) { absorb_rows(k, L); });
+          } else {
+            // (HPIPM's square-root form: P_k = F - Y'Y as the trailing block of the joint factor)
+            riccati_step_sqrt<1, false, greal>(P, A_, B_, loadR, loadSQ, lane, reg, f);
+          }
         } else {
           // P_k = F + K'H, symmetrized (riccati.h SYMP); H waits in the group's B block (dead
           // since the residual products; the record image overwrites it only afterwards)
@@ -1278,12 +1350,13 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           store12(img + kRecKv, f.Kc);
           store12(img + kRecPv, f.F);
         }
-        sfor<0, 12>([&](auto i) {
-          constexpr int I = decltype(i)::value;
-          P[I] = f.F[I];
-        });
+        if (!(SQRT && use_lq))  // (riccati_step_lq leaves the next factor in P)
+          sfor<0, 12>([&](auto i) {
+            constexpr int I = decltype(i)::value;
+            P[I] = f.F[I];
+          });
         if constexpr (SQRT) {
-          sqrt_factor(P, lane);
+          if (!use_lq) sqrt_factor(P, lane);
           if constexpr (kRecFactor)
             if (lane < kMaxDim) store_packed_col(img + kRecP, lane, P);
         }
@@ -1344,7 +1417,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
 
     return;
   }
-  if constexpr (PH == kPhIR || PH == kPhIS || PH == kPhF3) {
+  if constexpr (PH == kPhIR || PH == kPhIRP || PH == kPhIS || PH == kPhF3 || PH == kPhLqChk) {
     // ============== iterative refinement of the step (HPIPM itref_corr_max) ==============
     // The step (du, dx, dpi and the bounds' dt, dlam) solves the Newton system only up to the
     // factorization's rounding.  IR (one group per stage) forms the linear residual of that system at the
@@ -1361,11 +1434,45 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     // dt / dlam (linear in the primal step: ddt = +-ddv, ddlam = -lam ddt / t) and redoes the
     // step lengths.  (A check that passes costs IR alone: IS and F3 return at the top.)
     // (F2 advanced iter: the step's factorization has the parity of iter - 1.)
-    if (qs[kQsItDone] != real(0.0)) return;
-    const int fpar = (iter - 1) & 1;
-    real* const next = a.stat && lane == 0 ? a.stat + ((size_t)qp * a.stat_rows + iter) * kStatCols
-                                           : nullptr;
-    if constexpr (PH == kPhIR) {
+    // (kPhIRP / kPhLqChk: HPIPM's lq_fact 1 check of the predictor step -- IR's residual of the
+    // predictor's system, then the switch -- for the QPs still on the Cholesky factorization)
+    constexpr bool kPred = PH == kPhIRP || PH == kPhLqChk;
+    if constexpr (kPred) {
+      if (a.lq_fact != 1 || qs[kQsForceLq] != real(0.0)) return;
+    } else if (qs[kQsItDone] != real(0.0)) {
+      return;
+    }
+    // parity of the step's factorization: this iteration's (the predictor, before F2 advanced
+    // iter) or the previous count's (after it); the other slot takes the residual
+    const int fpar = kPred ? (iter & 1) : ((iter - 1) & 1);
+    real* const next = !kPred && a.stat && lane == 0
+                           ? a.stat + ((size_t)qp * a.stat_rows + iter) * kStatCols
+                           : nullptr;
+    if constexpr (PH == kPhLqChk) {
+      // the predictor's linear residual above 1e-5 (or NaN): refactorize this iteration by LQ
+      // and keep LQ for the rest of the solve (d_ocp_qp_ipm_solve, lq_fact 1); the redo launch
+      // recomputes RB -> F1 from the same iterate (no step applied: alpha 0)
+      real ng = real(0.0), nb = real(0.0);
+      for (int k0 = 0; k0 <= N; k0 += kGroup) {
+        const int k = k0 + lane;
+        const real* slot = c.st(k <= N ? k : N) + (fpar ^ 1) * kRecSize;
+        const real g1 = slot[36], b1 = slot[37];
+        if (k <= N) {
+          ng = fmax(ng, g1);
+          nb = fmax(nb, b1);
+        }
+      }
+      const real nga = gmax(ng), nba = gmax(nb);
+      if (!(nga <= kLqSwitch) || !(nba <= kLqSwitch)) {
+        if (lane == 0) {
+          qs[kQsForceLq] = real(1.0);
+          qs[kQsLqRedo] = real(1.0);
+          qs[kQsAlphaP] = real(0.0);
+          qs[kQsAlphaD] = real(0.0);
+        }
+      }
+      return;
+    } else if constexpr (PH == kPhIR || PH == kPhIRP) {
       // one 12 x 12 LDS block per QP group (A, B, S in turn): 18 KB per workgroup, so the
       // sweep runs at its register occupancy (RB's three blocks would cap it at 2 waves/SIMD)
       __shared__ real ir_lds[(256 / kGroup) * 144];
@@ -1752,6 +1859,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     real ap = real(1e30), ad = real(1e30);
     real s1 = real(0.0), s2 = real(0.0);  // predictor sums lam dt + t dlam, dlam dt (element-owned)
     bool bad = false;  // a non-finite component in the final step (fp32 breakdown)
+    // the step is kept (kStStep): the final one (F2, or F1 without corrector), or the
+    // predictor whose linear residual decides HPIPM's lq_fact 1 switch (kPhIRP / kPhLqChk)
+    const bool final_step = corr || !a.pred_corr;
+    const bool lq_chk = !corr && a.lq_fact == 1 && !a.lq_redo && qs[kQsForceLq] == real(0.0);
+    const bool keep_step = final_step || lq_chk;
       // ---- forward step (F1 predictor / F2 corrector), row-owned ----
       ap = real(1e30);
       ad = real(1e30);
@@ -1762,7 +1874,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         const real* rec = stk + par * kRecSize;
         // dpi = P dx + p is part of the final step only (F2, or F1 without corrector)
         real dpi = real(0.0);
-        if (corr || !a.pred_corr) dpi = rec_P_mul(rec, dxk, rec[kRecPv + li]);
+        if (keep_step) dpi = rec_P_mul(rec, dxk, rec[kRecPv + li]);
         real du = real(0.0), dxn = real(0.0);
         if (k < N) {
           // du = K dx + k, dx+ = A dx + B du + b~ (open loop: the QP's own A, B; b~ = res_b,
@@ -1858,9 +1970,10 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           }
           c.put_bstep(stk, 0, lane, nu_);
           c.put_bstep(stk, 1, lane, nx_);
-          if (corr || !a.pred_corr) {  // the predictor's du / dx / dpi are not used
+          if (final_step)
             bad |= huge(du) || huge(dxk) || huge(dpi) || huge(nu_.dtl) || huge(nu_.dtu) ||
                    huge(nu_.dll) || huge(nu_.dlu);
+          if (keep_step) {  // (otherwise the predictor's du / dx / dpi are not used)
             stk[kStStep + lane] = du;
             stk[kStStep + 12 + lane] = dxk;
             stk[kStStep + 24 + lane] = k > 0 ? dpi : real(0.0);
@@ -1885,6 +1998,8 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         next[1] = mu_aff;
         next[2] = sg;
       }
+      if (next) next[11] = qs[kQsForceLq] != real(0.0) ? real(1.0) : real(0.0);  // HPIPM stat: lq_fact
+      if (a.lq_redo && lane == 0) qs[kQsLqRedo] = real(0.0);
     }
     if (corr || !a.pred_corr) {
       // ---- step length of the iteration ----
@@ -1957,7 +2072,7 @@ __device__ __forceinline__ bool solve_done(const ProblemArgsT<real>& a) {
   return a.ctl && __atomic_load_n(a.ctl + kCtlDone, __ATOMIC_RELAXED) != 0;
 }
 
-template <bool FULL, int GEN, int PH, bool SQRT = false>
+template <bool FULL, int GEN, int PH, bool SQRT = false, int LQ = 0>
 __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase_kernel(ProblemArgsT<real> a) {
   if constexpr (PH == kPhInit) {  // this solve's live-QP counters and control words start at 0
     if (a.ctl)
@@ -1966,7 +2081,7 @@ __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase_
   }
   if constexpr (PH != kPhInit && PH != kPhOut)
     if (solve_done(a)) return;
-  ipm_phase<FULL, GEN, PH, SQRT>(a);
+  ipm_phase<FULL, GEN, PH, SQRT, LQ>(a);
   if constexpr (PH == kPhRB) report_running(a);
 }
 
@@ -1975,13 +2090,14 @@ __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase_
 // their records are still in L2 / the Infinity Cache, and the launch count halves.
 // The second phase re-reads the per-QP state the first one wrote (same wave:
 // visible after the workgroup-scope fence).
-template <bool FULL, int GEN, int PH1, int PH2, bool SQRT = false>
+template <bool FULL, int GEN, int PH1, int PH2, bool SQRT = false, int LQ = 0>
 __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase2_kernel(ProblemArgsT<real> a) {
   if (solve_done(a)) return;
-  ipm_phase<FULL, GEN, PH1, SQRT>(a);
+  ipm_phase<FULL, GEN, PH1, SQRT, LQ>(a);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  ipm_phase<FULL, GEN, PH2, SQRT>(a);
-  if constexpr (PH1 == kPhRB) report_running(a);
+  ipm_phase<FULL, GEN, PH2, SQRT, LQ>(a);
+  if constexpr (PH1 == kPhRB)
+    if (!a.lq_redo) report_running(a);  // (the lq_fact 1 redo repeats an RB already counted)
 }
 
 // Active-QP compaction, decided on the device after the RB sweep of iteration `it`: when the
@@ -2022,7 +2138,7 @@ __global__ void __launch_bounds__(256) compact_running_kernel(const real* __rest
 #endif
 constexpr bool kIpmSplit = SRBD_IPM_SPLIT != 0;
 
-template <bool FULL, int GEN, bool SQRT>
+template <bool FULL, int GEN, bool SQRT, int LQ>
 static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream) {
   const int threads = 256;
   const long long lanes = (long long)a.batch * kGroup;
@@ -2056,14 +2172,24 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
     b.launch_it = it;
     if (it >= a.iter_max) {
       if (!a.skip_last_rb)
-        hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT>), grid, block, 0, stream, b);
+        hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT, LQ>), grid, block, 0, stream, b);
       break;
     }
     if (kIpmSplit) {  // diagnostic schedule: one launch per sweep
-      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT>), grid, block, 0, stream, b);
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT, LQ>), grid, block, 0, stream, b);
       hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF1, SQRT>), grid, block, 0, stream, b);
     } else {
-      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT>), grid, block, 0, stream, b);
+      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT, LQ>), grid, block, 0, stream, b);
+    }
+    if constexpr (LQ == 1) {
+      // HPIPM lq_fact 1: the predictor step's linear residual (stage-parallel, IR's arithmetic),
+      // the switch, and RB -> F1 again by LQ for the QPs it switched (from the same iterate)
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhIRP, SQRT>), dim3(grid.x * (unsigned)(a.N + 1)), block,
+                         0, stream, b);
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhLqChk, SQRT>), grid, block, 0, stream, b);
+      ProblemArgsT<real> r = b;
+      r.lq_redo = 1;
+      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT, LQ>), grid, block, 0, stream, r);
     }
     if (compact) {  // RB(it) has counted its live workgroups: compact for the rest of the solve?
       hipLaunchKernelGGL(compact_decide_kernel, dim3(1), dim3(64), 0, stream, a.ctl, it, a.qp_buf, a.batch);
@@ -2091,9 +2217,13 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
   return hipGetLastError();
 }
 
+// HPIPM's lq_fact (the C-ABI derives it from the mode, with ric_alg != 0 only)
 template <bool FULL, int GEN>
 static hipError_t launch_alg(const ProblemArgsT<real>& a, hipStream_t stream) {
-  return a.ric_alg ? launch_phases<FULL, GEN, true>(a, stream) : launch_phases<FULL, GEN, false>(a, stream);
+  if (!a.ric_alg) return launch_phases<FULL, GEN, false, 0>(a, stream);
+  if (a.lq_fact == 2) return launch_phases<FULL, GEN, true, 2>(a, stream);
+  if (a.lq_fact == 1) return launch_phases<FULL, GEN, true, 1>(a, stream);
+  return launch_phases<FULL, GEN, true, 0>(a, stream);
 }
 
 hipError_t launch(const ProblemArgsT<real>& a, hipStream_t stream) {

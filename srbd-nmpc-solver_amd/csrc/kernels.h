@@ -53,6 +53,11 @@ struct ProblemArgsT {
   // iterative refinement of the corrector step (HPIPM itref_corr_max; the C-ABI derives it
   // from settings.mode: Balance 2, Robust 4, else 0).
   int itref_corr_max;
+  // HPIPM's lq_fact (square-root Riccati only; the C-ABI derives it from settings.mode:
+  // Balance 1, Robust 2, else 0): 2 = every stage factorization by LQ, 1 = Cholesky until a
+  // predictor step's linear residual exceeds 1e-5, LQ from then on (ipm_box_impl.h).
+  // lq_redo: internal, set on the launch that redoes an iteration's RB -> F1 by LQ.
+  int lq_fact, lq_redo;
   // warm_start 2 only (internal: the fp64 continuation of srbd_qp_settings.f64_rescue):
   // per QP and stage the barrier state [kStLam block 96][nch chunks x 48], see ipm_box.hip
   const T* warm_bars;

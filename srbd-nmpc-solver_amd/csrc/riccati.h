@@ -409,6 +409,252 @@ __device__ __forceinline__ void riccati_step_sqrt(const T (&Lp)[12], T (&A_)[12]
   riccati_tail<MidAt, SYMP>(lane, o, mid, hstash);
 }
 
+// ---------------------------------------------------------------------------
+// HPIPM's LQ factorization of the stage (lq_fact, hpipm_d_ocp_qp_ipm.h:78; its
+// d_ocp_qp_fact_lq_solve_kkt_step, hpipm_d_ocp_qp_kkt.h:58, restated): the stage factor
+// L = [Lu 0; Lxu Lx] (24 x 24, [u; x] order) is updated by Householder reflections from the
+// right that absorb dense columns, L L' <- L L' + [Au; Ax][Au; Ax]', without ever forming
+// the product (the barrier Hessians of ~1e13 never meet the O(1) data in a sum).
+// Row-owned: lane j < 12 holds u-row j (Lu row j, entries 0..j) and x-row j (Lxu row j; Lx
+// row j, entries 0..j) of L and the two rows' entries of the 12 columns being absorbed.
+// One reflection per row i = 0..23 maps row i's entries (pivot, its 12 column entries) to
+// (||.||, 0, ..., 0) with a positive diagonal (LAPACK dlarfgp's choice, BLASFEO dgelqf_pd);
+// the pivot row is broadcast to the group, every row below it updated.  Lanes 12..15 hold
+// zeros throughout.
+template <typename T>
+struct LqRows {
+  T Lu[12], Lxu[12], Lx[12];
+};
+
+// reflection data of a pivot row held by lane I: alpha = its diagonal, sigma = its squared
+// column entries; returns false when the row has nothing to absorb (a negative diagonal is
+// then flipped by the caller, as dlarfgp returns beta >= 0)
+template <int I, typename T>
+__device__ __forceinline__ bool lq_reflector(T al_own, T sig_own, T& nrm, T& v0, T& inv) {
+  const T al = bc<I>(al_own), sig = bc<I>(sig_own);
+  if (!(sig > T(0))) {
+    nrm = al;
+    return false;
+  }
+  nrm = __builtin_sqrt(al * al + sig);
+  v0 = al <= T(0) ? al - nrm : -sig / (al + nrm);
+  inv = T(2) / (v0 * v0 + sig);
+  return true;
+}
+
+template <typename T>
+__device__ __forceinline__ void lq_absorb(LqRows<T>& L, T (&Au)[12], T (&Ax)[12], const int lane) {
+  // ---- u rows (pivot row I on lane I, column I) ----
+  sfor<0, 12>([&](auto ii) {
+    constexpr int I = decltype(ii)::value;
+    T sig = T(0);
+    sfor<0, 12>([&](auto c) { sig = fmadd(Au[decltype(c)::value], Au[decltype(c)::value], sig); });
+    T nrm, v0, inv;
+    if (lq_reflector<I>(L.Lu[I], sig, nrm, v0, inv)) {
+      T vb[12];
+      sfor<0, 12>([&](auto c) { vb[decltype(c)::value] = bc<I>(Au[decltype(c)::value]); });
+      T du = L.Lu[I] * v0, dx = L.Lxu[I] * v0;
+      sfor<0, 12>([&](auto c) {
+        constexpr int C = decltype(c)::value;
+        du = fmadd(Au[C], vb[C], du);
+        dx = fmadd(Ax[C], vb[C], dx);
+      });
+      const T fu = lane > I ? du * inv : T(0);  // u rows below the pivot
+      const T fx = dx * inv;                    // every x row
+      L.Lu[I] = fmadd(-fu, v0, L.Lu[I]);
+      L.Lxu[I] = fmadd(-fx, v0, L.Lxu[I]);
+      sfor<0, 12>([&](auto c) {
+        constexpr int C = decltype(c)::value;
+        Au[C] = fmadd(-fu, vb[C], Au[C]);
+        Ax[C] = fmadd(-fx, vb[C], Ax[C]);
+      });
+      if (lane == I) {
+        L.Lu[I] = nrm;
+        sfor<0, 12>([&](auto c) { Au[decltype(c)::value] = T(0); });
+      }
+    } else if (nrm < T(0)) {  // nothing to absorb, negative diagonal: flip column I
+      if (lane >= I) L.Lu[I] = -L.Lu[I];
+      L.Lxu[I] = -L.Lxu[I];
+    }
+    SRBD_PHASE_FENCE();
+  });
+  // ---- x rows (pivot row 12 + I on lane I, column 12 + I; the u rows are done) ----
+  sfor<0, 12>([&](auto ii) {
+    constexpr int I = decltype(ii)::value;
+    T sig = T(0);
+    sfor<0, 12>([&](auto c) { sig = fmadd(Ax[decltype(c)::value], Ax[decltype(c)::value], sig); });
+    T nrm, v0, inv;
+    if (lq_reflector<I>(L.Lx[I], sig, nrm, v0, inv)) {
+      T vb[12];
+      sfor<0, 12>([&](auto c) { vb[decltype(c)::value] = bc<I>(Ax[decltype(c)::value]); });
+      T dx = L.Lx[I] * v0;
+      sfor<0, 12>([&](auto c) { dx = fmadd(Ax[decltype(c)::value], vb[decltype(c)::value], dx); });
+      const T fx = lane > I ? dx * inv : T(0);
+      L.Lx[I] = fmadd(-fx, v0, L.Lx[I]);
+      sfor<0, 12>([&](auto c) { Ax[decltype(c)::value] = fmadd(-fx, vb[decltype(c)::value], Ax[decltype(c)::value]); });
+      if (lane == I) {
+        L.Lx[I] = nrm;
+        sfor<0, 12>([&](auto c) { Ax[decltype(c)::value] = T(0); });
+      }
+    } else if (nrm < T(0)) {
+      if (lane >= I) L.Lx[I] = -L.Lx[I];
+    }
+    SRBD_PHASE_FENCE();
+  });
+}
+
+// Transpose of a 12 x 12 block between row- and column-owned through the group's LDS block
+// `blk` (144 reals): lane j's v (a row or a column) in, lane j's transposed vector out.
+// `keep` masks the result to entries I >= lane (lower: column-owned from row-owned) or I <=
+// lane (rows from a column-owned lower factor), 0 = full.
+template <typename T>
+__device__ __forceinline__ void group_transpose(T* blk, const int lane, T (&v)[12], int keep) {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  if (lane < 12) {
+    sfor<0, 6>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      blk[lane * 12 + 2 * I] = v[2 * I];
+      blk[lane * 12 + 2 * I + 1] = v[2 * I + 1];
+    });
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  const int r = lane < 12 ? lane : 0;
+  sfor<0, 12>([&](auto j) {
+    constexpr int J = decltype(j)::value;
+    const T x = blk[J * 12 + r];
+    const bool ok = lane < 12 && (keep > 0 ? J >= lane : keep < 0 ? J <= lane : true);
+    v[J] = ok ? x : T(0);
+  });
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// One backward step by LQ (lq_fact), ric_alg 1's recursion otherwise (riccati_step_sqrt):
+//   Lh = chol([R~ S'; S Q~])       R~ = R + box Gamma_u (+ reg on the pivots), Q~ = Q + box Gamma_x
+//   L  = LQ([Lh | [B'; A'] Lp | dense columns of `extra`])
+// `loadR` / `loadSQ` fill R~ and S, Q~ (VL: r~, q~) as for riccati_step_sqrt, without the dense
+// general-row terms; `extra(L, lane)` absorbs those (lq_absorb per 12-row chunk).  HPIPM keeps
+// the box Gamma as a diagonal block beside Lh ([L | L | A], dgelqf_pd_lla); here it is added to
+// the Hessian's diagonal before its Cholesky -- a diagonal addition, nothing can cancel -- and
+// only the dense terms (the cost-to-go [B'; A'] Lp and the general rows sqrt(Gamma) [D'; C'])
+// are absorbed by reflections.  On exit o holds Lu (o.Lc, o.rs), K | k (o.Kc), Y (o.H) and, on VL,
+// p_k (o.F); Lp holds the next factor Lx (column-owned, zeros above the diagonal) and on VL
+// s_k = Lx^-1 p_k.  `blk`: the group's 144-real LDS block (free here).
+template <typename T, typename LoadR, typename LoadSQ, typename Extra>
+__device__ __forceinline__ void riccati_step_lq(T (&Lp)[12], T (&A_)[12], T (&B_)[12], LoadR&& loadR,
+                                                LoadSQ&& loadSQ, const int lane, const T reg,
+                                                StageFactor<T>& o, T* blk, Extra&& extra) {
+  const bool isv = lane == kVecLane, own = lane < kMaxDim;
+  // ---- MB = Lp'B, MA = Lp'[A | b] + [0 | s] (VL: m), as riccati_step_sqrt
+  T MB[12], MA[12];
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    MB[I] = T(0);
+    MA[I] = isv ? Lp[I] : T(0);
+  });
+  tmul_acc(Lp, B_, MB);
+  tmul_acc(Lp, A_, MA);
+  SRBD_PHASE_FENCE();
+  // ---- vectors on the element owners: g_i = (MB'm)_i, f_i = (MA'm)_i (m on VL)
+  T gi = T(0), fi = T(0);
+  sfor<0, 12>([&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    const T mk = bc<kVecLane>(MA[K]);
+    gi = fmadd(MB[K], mk, gi);
+    fi = fmadd(MA[K], mk, fi);
+  });
+  SRBD_PHASE_FENCE();
+  // ---- Lh: Lu_h = chol(R~), Y_h = Lu_h^-1 S, Lx_h = chol(Q~ - Y_h'Y_h)
+  LqRows<T> L;
+  T Sc[12], Qc[12], rs_h;
+  {
+    T G[12];
+    loadR(G);
+    chol_cols(G, lane, reg, L.Lu, rs_h);
+  }
+  loadSQ(Sc, Qc);  // (VL: r~, q~)
+  // g_i = r~_i + (MB'm)_i, f_i = q~_i + (MA'm)_i on their element owners
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    const T r = bc<kVecLane>(Sc[I]), q = bc<kVecLane>(Qc[I]);
+    if (lane == I) {
+      gi += r;
+      fi += q;
+    }
+  });
+  trsv_lower(L.Lu, rs_h, Sc);  // lane l: Y_h[:, l] = row l of Lxu_h
+  {
+    T Yn[12];
+    sfor<0, 12>([&](auto i) { Yn[decltype(i)::value] = -Sc[decltype(i)::value]; });
+    tmul_acc(Sc, Yn, Qc);
+  }
+  T rs_x;
+  chol_cols(Qc, lane, T(0), L.Lx, rs_x);
+  sfor<0, 12>([&](auto i) { L.Lxu[decltype(i)::value] = own ? Sc[decltype(i)::value] : T(0); });
+  SRBD_PHASE_FENCE();
+  // column-owned lower factors (rows >= l meaningful) -> rows
+  group_transpose(blk, lane, L.Lu, -1);
+  group_transpose(blk, lane, L.Lx, -1);
+  // ---- absorb [B'; A'] Lp (u row j: MB[:, j], x row j: MA[:, j]) and the dense rows
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    if (!own) {
+      MB[I] = T(0);
+      MA[I] = T(0);
+    }
+  });
+  lq_absorb(L, MB, MA, lane);
+  extra(L, lane);
+  SRBD_PHASE_FENCE();
+  // ---- back to column-owned: Lu -> o.Lc, o.rs; Lx -> Lp (next stage); Y = Lxu rows
+  group_transpose(blk, lane, L.Lu, 1);
+  group_transpose(blk, lane, L.Lx, 1);
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    o.Lc[I] = L.Lu[I];
+  });
+  T du = T(0), dxx = T(0);
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    if (lane == I) {
+      du = L.Lu[I];
+      dxx = L.Lx[I];
+    }
+  });
+  o.rs = du > T(0) ? T(1) / du : T(0);
+  const T rsx = dxx > T(0) ? T(1) / dxx : T(0);
+  // ---- the vectors: y = Lu^-1 g, k = -Lu^-T y, p_k = f - Y'y, s_k = Lx^-1 p_k
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    const T g = bc<I>(gi), f = bc<I>(fi);
+    o.H[I] = isv ? g : T(0);
+    o.F[I] = isv ? f : T(0);
+  });
+  trsv_lower(o.Lc, o.rs, o.H);
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    if (own) o.H[I] = L.Lxu[I];
+  });
+  trsv_upper_t_neg_axpy(o.Lc, o.rs, o.H, o.Kc);
+  {
+    T Hn[12];
+    sfor<0, 12>([&](auto i) { Hn[decltype(i)::value] = -o.H[decltype(i)::value]; });
+    tmul_acc(o.H, Hn, o.F);
+  }
+  SRBD_PHASE_FENCE();
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    Lp[I] = isv ? o.F[I] : L.Lx[I];
+  });
+  trsv_lower(L.Lx, rsx, Lp);  // VL: s_k = Lx^-1 p_k (the matrix lanes' results are discarded)
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    if (!isv) Lp[I] = L.Lx[I];
+  });
+}
+
 // P (lane l: column l of P_k; VL: p_k) -> its square-root form for the next
 // riccati_step_sqrt: Lp = chol(P) (column l, zeros above the diagonal) and, on VL,
 // s = Lp^-1 p (the border column of the same elimination).  A non-positive pivot

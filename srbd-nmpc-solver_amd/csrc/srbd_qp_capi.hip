@@ -126,6 +126,7 @@ void srbd_qp_default_settings(srbd_qp_settings* s) {
   s->compute_residuals = 1;  // HPIPM's comp_res_exit
   s->f64_rescue = 0;
   s->f32_iters = 0;
+  s->lq_fact = -1;
 }
 
 int srbd_qp_check_settings(const srbd_qp_settings* s) {
@@ -143,6 +144,8 @@ int srbd_qp_check_settings(const srbd_qp_settings* s) {
   // extensions (srbd_qp.h)
   if (s->f64_rescue < 0) return fail(SRBD_QP_ESETTINGS, "srbd_qp_settings.f64_rescue must be non-negative");
   if (s->f32_iters < 0) return fail(SRBD_QP_ESETTINGS, "srbd_qp_settings.f32_iters must be non-negative");
+  if (s->lq_fact < -1 || s->lq_fact > 2)
+    return fail(SRBD_QP_ESETTINGS, "srbd_qp_settings.lq_fact must be -1 (the mode's), 0, 1 or 2");
   return SRBD_QP_OK;
 }
 
@@ -351,6 +354,10 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   // HPIPM's mode-dependent iterative refinement of the corrector (d_ocp_qp_ipm_arg_set_default:
   // itref_corr_max 2 in Balance, 4 in Robust, 0 in Speed / SpeedAbs)
   a.itref_corr_max = st->mode == 2 ? 2 : st->mode == 3 ? 4 : 0;
+  // and its lq_fact: 1 in Balance, 2 in Robust, with the square-root Riccati only
+  // ("for square_root_alg==1", hpipm_d_ocp_qp_ipm.h:78)
+  a.lq_fact = !st->ric_alg ? 0 : st->lq_fact >= 0 ? st->lq_fact : st->mode == 2 ? 1 : st->mode == 3 ? 2 : 0;
+  a.lq_redo = 0;
   a.warm_start = st->warm_start;
   a.alpha_min = st->alpha_min;
   a.mu0 = st->mu0;

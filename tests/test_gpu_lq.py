@@ -1,0 +1,131 @@
+"""GPU parity of HPIPM's lq_fact (hpipm_d_ocp_qp_ipm.h:78; d_ocp_qp_fact_lq_solve_kkt_step,
+hpipm_d_ocp_qp_kkt.h:58) in the batched IPM: riccati.h riccati_step_lq, ipm_box_impl.h LQ.
+
+With the square-root Riccati, HPIPM's Balance mode sets lq_fact 1 (Cholesky until a
+predictor step's linear residual exceeds 1e-5, then LQ for the rest of the solve) and Robust
+lq_fact 2 (every stage factorization by LQ: the dense barrier terms and the cost-to-go are
+absorbed as columns by Householder reflections, never summed into the Hessian).  The C-ABI
+derives it from the mode like HPIPM's d_ocp_qp_ipm_arg_set_default, or takes
+srbd_qp_settings.lq_fact (HPIPM's d_ocp_qp_ipm_arg_set "lq_fact").  The oracle restates the
+same factorization block by block (oracle/ocp_qp_oracle.c riccati_factor_lq); HPIPM itself is
+not vendored, so parity with HPIPM is unpinned beyond that restatement."""
+import numpy as np
+import pytest
+
+import helpers
+
+pytestmark = pytest.mark.gpu
+
+
+def _family(pkg, M=64):
+    """The near-degenerate endgame family of test_gpu_ipm.py::test_degenerate_endgame_family."""
+    qp, x0 = helpers.random_constrained(20, 12, 12, 4, 14, 200, pkg.OcpQpBatch)
+    rng = np.random.default_rng(7)
+    fields = {}
+    for name in ("Q", "R", "S", "A", "B", "q", "r", "b", "C", "D", "lg", "ug", "lbu", "ubu", "lbx",
+                 "ubx", "lg_mask", "ug_mask", "lbu_mask", "ubu_mask", "lbx_mask", "ubx_mask"):
+        a = getattr(qp, name, None)
+        if a is None:
+            continue
+        a = np.repeat(np.asarray(a)[12:13], M, axis=0)
+        if name in ("Q", "R", "S", "A", "B", "q", "r", "b"):
+            a = a * (1 + 1e-15 * rng.standard_normal(a.shape))
+        fields[name] = a
+    fam = pkg.OcpQpBatch(N=qp.N, nx=qp.nx, nu=qp.nu, ng=qp.ng, **fields)
+    return fam, np.repeat(np.asarray(x0)[12:13], M, axis=0)
+
+
+@pytest.mark.parametrize("ng", [0, 14])
+@pytest.mark.parametrize("dims", [(12, 12), (12, 4), (5, 3)])
+def test_lq_robust_vs_oracle(pkg, oracle, dims, ng):
+    """Robust with ric_alg 1 (lq_fact 2, 4 refinement steps): every QP converges in the
+    oracle's iterations +-1 with x, u within 1e-7 of its LQ solution, and the stat table's
+    lq_fact column (11) is 1 on every step.  Boxes on u and x, general rows with C and D."""
+    nx, nu = dims
+    qp, x0 = helpers.random_constrained(24, 15, nx, nu, ng, 31 + nx + ng, pkg.OcpQpBatch)
+    st = dict(iter_max=40, mode="Robust", ric_alg=1)
+    out = pkg.capi.solve(qp, x0, st, stats=True)
+    ref = oracle.solve(qp, st, x0=x0)
+    assert np.all(ref["status"] == 0) and np.all(ref["lq_iters"] == ref["iter"])
+    assert np.all(out["status"] == 0), (out["status"], out["res"])
+    assert np.all(np.abs(out["iter"] - ref["iter"]) <= 1), (out["iter"], ref["iter"])
+    for i in range(qp.batch):
+        it = int(out["iter"][i])
+        assert np.all(out["stat"][i, 1:it + 1, 11] == 1.0), i
+        for key in ("x", "u"):
+            assert helpers.is_approx(out[key][i], ref[key][i], 1e-7), (key, i)
+
+
+@pytest.mark.parametrize("constraints", ["box_u", "cone"])
+def test_lq_srbd_vs_oracle_and_cholesky(pkg, oracle, constraints):
+    """SRBD QPs (N = 20, BASELINE configs 3 and 5's problems in fp64) with lq_fact 2: the
+    oracle's LQ solution at 1e-7, and the Cholesky factorization's (lq_fact 0, same mode) at
+    the solve tolerance -- the two factorizations are one algorithm in exact arithmetic."""
+    qp, x0 = pkg.srbd_model.generate_batch(32, N=20, seed=808, constraints=constraints)
+    st = dict(iter_max=40, mode="Speed", ric_alg=1, tol_stat=1e-8, tol_eq=1e-8, tol_ineq=1e-8,
+              tol_comp=1e-8)
+    lq = pkg.capi.solve(qp, x0, dict(st, lq_fact=2), stats=True)
+    chol = pkg.capi.solve(qp, x0, dict(st, lq_fact=0), stats=True)
+    ref = oracle.solve(qp, dict(st, lq_fact=2), x0=x0)
+    assert np.all(lq["status"] == 0) and np.all(chol["status"] == 0) and np.all(ref["status"] == 0)
+    assert np.all(np.abs(lq["iter"] - ref["iter"]) <= 1), (lq["iter"], ref["iter"])
+    assert np.all(chol["stat"][:, :, 11] == 0)
+    for i in range(qp.batch):
+        for key in ("x", "u"):
+            assert helpers.is_approx(lq[key][i], ref[key][i], 1e-7), (key, i)
+            assert helpers.is_approx(lq[key][i], chol[key][i], 1e-5), (key, i)
+
+
+def test_lq_fact2_degenerate_family(pkg, oracle):
+    """The degenerate endgame family in Speed (no refinement): the Cholesky square root
+    converges on 48 of 64 copies (GPU and oracle); lq_fact 2, which never sums
+    the ~1e13 barrier Hessians with the data, converges on every copy, as the oracle's LQ does,
+    with x, u within 1e-6 of the oracle's."""
+    fam, xb = _family(pkg)
+    st = dict(iter_max=50, mode="Speed", ric_alg=1, lq_fact=2)
+    out = pkg.capi.solve(fam, xb, st)
+    ref = oracle.solve(fam, st, x0=xb)
+    assert np.all(ref["status"] == 0)
+    assert np.all(out["status"] == 0), (np.bincount(out["status"], minlength=4), out["res"][out["status"] != 0])
+    assert np.all(np.abs(out["iter"] - ref["iter"]) <= 1), (out["iter"], ref["iter"])
+    for i in range(fam.batch):
+        for key in ("x", "u"):
+            assert helpers.is_approx(out[key][i], ref[key][i], 1e-6), (key, i)
+
+
+def test_lq_fact1_switch(pkg, oracle):
+    """lq_fact 1 in Speed on the degenerate family: the switch to LQ follows the predictor
+    step's linear residual (> 1e-5: HPIPM's d_ocp_qp_ipm_solve test), redone by LQ from the same
+    iterate and kept for the rest of the solve.  The stat table marks the LQ iterations
+    (column 11: 0 before the switch, 1 from it on, never back), copies switch on the GPU as in
+    the oracle (counts within 8 of 64), and every copy that ends converged without switching
+    is the Cholesky solve's (lq_fact 0) bit for bit."""
+    fam, xb = _family(pkg)
+    st = dict(iter_max=50, mode="Speed", ric_alg=1)
+    out = pkg.capi.solve(fam, xb, dict(st, lq_fact=1), stats=True)
+    chol = pkg.capi.solve(fam, xb, dict(st, lq_fact=0))
+    ref = oracle.solve(fam, dict(st, lq_fact=1), x0=xb)
+    switched = np.zeros(fam.batch, dtype=bool)
+    for i in range(fam.batch):
+        col = out["stat"][i, 1:int(out["iter"][i]) + 1, 11]
+        assert np.all(np.diff(col) >= 0), (i, col)  # 0 ... 0 1 ... 1
+        switched[i] = col.size > 0 and col[-1] == 1.0
+    ref_sw = ref["lq_iters"] > 0
+    assert switched.sum() > 0 and ref_sw.sum() > 0
+    assert abs(int(switched.sum()) - int(ref_sw.sum())) <= 8, (switched.sum(), ref_sw.sum())
+    assert abs(int((out["status"] == 0).sum()) - int((ref["status"] == 0).sum())) <= 8
+    for i in np.nonzero(~switched)[0]:
+        for key in ("x", "u", "status", "iter"):
+            assert np.array_equal(out[key][i], chol[key][i]), (key, i)
+
+
+def test_lq_settings_validation_and_classical_ignores_it(pkg):
+    """srbd_qp_settings.lq_fact outside -1..2 is rejected; with the classical Riccati
+    (ric_alg 0) lq_fact is ignored (HPIPM: "for square_root_alg==1"): bit-identical outputs."""
+    qp, x0 = helpers.random_constrained(8, 10, 12, 12, 4, 3, pkg.OcpQpBatch)
+    a = pkg.capi.solve(qp, x0, dict(iter_max=30, ric_alg=0, lq_fact=0))
+    b = pkg.capi.solve(qp, x0, dict(iter_max=30, ric_alg=0, lq_fact=2))
+    for key in ("x", "u", "pi", "status", "iter"):
+        assert np.array_equal(a[key], b[key]), key
+    with pytest.raises(Exception):
+        pkg.capi.solve(qp, x0, dict(iter_max=30, ric_alg=1, lq_fact=3))
