@@ -457,8 +457,13 @@ __device__ __forceinline__ int group_qp(const ProblemArgsT<real>& a) {
   return slot_qp(a, (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4));
 }
 
-// LQ (ric_alg 1 only): HPIPM's lq_fact -- 0 Cholesky factorizations, 2 LQ (riccati.h
-// riccati_step_lq) in every RB, 1 per QP: Cholesky until the switch (kQsForceLq), then LQ.
+// LQ (ric_alg 1 only), HPIPM's lq_fact: the RB factorizations by Cholesky (0, 1) or by LQ
+// (riccati.h riccati_step_lq: 2, 3), of every QP (0, 2) or, for lq_fact 1's per-QP switch
+// (kQsForceLq), of the QPs not switched (1) / switched (3).  lq_fact 1 launches 1 and 3 one after
+// the other, so each instantiation keeps its own registers (one kernel with both paths spilled
+// 540 B/lane into the Cholesky path too).
+template <int LQ>
+constexpr bool kLqFactor = LQ >= 2;
 template <bool FULL, int GEN, int PH, bool SQRT = false, int LQ = 0>
 __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
   // the refinement check runs stage-parallel: group g on QP slot g / (N + 1), stage
@@ -922,9 +927,13 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     return;
   }
   if (status >= 0) return;  // this QP has exited
-  // the lq_fact 1 redo launch (RB -> F1 by LQ of the QPs whose check switched them)
-  if constexpr (PH == kPhRB || PH == kPhF1)
+  // lq_fact 1: RB -> F1 of the QPs this instantiation factorizes, and the redo launch (RB -> F1
+  // by LQ of the QPs whose check switched them)
+  if constexpr (PH == kPhRB || PH == kPhF1) {
+    if constexpr (LQ == 1 || LQ == 3)
+      if ((qs[kQsForceLq] != real(0.0)) != (LQ == 3)) return;
     if (a.lq_redo && qs[kQsLqRedo] == real(0.0)) return;
+  }
   const int par = iter & 1;  // record written by this iteration's factorization
   const real alpha_p = qs[kQsAlphaP], alpha_d = qs[kQsAlphaD], last_amin = qs[kQsLastAmin];
   if constexpr (PH == kPhRB) {
@@ -961,7 +970,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
     real P[12];
     // this QP's factorizations by LQ (HPIPM lq_fact): the general rows' sqrt(Gamma) [D'; C'] and
     // the cost-to-go are absorbed by reflections instead of summed into the Hessian
-    const bool use_lq = SQRT && (LQ == 2 || (LQ == 1 && qs[kQsForceLq] != real(0.0)));
+    constexpr bool use_lq = SQRT && kLqFactor<LQ>;
     const bool own = lane < kMaxDim;
     // stage ks's general-row columns sqrt(Gamma_r) [D_r'; C_r'], one 12-row chunk at a time
     auto absorb_rows = [&](int ks, LqRows<real>& L) {
@@ -1318,7 +1327,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         tstamp(22);
         StageFactor<real> f;
         if constexpr (SQRT) {
-          if (LQ != 0 && use_lq) {
+          if constexpr (use_lq) {
             auto loadR_lq = [&](real (&Rc)[12]) {
               greal Rg[12];
               loadR(Rg);
@@ -2082,7 +2091,7 @@ __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase_
   if constexpr (PH != kPhInit && PH != kPhOut)
     if (solve_done(a)) return;
   ipm_phase<FULL, GEN, PH, SQRT, LQ>(a);
-  if constexpr (PH == kPhRB) report_running(a);
+  if constexpr (PH == kPhRB && LQ != 3) report_running(a);  // (3: counted by the 1 launch)
 }
 
 // Two consecutive sweeps of one iteration in one launch (RB -> F1, B2 -> F2):
@@ -2096,8 +2105,8 @@ __global__ void __launch_bounds__(256, FULL ? kIpmMinBlocks<GEN> : 1) ipm_phase2
   ipm_phase<FULL, GEN, PH1, SQRT, LQ>(a);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   ipm_phase<FULL, GEN, PH2, SQRT, LQ>(a);
-  if constexpr (PH1 == kPhRB)
-    if (!a.lq_redo) report_running(a);  // (the lq_fact 1 redo repeats an RB already counted)
+  if constexpr (PH1 == kPhRB && LQ != 3)  // (lq_fact 1: the LQ launch's QPs are counted, as
+    if (!a.lq_redo) report_running(a);   // running, by the Cholesky launch before it)
 }
 
 // Active-QP compaction, decided on the device after the RB sweep of iteration `it`: when the
@@ -2171,25 +2180,30 @@ static hipError_t launch_phases(const ProblemArgsT<real>& a, hipStream_t stream)
   for (int it = 0;; ++it) {
     b.launch_it = it;
     if (it >= a.iter_max) {
-      if (!a.skip_last_rb)
+      if (!a.skip_last_rb) {
         hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT, LQ>), grid, block, 0, stream, b);
+        if constexpr (LQ == 1)  // (lq_fact 1: the switched QPs' RB by LQ)
+          hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT, 3>), grid, block, 0, stream, b);
+      }
       break;
     }
     if (kIpmSplit) {  // diagnostic schedule: one launch per sweep
       hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhRB, SQRT, LQ>), grid, block, 0, stream, b);
-      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF1, SQRT>), grid, block, 0, stream, b);
+      hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhF1, SQRT, LQ>), grid, block, 0, stream, b);
     } else {
       hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT, LQ>), grid, block, 0, stream, b);
     }
     if constexpr (LQ == 1) {
-      // HPIPM lq_fact 1: the predictor step's linear residual (stage-parallel, IR's arithmetic),
-      // the switch, and RB -> F1 again by LQ for the QPs it switched (from the same iterate)
+      // HPIPM lq_fact 1: RB -> F1 by LQ of the QPs switched in an earlier iteration, then the
+      // predictor step's linear residual of the others (stage-parallel, IR's arithmetic), the
+      // switch, and RB -> F1 again by LQ for the QPs it switched (from the same iterate)
+      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT, 3>), grid, block, 0, stream, b);
       hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhIRP, SQRT>), dim3(grid.x * (unsigned)(a.N + 1)), block,
                          0, stream, b);
       hipLaunchKernelGGL((ipm_phase_kernel<FULL, GEN, kPhLqChk, SQRT>), grid, block, 0, stream, b);
       ProblemArgsT<real> r = b;
       r.lq_redo = 1;
-      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT, LQ>), grid, block, 0, stream, r);
+      hipLaunchKernelGGL((ipm_phase2_kernel<FULL, GEN, kPhRB, kPhF1, SQRT, 3>), grid, block, 0, stream, r);
     }
     if (compact) {  // RB(it) has counted its live workgroups: compact for the rest of the solve?
       hipLaunchKernelGGL(compact_decide_kernel, dim3(1), dim3(64), 0, stream, a.ctl, it, a.qp_buf, a.batch);
