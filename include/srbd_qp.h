@@ -382,6 +382,11 @@ srbd_qp_handle srbd_qp_multi_handle(srbd_qp_multi m, int i);
 int srbd_qp_multi_solve_f64(srbd_qp_multi m, const int* batch, const srbd_qp_settings* settings,
                             const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol,
                             double* root_x, double* root_u, double* root_pi);
+/* The fp32 twin (BASELINE config 5 sharded; HPIPM's s_ocp_qp_ipm), the same
+ * contract with srbd_qp_solve_f32 on every shard.  (ABI 11)                   */
+int srbd_qp_multi_solve_f32(srbd_qp_multi m, const int* batch, const srbd_qp_settings* settings,
+                            const srbd_qp_data_f32* data, const srbd_qp_solution_f32* sol,
+                            float* root_x, float* root_u, float* root_pi);
 
 /* Blocks until all work queued on the handle's stream is done.            */
 int srbd_qp_synchronize(srbd_qp_handle h);

@@ -3,7 +3,8 @@
 # separate FETCH_SIZE / WRITE_SIZE passes of the default workload and the two IPM configs,
 # summarised (scripts/pmc_summary.py -> profiles/TAG/ and profiles/pmc_traffic.json on the
 # box), then the default bench line itself, which reads that fresh traffic summary.
-# Everything is written under gpurun_out/TAG/ (merged back; copy into profiles/ after).
+# Everything is written under gpurun_out/TAG/ (merged back); scripts/collect_round.sh TAG then
+# copies it into profiles/TAG/ and profiles/pmc_traffic.json.
 # Usage: profile_round.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp

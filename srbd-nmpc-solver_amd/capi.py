@@ -123,6 +123,11 @@ def lib():
                                                   C.POINTER(Data), C.POINTER(Solution), C.c_void_p,
                                                   C.c_void_p, C.c_void_p]
             L.srbd_qp_multi_solve_f64.restype = C.c_int
+        if hasattr(L, "srbd_qp_multi_solve_f32"):  # ABI 11
+            L.srbd_qp_multi_solve_f32.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(Settings),
+                                                  C.POINTER(Data32), C.POINTER(Solution32), C.c_void_p,
+                                                  C.c_void_p, C.c_void_p]
+            L.srbd_qp_multi_solve_f32.restype = C.c_int
         if hasattr(L, "srbd_qp_host_staging_f64"):  # ABI 10 (older builds: A/B runs)
             L.srbd_qp_host_staging_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
                                                    C.POINTER(Data), C.POINTER(Solution)]
@@ -292,13 +297,16 @@ class Multi:
         self._m = m
 
     def solve(self, batches, settings: Settings, datas, sols, root_x=None, root_u=None, root_pi=None):
+        """fp64 shards (Data / Solution), or fp32 ones (Data32 / Solution32: srbd_qp_multi_solve_f32)."""
         n = len(self.devices)
         b = (C.c_int * n)(*[int(x) for x in batches])
-        d = (Data * n)(*datas)
-        s = (Solution * n)(*sols)
+        f32 = isinstance(datas[0], Data32)
+        d = ((Data32 if f32 else Data) * n)(*datas)
+        s = ((Solution32 if f32 else Solution) * n)(*sols)
         ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
-        check(lib().srbd_qp_multi_solve_f64(self._m, b, C.byref(settings), d, s, ptr(root_x), ptr(root_u),
-                                            ptr(root_pi)), "srbd_qp_multi_solve_f64")
+        fn = "srbd_qp_multi_solve_f32" if f32 else "srbd_qp_multi_solve_f64"
+        check(getattr(lib(), fn)(self._m, b, C.byref(settings), d, s, ptr(root_x), ptr(root_u),
+                                 ptr(root_pi)), fn)
 
     def close(self) -> None:
         if getattr(self, "_m", None):

@@ -73,15 +73,28 @@ srbd_qp_handle srbd_qp_multi_handle(srbd_qp_multi m, int i) {
   return m && i >= 0 && i < (int)m->h.size() ? m->h[i] : nullptr;
 }
 
-int srbd_qp_multi_solve_f64(srbd_qp_multi m, const int* batch, const srbd_qp_settings* settings,
-                            const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol, double* root_x,
-                            double* root_u, double* root_pi) {
+}  // extern "C"
+
+namespace {
+// srbd_qp_solve_f64 / _f32 by the precision's structs
+int solve_one(srbd_qp_handle h, int b, const srbd_qp_settings* st, const srbd_qp_data_f64* d,
+              const srbd_qp_solution_f64* s) {
+  return srbd_qp_solve_f64(h, b, st, d, s, nullptr);
+}
+int solve_one(srbd_qp_handle h, int b, const srbd_qp_settings* st, const srbd_qp_data_f32* d,
+              const srbd_qp_solution_f32* s) {
+  return srbd_qp_solve_f32(h, b, st, d, s, nullptr);
+}
+
+template <typename T, typename Data, typename Sol>
+int multi_solve(srbd_qp_multi m, const int* batch, const srbd_qp_settings* settings, const Data* data,
+                const Sol* sol, T* root_x, T* root_u, T* root_pi) {
   if (!m || !batch || !data || !sol) return srbd::set_error(SRBD_QP_EINVAL, "multi: NULL argument");
   const int n = (int)m->h.size();
   const size_t N = (size_t)m->dims.N, nx = (size_t)m->dims.nx, nu = (size_t)m->dims.nu;
   // every shard's launch sequence first: the devices run concurrently
   for (int i = 0; i < n; ++i) {
-    const int rc = srbd_qp_solve_f64(m->h[i], batch[i], settings, &data[i], &sol[i], nullptr);
+    const int rc = solve_one(m->h[i], batch[i], settings, &data[i], &sol[i]);
     if (rc) {
       for (int j = 0; j < i; ++j) srbd_qp_synchronize(m->h[j]);
       return rc;
@@ -96,9 +109,9 @@ int srbd_qp_multi_solve_f64(srbd_qp_multi m, const int* batch, const srbd_qp_set
     const size_t b = (size_t)batch[i];
     hipSetDevice(m->dev[i]);
     hipStream_t s = reinterpret_cast<hipStream_t>(srbd_qp_stream(m->h[i]));
-    auto copy = [&](double* dst, const double* src, size_t per_qp) {
+    auto copy = [&](T* dst, const T* src, size_t per_qp) {
       if (e != hipSuccess || !dst || !src || !b) return;
-      e = hipMemcpyPeerAsync(dst + row * per_qp, m->dev[0], src, m->dev[i], b * per_qp * sizeof(double), s);
+      e = hipMemcpyPeerAsync(dst + row * per_qp, m->dev[0], src, m->dev[i], b * per_qp * sizeof(T), s);
     };
     copy(root_x, sol[i].x, (N + 1) * nx);
     copy(root_u, sol[i].u, N * nu);
@@ -113,6 +126,21 @@ int srbd_qp_multi_solve_f64(srbd_qp_multi m, const int* batch, const srbd_qp_set
   }
   if (e != hipSuccess) return srbd::set_error(SRBD_QP_EDEVICE, std::string("multi gather: ") + hipGetErrorString(e));
   return rc;
+}
+}  // namespace
+
+extern "C" {
+
+int srbd_qp_multi_solve_f64(srbd_qp_multi m, const int* batch, const srbd_qp_settings* settings,
+                            const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol, double* root_x,
+                            double* root_u, double* root_pi) {
+  return multi_solve<double>(m, batch, settings, data, sol, root_x, root_u, root_pi);
+}
+
+int srbd_qp_multi_solve_f32(srbd_qp_multi m, const int* batch, const srbd_qp_settings* settings,
+                            const srbd_qp_data_f32* data, const srbd_qp_solution_f32* sol, float* root_x,
+                            float* root_u, float* root_pi) {
+  return multi_solve<float>(m, batch, settings, data, sol, root_x, root_u, root_pi);
 }
 
 }  // extern "C"

@@ -104,3 +104,33 @@ def test_multi_device_shards_and_gather(pkg):
     for (lo, hi), (_, st) in zip(shards, keep):
         np.testing.assert_array_equal(st["status"].cpu().numpy(), ref["status"][lo:hi])
     m.close()
+
+
+def test_multi_device_fp32_shards(pkg):
+    """srbd_qp_multi_solve_f32 (ABI 11): config 5's fp32 friction-cone problem in two shards
+    (both on device 0 here) -- every QP's x, u, pi gathered in shard order equals the
+    single-handle fp32 solve of the whole batch bit for bit, status included."""
+    import torch
+    capi = pkg.capi
+    qp, x0 = pkg.srbd_model.generate_batch(96, N=20, seed=62, constraints="cone")
+    st_d = dict(iter_max=30, tol_stat=1e-2, tol_eq=1e-3, tol_ineq=1e-3, tol_comp=1e-3, split_step=1)
+    ref = capi.solve(qp, x0, st_d, dtype=np.float32)
+    s = capi.settings_struct(st_d)
+    shards = [(0, 40), (40, 96)]
+    m = capi.Multi(20, 12, 12, [0, 0], ng=qp.ng, has_box_u=qp.has_box_u, has_box_x=qp.has_box_x, capacity=56)
+    keep, datas, sols = [], [], []
+    for lo, hi in shards:
+        dt, st, data, sol = capi.device_buffers(qp.subset(slice(lo, hi)), x0[lo:hi], "cuda:0",
+                                                dtype=np.float32)
+        keep.append((dt, st))
+        datas.append(data)
+        sols.append(sol)
+    f = dict(dtype=torch.float32, device="cuda:0")
+    rx, ru, rpi = torch.zeros(96, 21, 12, **f), torch.zeros(96, 20, 12, **f), torch.zeros(96, 21, 12, **f)
+    torch.cuda.synchronize()
+    m.solve([hi - lo for lo, hi in shards], s, datas, sols, rx, ru, rpi)
+    for key, t in (("x", rx), ("u", ru), ("pi", rpi)):
+        np.testing.assert_array_equal(t.cpu().numpy(), ref[key])
+    for (lo, hi), (_, st) in zip(shards, keep):
+        np.testing.assert_array_equal(st["status"].cpu().numpy(), ref["status"][lo:hi])
+    m.close()
