@@ -5,7 +5,7 @@ ARCH ?= gfx950
 PKG := srbd-nmpc-solver_amd
 CSRC := $(PKG)/csrc
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-unused-result -Wno-unused-value
-HIP_SRCS := $(CSRC)/riccati_unconstr.hip $(CSRC)/ipm_box.hip $(CSRC)/srbd_linearize.hip $(CSRC)/pad.hip $(CSRC)/rescue.hip $(CSRC)/srbd_qp_capi.hip $(CSRC)/multi.hip
+HIP_SRCS := $(CSRC)/riccati_unconstr.hip $(CSRC)/ipm_box.hip $(CSRC)/ipm_latency.hip $(CSRC)/srbd_linearize.hip $(CSRC)/pad.hip $(CSRC)/rescue.hip $(CSRC)/srbd_qp_capi.hip $(CSRC)/multi.hip
 HIP_HDRS := $(wildcard $(CSRC)/*.h) include/srbd_qp.h
 LIB := $(PKG)/libsrbd_qp.so
 OBJDIR := build/obj

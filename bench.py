@@ -424,6 +424,8 @@ def main():
         secondary["nmpc_step_config1"] = nmpc_config1(pkg, capi, device, args.seed,
                                                       with_cpu=not args.no_cpu_baseline)
         secondary["unconstr_n20_full_outputs"] = full_outputs_line(pkg, capi, device, args.seed)
+        secondary["ipm_small_batch"] = ipm_small_batch(pkg, capi, device, args.seed,
+                                                       with_cpu=not args.no_cpu_baseline)
 
     traffic = pmc_traffic(args.workload, batch)
     line = {
@@ -575,6 +577,49 @@ def secondary_workload(pkg, capi, name, device, seed, steps=3, warmup=1, rescue=
     log(f"[secondary] {name}: kernel {kernel_ms:.2f} ms, {out['value']:.4g} QP/s, "
         f"success {out['success_rate']:.3f}, iters {it:.2f}")
     del h
+    torch.cuda.empty_cache()
+    return out
+
+
+def ipm_small_batch(pkg, capi, device, seed, N=20, reps=20, with_cpu=True):
+    """Small-batch IPM latency: box-u (config 3's QP) at batch 1 / 16 / 256 and the friction
+    cone (config 5's QP, fp64) at batch 1, the NMPC settings, device buffers, one C-ABI call per
+    solve, wall time per call (median).  Up to 512 QPs these run on the one-launch latency IPM
+    (ipm_latency.hip); beside batch 1 box-u, the oracle's solve of the same QP on one host core."""
+    import torch
+    st = capi.settings_struct(NMPC_SETTINGS)
+    out = {"what": "wall ms per srbd_qp_solve_f64 call (launch + solve + sync), device buffers, "
+                   "NMPC settings; ipm_latency.hip up to 512 QPs", "N": N, "cases": {}}
+    for cons, batches in (("box_u", (1, 16, 256)), ("cone", (1,))):
+        for b in batches:
+            qp, x0 = pkg.srbd_model.generate_batch(b, N=N, seed=seed + 17, constraints=cons)
+            h = capi.Handle(N, 12, 12, qp.ng, qp.has_box_u, qp.has_box_x, capacity=b,
+                            device=device.index or 0)
+            _, stt, data, sol = capi.device_buffers(qp, x0, str(device))
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(reps + 2):
+                t0 = time.perf_counter()
+                h.solve_device(b, st, data, sol)
+                h.synchronize()
+                ts.append(time.perf_counter() - t0)
+            it = stt["iter"].cpu().numpy()
+            out["cases"][f"{cons}_batch{b}"] = {
+                "median_ms": float(np.median(ts[2:])) * 1e3, "min_ms": float(np.min(ts[2:])) * 1e3,
+                "iters_mean": float(it.mean()), "success_rate": float((stt["status"].cpu().numpy() == 0).mean())}
+            if with_cpu and cons == "box_u" and b == 1:
+                sys.path.insert(0, str(REPO / "oracle"))
+                import oracle  # test infrastructure: CPU baseline leg only
+                ts = []
+                for _ in range(5):
+                    t0 = time.perf_counter()
+                    oracle.solve(qp, settings_dict(st), x0=x0, riccati=False)
+                    ts.append(time.perf_counter() - t0)
+                out["cpu_box_u_batch1"] = {"median_ms": float(np.median(ts)) * 1e3, "cores": 1, "kind": "port",
+                                           "sample": "the same QP, oracle/ocp_qp_oracle.c through ctypes"}
+            h.close()
+    c = out["cases"]
+    log("[secondary] ipm small batch: " + ", ".join(f"{k} {v['median_ms']:.3f} ms" for k, v in c.items()))
     torch.cuda.empty_cache()
     return out
 

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Small-batch IPM latency: box-u SRBD QPs, N = 20, the NMPC's
-settings (iter_max 30), batches 1 / 16 / 256, one C-ABI call per solve on device
+settings (iter_max 30), batches 1 / 16 / 256 / 512 / 1024, one C-ABI call per solve on device
 buffers; prints one JSON line {batch: {median_ms, min_ms, iters_max, iters_mean}}.
-SRBD_QP_LIB selects the library (A/B against an older build)."""
+SRBD_QP_LIB selects the library (A/B against an older build); SRBD_IPM_LATENCY_MAX=0 in the
+environment keeps every batch on the batched kernels (ipm_latency.hip is the default up to 512).
+Usage: ipm_small_batch.py [reps] [constraints]"""
 import importlib.util
 import json
 import sys
@@ -22,10 +24,11 @@ def main():
     import torch
     capi = pkg.capi
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+    cons = sys.argv[2] if len(sys.argv) > 2 else "box_u"
     out = {}
-    for batch in (1, 16, 256):
-        qp, x0 = pkg.srbd_model.generate_batch(batch, N=20, seed=11, constraints="box_u")
-        h = capi.Handle(20, 12, 12, 0, True, False, capacity=batch)
+    for batch in (1, 16, 256, 512, 1024):
+        qp, x0 = pkg.srbd_model.generate_batch(batch, N=20, seed=11, constraints=cons)
+        h = capi.Handle(20, 12, 12, qp.ng, qp.has_box_u, qp.has_box_x, capacity=batch)
         s = capi.settings_struct(bench.NMPC_SETTINGS)
         dt, st, data, sol = capi.device_buffers(qp, x0)
         torch.cuda.synchronize()

@@ -31,6 +31,8 @@
 // lane-local and the barrier Hessian only touches the diagonals of R and Q.
 // General rows (D u + C x, ng <= 64) go in 12-row chunks, lane i = row i.
 #include "kernels.h"
+
+#include <cstdlib>
 #include "riccati.h"
 
 #define SRBD_REAL double
@@ -156,8 +158,17 @@ hipError_t launch_gather_warm_bars(const float* ws32, size_t ws_qp, int N, int n
   return hipGetLastError();
 }
 
+// Small fp64 batches of the classical-Riccati Speed solve go to the one-launch latency IPM
+// (ipm_latency.hip); SRBD_IPM_LATENCY_MAX (QPs, default kIpmLatencyMaxBatch, 0 = off) moves the
+// switch point (read at every launch, so a test can run one problem through both paths).
+int ipm_latency_max_batch() {
+  const char* e = std::getenv("SRBD_IPM_LATENCY_MAX");
+  return e ? std::atoi(e) : kIpmLatencyMaxBatch;
+}
+
 template <>
 hipError_t launch_ipm_box<double>(const ProblemArgsT<double>& a, hipStream_t stream) {
+  if (ipm_latency_ok(a, ipm_latency_max_batch())) return launch_ipm_latency(a, stream);
   return ipm_f64::launch(a, stream);
 }
 template <>

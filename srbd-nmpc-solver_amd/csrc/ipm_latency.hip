@@ -1,0 +1,1354 @@
+// ipm_latency.hip -- the box / general-constraint IPM for small batches: one workgroup per QP,
+// the whole solve (init, every iteration, outputs) in one launch, the serial recursions on
+// fp64 matrix cores.
+//
+// Same algorithm as the batched IPM (ipm_box_impl.h) and the oracle (oracle/ocp_qp_oracle.c
+// oracle_solve): HPIPM's d_ocp_qp_ipm_solve (hpipm_d_ocp_qp_ipm.h:238) in the classical
+// Riccati form (ric_alg 0, NMPC_solver.cpp:81), Mehrotra predictor-corrector, no iterative
+// refinement (Speed / SpeedAbs: itref_corr_max 0).  Another summation order: results agree
+// with the batched kernels' and the oracle's to rounding, not bit for bit.
+//
+// Why a separate kernel.  In the batched kernels a QP is one 16-lane group that walks its
+// stages serially in every phase; for a lone QP that is a chain of 12-wide DPP products
+// (RB -> F1 ~10.5 us per stage, B2 -> F2 ~4.2 us: DESIGN.md 4.9), ~2.8 ms for a box-u N = 20
+// solve.  Here only what is recursive in the stage index stays serial:
+//   * the factorization (backward, one stage after another) on matrix cores exactly like the
+//     unconstrained single-QP kernel (riccati_latency_impl.h: wave 0 the Riccati products and
+//     the Cholesky, wave 1 one stage behind with K, the record and the closed loop Acl),
+//     with the predictor's right-hand side as the tiles' 13th column;
+//   * the corrector's backward vector recursion, reduced to one matrix-vector product per
+//     stage, p_k = Acl_k' p_k+1 + c_k with c_k = g~x + K'g~u + Acl_k' P_k+1 b~_k formed
+//     for every stage at once beforehand;
+//   * the forward recursions dx_k+1 = Acl_k dx_k + bcl_k (one product per stage).
+// Everything else -- residuals, barrier terms, the Hessian updates, du = K dx + k, dpi, the
+// step lengths and the update -- runs with one 16-lane group per stage, all stages at once.
+//
+// Memory: the iterate, the barrier state, the steps and the closed-loop rows in LDS; the
+// barrier-augmented stage blocks (R~, S~, Q~, r~, q~, b~) and the factorization record
+// (K | k rows, P, p, L) in the QP's workspace, where the next recursion reads them from L2
+// one stage ahead of their use.  QP data is read where it lies (HBM / L2).
+#include "kernels.h"
+#include "mfma_lat.h"
+
+namespace srbd {
+namespace ipm_lat {
+
+constexpr int kThreads = 512;
+constexpr int kGroups = kThreads / kGroup;  // one stage per 16-lane group
+constexpr double kThr0 = 0.1;               // HPIPM init_var minimum slack
+constexpr double kTau = 0.995;              // fraction to the boundary
+
+// stage record in the QP's workspace (doubles); K | k rows and P, p as kernels.h kWs*
+constexpr int kRK = 0, kRP = 156, kRp = 234, kRL = 246, kRrs = 324;
+// the stage's barrier-augmented blocks: b~, R~, S~ (nu x nx), Q~ (column-major), r~, q~
+constexpr int kRb = 336, kRR = 348, kRS = 492, kRQ = 636, kRr = 780, kRq = 792;
+constexpr int kRStage = 804;
+static_assert(kRStage % 2 == 0, "16-byte aligned stage records");
+
+constexpr int kRedSlots = 8;
+// general rows, per stage and 12-row chunk: bars [48], steps [48], row values [12], Gamma [12]
+constexpr int kGenChunk = 120;
+// the factorization's operand ring (three stages): A, B, then the record's b~ R~ S~ Q~ r~ q~
+constexpr int kSA = 0, kSB = 144, kSb = 288, kSR = 300, kSS = 444, kSQ = 588, kSr = 732, kSq = 744;
+constexpr int kSlot = 756;
+static_assert(kSb - kSA == 2 * 144 && kRR - kRb == kSR - kSb && kRq - kRb == kSq - kSb, "ring = A, B, record blocks");
+
+__host__ __device__ constexpr size_t lds_doubles(int N, int nch) {
+  return (size_t)29 * (N + 1) * 12 + (size_t)nch * (N + 1) * kGenChunk + (size_t)N * 156 + 648 +
+         (size_t)kGroups * kRedSlots + 3 * kSlot;
+}
+
+// Offsets, not stored pointers: every address is formed from the one __shared__ base, so the
+// compiler keeps LDS accesses as ds_read / ds_write (a pointer table in memory would turn them
+// into flat accesses through the stack).
+struct Lds {
+  double* base;
+  int S;    // (N + 1) * 12
+  int N, nch;
+  // [N+1][12]: iterate, step, residuals, corrector gradients, corrector k and p
+  __device__ double* v12(int i) const { return base + i * S; }
+  __device__ double* x() const { return v12(0); }
+  __device__ double* u() const { return v12(1); }
+  __device__ double* pi() const { return v12(2); }
+  __device__ double* dx() const { return v12(3); }
+  __device__ double* du() const { return v12(4); }
+  __device__ double* dpi() const { return v12(5); }
+  __device__ double* rgu() const { return v12(6); }
+  __device__ double* rgx() const { return v12(7); }
+  __device__ double* rb() const { return v12(8); }
+  __device__ double* gtu() const { return v12(9); }
+  __device__ double* gtx() const { return v12(10); }
+  __device__ double* kv() const { return v12(11); }
+  __device__ double* pv() const { return v12(12); }
+  // [N+1][48]: box barrier state of u / x (lam_l, lam_u, t_l, t_u) and its step
+  // (dt_l, dt_u, dlam_l, dlam_u)
+  __device__ double* bu() const { return base + 13 * S; }
+  __device__ double* bx() const { return base + 17 * S; }
+  __device__ double* su() const { return base + 21 * S; }
+  __device__ double* sx() const { return base + 25 * S; }
+  // general rows, [N+1][nch][kGenChunk]
+  __device__ double* gb(int k, int ch) const { return base + 29 * S + (k * nch + ch) * kGenChunk; }
+  __device__ double* acl() const { return base + 29 * S + (N + 1) * nch * kGenChunk; }  // [N][156]
+  // factorization hand-over: G/H tile, two Y tiles, two L factors
+  __device__ double* scr() const { return acl() + N * 156; }
+  __device__ double* red() const { return scr() + 648; }  // [kGroups][kRedSlots]
+  __device__ double* ring() const { return red() + kGroups * kRedSlots; }  // [3][kSlot]
+};
+
+__device__ __forceinline__ Lds carve(double* base, int N, int nch) {
+  Lds L;
+  L.base = base;
+  L.S = (N + 1) * 12;
+  L.N = N;
+  L.nch = nch;
+  return L;
+}
+
+// An opaque copy of a thread index or the QP index at the top of each phase: the phases are
+// inlined into one kernel loop, and without this the compiler hoists their address arithmetic
+// out of the loop and keeps it live across every other phase (976 B/lane of scratch).
+__device__ __forceinline__ int opq(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+// QP data (QP-major, the only layout the constrained solve takes: srbd_qp_capi.hip check_dims)
+struct Qp {
+  const ProblemArgsT<double>& a;
+  int q, N;
+  __device__ size_t qi() const { return (size_t)opq(q); }  // (opaque: see opq)
+  __device__ const double* A(int k) const { return a.A + (qi() * N + k) * 144; }
+  __device__ const double* B(int k) const { return a.B + (qi() * N + k) * 144; }
+  __device__ const double* b(int k) const { return a.b + (qi() * N + k) * 12; }
+  __device__ const double* Q(int k) const { return a.Q + (qi() * (N + 1) + k) * 144; }
+  __device__ const double* S(int k) const { return a.S + (qi() * N + k) * 144; }
+  __device__ const double* R(int k) const { return a.R + (qi() * N + k) * 144; }
+  __device__ const double* qv(int k) const { return a.q + (qi() * (N + 1) + k) * 12; }
+  __device__ const double* rv(int k) const { return a.r + (qi() * N + k) * 12; }
+  __device__ double* rec(int k) const { return a.ws + qi() * a.ws_qp + (size_t)k * kRStage; }
+  // row r of D_k / C_k (ng x 12, column-major): element j at [j * ng]; null when absent
+  // (D_N: no input; C_0: dropped with x_0, ocp_qp_ipm_solver.cpp:128)
+  __device__ const double* Drow(int k, int r) const {
+    return (a.D && k < N) ? a.D + (qi() * N + k) * a.ng * 12 + r : nullptr;
+  }
+  __device__ const double* Crow(int k, int r) const {
+    return (a.C && k > 0) ? a.C + (qi() * (N + 1) + k) * a.ng * 12 + r : nullptr;
+  }
+};
+
+struct Side {
+  double lb, ub, ml, mu;
+};
+__device__ __forceinline__ Side side_at(const double* lb, const double* ub, const double* lm,
+                                        const double* um, size_t o) {
+  const double ml = lm ? lm[o] : 1.0, mu = um ? um[o] : 1.0;
+  return Side{lb[o], ub[o], ml != 0.0 ? 1.0 : 0.0, mu != 0.0 ? 1.0 : 0.0};
+}
+__device__ __forceinline__ Side side_u(const Qp& Q, int k, int i) {
+  const ProblemArgsT<double>& a = Q.a;
+  if (!a.lbu || k >= Q.N || i >= 12) return Side{0, 0, 0, 0};
+  return side_at(a.lbu, a.ubu, a.lbu_mask, a.ubu_mask, ((size_t)Q.q * Q.N + k) * 12 + i);
+}
+__device__ __forceinline__ Side side_x(const Qp& Q, int k, int i) {
+  const ProblemArgsT<double>& a = Q.a;
+  if (!a.lbx || k == 0 || i >= 12) return Side{0, 0, 0, 0};  // stage-0 x bounds dropped
+  return side_at(a.lbx, a.ubx, a.lbx_mask, a.ubx_mask, ((size_t)Q.q * (Q.N + 1) + k) * 12 + i);
+}
+__device__ __forceinline__ Side side_g(const Qp& Q, int k, int r) {
+  const ProblemArgsT<double>& a = Q.a;
+  if (r >= a.ng) return Side{0, 0, 0, 0};
+  return side_at(a.lg, a.ug, a.lg_mask, a.ug_mask, ((size_t)Q.q * (Q.N + 1) + k) * a.ng + r);
+}
+
+struct Bar {
+  double ll, lu, tl, tu;
+};
+struct BarStep {
+  double dtl, dtu, dll, dlu;
+};
+__device__ __forceinline__ Bar ld_bar(const double* p, int i) { return Bar{p[i], p[12 + i], p[24 + i], p[36 + i]}; }
+__device__ __forceinline__ void st_bar(double* p, int i, const Bar& b) {
+  p[i] = b.ll;
+  p[12 + i] = b.lu;
+  p[24 + i] = b.tl;
+  p[36 + i] = b.tu;
+}
+__device__ __forceinline__ BarStep ld_step(const double* p, int i) {
+  return BarStep{p[i], p[12 + i], p[24 + i], p[36 + i]};
+}
+__device__ __forceinline__ void st_step(double* p, int i, const BarStep& d) {
+  p[i] = d.dtl;
+  p[12 + i] = d.dtu;
+  p[24 + i] = d.dll;
+  p[36 + i] = d.dlu;
+}
+
+// HPIPM init_var for one box-bounded variable: project into the box by thr0, t, lam = mu0 / t
+__device__ __forceinline__ Bar init_box(const Side& s, double& v, double mu0) {
+  Bar bb{0.0, 0.0, 1.0, 1.0};
+  if (s.ml == 0.0 && s.mu == 0.0) return bb;
+  double tl = v - s.lb, tu = s.ub - v;
+  if (s.ml != 0.0 && s.mu != 0.0) {
+    if (tl < kThr0) {
+      if (tu < kThr0) {
+        v = 0.5 * (s.lb + s.ub);
+        tl = tu = kThr0;
+      } else {
+        tl = kThr0;
+        v = s.lb + kThr0;
+        tu = s.ub - v;
+      }
+    } else if (tu < kThr0) {
+      tu = kThr0;
+      v = s.ub - kThr0;
+      tl = v - s.lb;
+    }
+  } else if (s.ml != 0.0) {
+    if (tl < kThr0) {
+      tl = kThr0;
+      v = s.lb + kThr0;
+    }
+  } else if (tu < kThr0) {
+    tu = kThr0;
+    v = s.ub - kThr0;
+  }
+  bb.tl = s.ml != 0.0 ? tl : 1.0;
+  bb.tu = s.mu != 0.0 ? tu : 1.0;
+  bb.ll = s.ml != 0.0 ? mu0 / tl : 0.0;
+  bb.lu = s.mu != 0.0 ? mu0 / tu : 0.0;
+  return bb;
+}
+// Gamma / gamma of one side pair (ipm_box_impl.h gamma_of): rm = lam t + ext - smu
+__device__ __forceinline__ void gamma_of(const Side& s, const Bar& b, double v, double el, double eu,
+                                         double smu, double& G, double& g) {
+  G = 0.0;
+  g = 0.0;
+  if (s.ml != 0.0) {
+    const double rd = v - s.lb - b.tl, rm = b.ll * b.tl + el - smu;
+    G += b.ll / b.tl;
+    g += (rm + b.ll * rd) / b.tl;
+  }
+  if (s.mu != 0.0) {
+    const double rd = s.ub - v - b.tu, rm = b.lu * b.tu + eu - smu;
+    G += b.lu / b.tu;
+    g -= (rm + b.lu * rd) / b.tu;
+  }
+}
+__device__ __forceinline__ BarStep bar_step(const Side& s, const Bar& b, double v, double dv, double el,
+                                            double eu, double smu) {
+  BarStep d{0.0, 0.0, 0.0, 0.0};
+  if (s.ml != 0.0) {
+    d.dtl = (v - s.lb - b.tl) + dv;
+    d.dll = -(b.ll * b.tl + el - smu + b.ll * d.dtl) / b.tl;
+  }
+  if (s.mu != 0.0) {
+    d.dtu = (s.ub - v - b.tu) - dv;
+    d.dlu = -(b.lu * b.tu + eu - smu + b.lu * d.dtu) / b.tu;
+  }
+  return d;
+}
+__device__ __forceinline__ void ratio(const Side& s, const Bar& b, const BarStep& d, double& ap, double& ad) {
+  if (s.ml != 0.0) {
+    if (d.dtl < 0.0) ap = fmin(ap, -b.tl / d.dtl);
+    if (d.dll < 0.0) ad = fmin(ad, -b.ll / d.dll);
+  }
+  if (s.mu != 0.0) {
+    if (d.dtu < 0.0) ap = fmin(ap, -b.tu / d.dtu);
+    if (d.dlu < 0.0) ad = fmin(ad, -b.lu / d.dlu);
+  }
+}
+__device__ __forceinline__ void aff_sums(const Side& s, const Bar& b, const BarStep& d, double& s1, double& s2) {
+  if (s.ml != 0.0) {
+    s1 += b.ll * d.dtl + b.tl * d.dll;
+    s2 += d.dll * d.dtl;
+  }
+  if (s.mu != 0.0) {
+    s1 += b.lu * d.dtu + b.tu * d.dlu;
+    s2 += d.dlu * d.dtu;
+  }
+}
+__device__ __forceinline__ double nabs(double v) { return v == v ? fabs(v) : __builtin_inf(); }
+__device__ __forceinline__ bool huge(double v) { return !(fabs(v) < 1.3e150); }
+__device__ __forceinline__ double stepv(double v, double a, double d) { return a != 0.0 ? fma(a, d, v) : v; }
+
+__device__ __forceinline__ double g16sum(double v) {
+  v += __shfl_xor(v, 8, kGroup);
+  v += __shfl_xor(v, 4, kGroup);
+  v += __shfl_xor(v, 2, kGroup);
+  v += __shfl_xor(v, 1, kGroup);
+  return v;
+}
+__device__ __forceinline__ double g16max(double v) {
+  v = fmax(v, __shfl_xor(v, 8, kGroup));
+  v = fmax(v, __shfl_xor(v, 4, kGroup));
+  v = fmax(v, __shfl_xor(v, 2, kGroup));
+  v = fmax(v, __shfl_xor(v, 1, kGroup));
+  return v;
+}
+__device__ __forceinline__ double g16min(double v) {
+  v = fmin(v, __shfl_xor(v, 8, kGroup));
+  v = fmin(v, __shfl_xor(v, 4, kGroup));
+  v = fmin(v, __shfl_xor(v, 2, kGroup));
+  v = fmin(v, __shfl_xor(v, 1, kGroup));
+  return v;
+}
+
+// 12 strided values p[i * ld] (a row of a column-major block), 0 where p is null
+__device__ __forceinline__ void load_strided(const double* p, int ld, double (&v)[12]) {
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    v[I] = p ? p[I * ld] : 0.0;
+  });
+}
+__device__ __forceinline__ void load12z(const double* p, double (&v)[12]) {
+  if (p) {
+    load12(p, v);
+  } else {
+    sfor<0, 12>([&](auto i) { v[decltype(i)::value] = 0.0; });
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// block-wide reductions of per-group partials: slot values written by each group's lane 0,
+// reduced by every thread after the barrier (same order everywhere: uniform results)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void red_put(const Lds& L, int slot, double v) {
+  if ((threadIdx.x & 15) == 0) L.red()[(threadIdx.x >> 4) * kRedSlots + slot] = v;
+}
+__device__ __forceinline__ double red_sum(const Lds& L, int slot) {
+  double s = 0.0;
+  for (int g = 0; g < kGroups; ++g) s += L.red()[g * kRedSlots + slot];
+  return s;
+}
+__device__ __forceinline__ double red_max(const Lds& L, int slot) {
+  double s = 0.0;
+  for (int g = 0; g < kGroups; ++g) {
+    const double v = L.red()[g * kRedSlots + slot];
+    s = (v > s || v != v) ? v : s;
+  }
+  return s;
+}
+__device__ __forceinline__ double red_min(const Lds& L, int slot) {
+  double s = 1e30;
+  for (int g = 0; g < kGroups; ++g) s = fmin(s, L.red()[g * kRedSlots + slot]);
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase: initial point (HPIPM init_var, ipm_box_impl.h kPhInit)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void init_point(const Qp Q, const Lds L) {
+  const ProblemArgsT<double>& a = Q.a;
+  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
+  const bool el = j < 12;
+  double ncl = 0.0;
+  for (int k = grp; k <= N; k += kGroups) {
+    double uv = 0.0, xv = 0.0;
+    if (k < N) {
+      double v = (a.warm_start && el) ? a.u[((size_t)Q.q * N + k) * 12 + j] : 0.0;
+      const Side s = side_u(Q, k, j);
+      const Bar bb = init_box(s, v, a.mu0);
+      ncl += s.ml + s.mu;
+      if (el) {
+        st_bar(L.bu() + k * 48, j, bb);
+        st_step(L.su() + k * 48, j, BarStep{0, 0, 0, 0});
+        L.u()[k * 12 + j] = v;
+      }
+      uv = el ? v : 0.0;
+    } else if (el) {
+      st_bar(L.bu() + k * 48, j, Bar{0, 0, 1, 1});
+      st_step(L.su() + k * 48, j, BarStep{0, 0, 0, 0});
+      L.u()[k * 12 + j] = 0.0;
+    }
+    {
+      double v = k == 0 ? (el ? a.x0[(size_t)Q.q * 12 + j] : 0.0)
+                        : ((a.warm_start && el) ? a.x[((size_t)Q.q * (N + 1) + k) * 12 + j] : 0.0);
+      const Side s = side_x(Q, k, j);
+      const Bar bb = init_box(s, v, a.mu0);
+      ncl += s.ml + s.mu;
+      if (el) {
+        st_bar(L.bx() + k * 48, j, bb);
+        st_step(L.sx() + k * 48, j, BarStep{0, 0, 0, 0});
+        L.x()[k * 12 + j] = v;
+        L.pi()[k * 12 + j] = 0.0;
+      }
+      xv = el ? v : 0.0;
+    }
+    // general rows: t = max(v - lg, thr0), max(ug - v, thr0) at the initial point
+    for (int ch = 0; ch < L.nch; ++ch) {
+      const int r = ch * 12 + j;
+      const bool ok = el && r < a.ng;
+      double Dr[12], Cr[12];
+      load_strided(ok ? Q.Drow(k, r) : nullptr, a.ng, Dr);
+      load_strided(ok ? Q.Crow(k, r) : nullptr, a.ng, Cr);
+      const double v = dot_bcast(Cr, xv, dot_bcast(Dr, uv, 0.0));
+      const Side s = ok ? side_g(Q, k, r) : Side{0, 0, 0, 0};
+      Bar bb{0.0, 0.0, 1.0, 1.0};
+      if (s.ml != 0.0) {
+        bb.tl = fmax(v - s.lb, kThr0);
+        bb.ll = a.mu0 / bb.tl;
+      }
+      if (s.mu != 0.0) {
+        bb.tu = fmax(s.ub - v, kThr0);
+        bb.lu = a.mu0 / bb.tu;
+      }
+      ncl += s.ml + s.mu;
+      if (el) {
+        double* g = L.gb(k, ch);
+        st_bar(g, j, bb);
+        st_step(g + 48, j, BarStep{0, 0, 0, 0});
+        g[96 + j] = v;
+      }
+    }
+  }
+  red_put(L, 0, g16sum(ncl));
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase: residuals at the iterate (oracle compute_residuals; HPIPM d_ocp_qp_res_compute)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void residuals(const Qp Q, const Lds L) {
+  const ProblemArgsT<double>& a = Q.a;
+  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
+  const bool el = j < 12;
+  const int jj = el ? j : 11;
+  double mg = 0.0, mb = 0.0, md = 0.0, mm = 0.0, musum = 0.0, objl = 0.0;
+  for (int k = grp; k <= N; k += kGroups) {
+    const double uj = (el && k < N) ? L.u()[k * 12 + j] : 0.0;
+    const double xj = el ? L.x()[k * 12 + j] : 0.0;
+    const double pij = el ? L.pi()[k * 12 + j] : 0.0;
+    const double pinj = (el && k < N) ? L.pi()[(k + 1) * 12 + j] : 0.0;
+    double gu = 0.0, gx;
+    double Mc[12];
+    double sx = 0.0;  // (S x)_j
+    if (k < N) {
+      load12(Q.R(k) + jj * 12, Mc);
+      const double t1 = dot_bcast(Mc, uj, 0.0);
+      load_strided(Q.S(k) + jj, 12, Mc);
+      sx = dot_bcast(Mc, xj, 0.0);
+      const double rj = el ? Q.rv(k)[j] : 0.0;
+      load12(Q.B(k) + jj * 12, Mc);
+      const double bpi = dot_bcast(Mc, pinj, 0.0);
+      gu = t1 + sx + rj + bpi;
+      double o = uj * (0.5 * t1 + rj);
+      if (k == 0) o += uj * sx;
+      objl += el ? o : 0.0;
+    }
+    {
+      load12(Q.Q(k) + jj * 12, Mc);
+      const double t1 = dot_bcast(Mc, xj, 0.0);
+      const double qj = el ? Q.qv(k)[j] : 0.0;
+      gx = t1 + qj - pij;
+      if (k > 0) {
+        double o = xj * (0.5 * t1 + qj);
+        if (k < N) o += uj * sx;
+        objl += el ? o : 0.0;
+      }
+      if (k < N) {
+        load12(Q.S(k) + jj * 12, Mc);
+        gx += dot_bcast(Mc, uj, 0.0);
+        load12(Q.A(k) + jj * 12, Mc);
+        gx += dot_bcast(Mc, pinj, 0.0);
+      }
+    }
+    // box rows
+    if (k < N) {
+      const Side s = side_u(Q, k, j);
+      const Bar b = el ? ld_bar(L.bu() + k * 48, j) : Bar{0, 0, 1, 1};
+      gu -= (s.ml != 0.0 ? b.ll : 0.0) - (s.mu != 0.0 ? b.lu : 0.0);
+      if (s.ml != 0.0) {
+        const double rd = uj - s.lb - b.tl, rm = b.ll * b.tl;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (s.mu != 0.0) {
+        const double rd = s.ub - uj - b.tu, rm = b.lu * b.tu;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+    }
+    if (k > 0) {
+      const Side s = side_x(Q, k, j);
+      const Bar b = el ? ld_bar(L.bx() + k * 48, j) : Bar{0, 0, 1, 1};
+      gx -= (s.ml != 0.0 ? b.ll : 0.0) - (s.mu != 0.0 ? b.lu : 0.0);
+      if (s.ml != 0.0) {
+        const double rd = xj - s.lb - b.tl, rm = b.ll * b.tl;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (s.mu != 0.0) {
+        const double rd = s.ub - xj - b.tu, rm = b.lu * b.tu;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+    }
+    // general rows (lane j = row ch * 12 + j of the chunk): values, rd / rm, gradient terms
+    for (int ch = 0; ch < L.nch; ++ch) {
+      const int r = ch * 12 + j;
+      const bool ok = el && r < a.ng;
+      double Dr[12], Cr[12];
+      load_strided(ok ? Q.Drow(k, r) : nullptr, a.ng, Dr);
+      load_strided(ok ? Q.Crow(k, r) : nullptr, a.ng, Cr);
+      const double v = dot_bcast(Cr, xj, dot_bcast(Dr, uj, 0.0));
+      const Side s = ok ? side_g(Q, k, r) : Side{0, 0, 0, 0};
+      double* g = L.gb(k, ch);
+      const Bar b = el ? ld_bar(g, j) : Bar{0, 0, 1, 1};
+      if (el) g[96 + j] = v;
+      if (s.ml != 0.0) {
+        const double rd = v - s.lb - b.tl, rm = b.ll * b.tl;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (s.mu != 0.0) {
+        const double rd = s.ub - v - b.tu, rm = b.lu * b.tu;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      const double cr = (s.ml != 0.0 ? b.ll : 0.0) - (s.mu != 0.0 ? b.lu : 0.0);
+      // gu -= D' c, gx -= C' c: column j of D / C against the chunk's row-owned c
+      const int rr = ch * 12;
+      double Dc[12], Cc[12];
+      const bool okc = el && rr < a.ng;
+      sfor<0, 12>([&](auto i) {
+        constexpr int I = decltype(i)::value;
+        const double* dp = Q.Drow(k, rr + I);
+        const double* cp = Q.Crow(k, rr + I);
+        const bool iok = okc && rr + I < a.ng;
+        Dc[I] = (iok && dp) ? dp[(size_t)a.ng * jj] : 0.0;
+        Cc[I] = (iok && cp) ? cp[(size_t)a.ng * jj] : 0.0;
+      });
+      gu -= dot_bcast(Dc, cr, 0.0);
+      gx -= dot_bcast(Cc, cr, 0.0);
+    }
+    if (k < N) mg = fmax(mg, el ? nabs(gu) : 0.0);
+    if (k > 0) mg = fmax(mg, el ? nabs(gx) : 0.0);
+    double rbj = 0.0;
+    if (k < N) {
+      double Ar[12], Br[12];
+      load_strided(Q.A(k) + jj, 12, Ar);
+      load_strided(Q.B(k) + jj, 12, Br);
+      const double t1 = dot_bcast(Ar, xj, 0.0), t2 = dot_bcast(Br, uj, 0.0);
+      const double xn = el ? L.x()[(k + 1) * 12 + j] : 0.0;
+      rbj = t1 + t2 + (el ? Q.b(k)[j] : 0.0) - xn;
+      mb = fmax(mb, el ? nabs(rbj) : 0.0);
+    }
+    if (el) {
+      L.rgu()[k * 12 + j] = gu;
+      L.rgx()[k * 12 + j] = gx;
+      L.rb()[k * 12 + j] = rbj;
+    }
+  }
+  red_put(L, 0, g16max(mg));
+  red_put(L, 1, g16max(mb));
+  red_put(L, 2, g16max(md));
+  red_put(L, 3, g16max(mm));
+  red_put(L, 4, g16sum(el ? musum : 0.0));
+  red_put(L, 5, g16sum(objl));
+}
+
+// ---------------------------------------------------------------------------------------------
+// column j of chunk ch's rows of D_k (or C_k): v[i] = D[ch * 12 + i][j], 0 past ng / when absent
+// ---------------------------------------------------------------------------------------------
+template <bool ISC>
+__device__ __forceinline__ void gen_col(const Qp& Q, int k, int ch, int jj, bool el, double (&v)[12]) {
+  const int rr = ch * 12, ng = Q.a.ng;
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    const bool iok = el && rr + I < ng;
+    const double* p = iok ? (ISC ? Q.Crow(k, rr + I) : Q.Drow(k, rr + I)) : nullptr;
+    v[I] = p ? p[(size_t)ng * jj] : 0.0;
+  });
+}
+// row j of chunk ch (lane j = row ch * 12 + j): v[i] = D[ch * 12 + j][i]
+template <bool ISC>
+__device__ __forceinline__ void gen_row(const Qp& Q, int k, int ch, int j, bool el, double (&v)[12]) {
+  const int r = ch * 12 + j;
+  const bool ok = el && r < Q.a.ng;
+  load_strided(ok ? (ISC ? Q.Crow(k, r) : Q.Drow(k, r)) : nullptr, Q.a.ng, v);
+}
+// C[i] += sum_r X[r][i] Gamma_r Y[r][j] over the general rows (column j of X'Gamma Y; X = D or C
+// row-owned on the chunk's lanes, Y's column j on lane j, Gamma from the chunk's LDS slot)
+template <bool XC, bool YC>
+__device__ __forceinline__ void gen_syrk(const Qp Q, const Lds L, int k, int j, int jj, bool el,
+                                         double (&C)[12]) {
+  for (int ch = 0; ch < L.nch; ++ch) {
+    double Xr[12], Yc[12];
+    gen_row<XC>(Q, k, ch, j, el, Xr);
+    gen_col<YC>(Q, k, ch, jj, el, Yc);
+    const double G = el ? L.gb(k, ch)[108 + j] : 0.0;
+    sfor<0, 12>([&](auto rs) {
+      constexpr int R = decltype(rs)::value;
+      fma_bcast_src<R>(C, Xr, bc<R>(G) * Yc[R]);
+    });
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase: barrier terms of the predictor (CORR false: Gamma, gamma; the stage blocks R~, S~,
+// Q~, r~, q~, b~ into the workspace for the factorization) or of the corrector (CORR true:
+// gamma with the predictor's dlam dt and sigma mu, into gtu / gtx).  HAS_C: the problem has C
+// (C-free general rows -- the friction cone -- skip every C product).  One pass per Hessian
+// block, so no more than one 12 x 12 accumulator is live.
+// ---------------------------------------------------------------------------------------------
+template <bool CORR, bool HAS_C>
+__device__ __forceinline__ void barrier_terms(const Qp Q, const Lds L, double smu) {
+  const ProblemArgsT<double>& a = Q.a;
+  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
+  const bool el = j < 12;
+  const int jj = el ? j : 11;
+  for (int k = grp; k <= N; k += kGroups) {
+    double Gu = 0.0, gam_u = 0.0, Gx = 0.0, gam_x = 0.0;
+    if (k < N && el) {
+      const Side s = side_u(Q, k, j);
+      const Bar b = ld_bar(L.bu() + k * 48, j);
+      double e1 = 0.0, e2 = 0.0;
+      if (CORR) {
+        const BarStep d = ld_step(L.su() + k * 48, j);
+        e1 = d.dll * d.dtl;
+        e2 = d.dlu * d.dtu;
+      }
+      gamma_of(s, b, L.u()[k * 12 + j], e1, e2, CORR ? smu : 0.0, Gu, gam_u);
+    }
+    if (k > 0 && el) {
+      const Side s = side_x(Q, k, j);
+      const Bar b = ld_bar(L.bx() + k * 48, j);
+      double e1 = 0.0, e2 = 0.0;
+      if (CORR) {
+        const BarStep d = ld_step(L.sx() + k * 48, j);
+        e1 = d.dll * d.dtl;
+        e2 = d.dlu * d.dtu;
+      }
+      gamma_of(s, b, L.x()[k * 12 + j], e1, e2, CORR ? smu : 0.0, Gx, gam_x);
+    }
+    double gu = (el ? L.rgu()[k * 12 + j] : 0.0) + gam_u;
+    double gx = (el ? L.rgx()[k * 12 + j] : 0.0) + gam_x;
+    // general rows: Gamma (kept for the Hessian passes), gradient D'gamma / C'gamma
+    for (int ch = 0; ch < L.nch; ++ch) {
+      const int r = ch * 12 + j;
+      const bool ok = el && r < a.ng;
+      double* g = L.gb(k, ch);
+      double G = 0.0, gam = 0.0;
+      if (ok) {
+        double e1 = 0.0, e2 = 0.0;
+        if (CORR) {
+          const BarStep d = ld_step(g + 48, j);
+          e1 = d.dll * d.dtl;
+          e2 = d.dlu * d.dtu;
+        }
+        gamma_of(side_g(Q, k, r), ld_bar(g, j), g[96 + j], e1, e2, CORR ? smu : 0.0, G, gam);
+      }
+      if (!CORR && el) g[108 + j] = G;
+      double Mc[12];
+      gen_col<false>(Q, k, ch, jj, el, Mc);
+      gu = dot_bcast(Mc, gam, gu);
+      if constexpr (HAS_C) {
+        gen_col<true>(Q, k, ch, jj, el, Mc);
+        gx = dot_bcast(Mc, gam, gx);
+      }
+    }
+    if (CORR) {
+      if (el) {
+        L.gtu()[k * 12 + j] = gu;
+        L.gtx()[k * 12 + j] = gx;
+      }
+      continue;
+    }
+    // predictor: the barrier-augmented blocks of stage k into its record
+    double* rk = Q.rec(k);
+    double C[12];
+    if (k < N) {
+      load12(Q.R(k) + jj * 12, C);  // R~ = R + diag(Gamma_u) + D'Gamma D
+      sfor<0, 12>([&](auto i) { C[decltype(i)::value] += decltype(i)::value == j ? Gu : 0.0; });
+      gen_syrk<false, false>(Q, L, k, j, jj, el, C);
+      if (el) store12(rk + kRR + j * 12, C);
+      load12(Q.S(k) + jj * 12, C);  // S~ = S + D'Gamma C
+      if constexpr (HAS_C) gen_syrk<false, true>(Q, L, k, j, jj, el, C);
+      if (el) {
+        store12(rk + kRS + j * 12, C);
+        rk[kRr + j] = gu;
+        rk[kRb + j] = L.rb()[k * 12 + j];
+      }
+    }
+    load12(Q.Q(k) + jj * 12, C);  // Q~ = Q + diag(Gamma_x) + C'Gamma C
+    sfor<0, 12>([&](auto i) { C[decltype(i)::value] += decltype(i)::value == j ? Gx : 0.0; });
+    if constexpr (HAS_C) gen_syrk<true, true>(Q, L, k, j, jj, el, C);
+    if (el) {
+      store12(rk + kRQ + j * 12, C);
+      rk[kRq + j] = gx;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase: the factorization (backward, serial in k) on matrix cores -- riccati_latency_impl.h's
+// sweep.  Wave 0: stage k's products and Cholesky; wave 1: stage k+1's K, record and closed
+// loop; wave 2: stage k-1's operands (A, B from the QP, R~ S~ Q~ r~ q~ b~ from the record) into
+// the LDS ring, so no global load sits on the chain.  Records per stage: [K | k] rows, P packed,
+// p, L packed + 1 / diag; [Acl | bcl] rows in LDS.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
+  const ProblemArgsT<double>& a = Q.a;
+  const int N = Q.N;
+  const int wave = threadIdx.x >> 6, l = opq(threadIdx.x & 63);
+  const int g = l >> 4, c = l & 15;
+  const bool cv = c < 12, cw = c <= 12;
+  const int cc = cv ? c : 11;
+  double* const gh = L.scr();
+  double* const ybuf = L.scr() + 156;
+  double* const lbuf = L.scr() + 3 * 156;
+  double* const ring = L.ring();
+  auto slot = [&](int k) { return ring + (k % 3) * kSlot; };
+  auto load_slot = [&](int k) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    d2* s2 = reinterpret_cast<d2*>(slot(k));
+    const d2* A2 = reinterpret_cast<const d2*>(Q.A(k));
+    const d2* B2 = reinterpret_cast<const d2*>(Q.B(k));
+    const d2* I2 = reinterpret_cast<const d2*>(Q.rec(k) + kRb);
+    for (int t = l; t < 72; t += 64) {
+      s2[kSA / 2 + t] = A2[t];
+      s2[kSB / 2 + t] = B2[t];
+    }
+    for (int t = l; t < (kSlot - kSb) / 2; t += 64) s2[kSb / 2 + t] = I2[t];
+  };
+  lat_d4 Pt;
+  if (wave == 0) {
+    const double* rn = Q.rec(N);
+    sfor<0, 4>([&](auto rr) {
+      constexpr int R = decltype(rr)::value;
+      const int row = g + 4 * R < 12 ? g + 4 * R : 11;
+      const double v = rn[cv ? kRQ + c * 12 + row : kRq + row];
+      Pt[R] = (g + 4 * R < 12 && cw) ? v : 0.0;
+    });
+    double* wn = Q.rec(N);
+    sfor<0, 3>([&](auto rr) {
+      constexpr int R = decltype(rr)::value;
+      const int row = g + 4 * R;
+      if (cv && row >= c) wn[kRP + packed_col(c) + row - c] = Pt[R];
+      if (c == 12) wn[kRp + row] = Pt[R];
+    });
+  } else if (wave == 2) {
+    load_slot(N - 1);
+  }
+  __syncthreads();
+  auto finish_stage = [&](int jst) {
+    const double* lb = lbuf + (jst & 1) * 90;
+    const double* yb = ybuf + (jst & 1) * 156;
+    const double* sl = slot(jst);
+    double Lc[12], Yc[12], Kc[12];
+    load_packed_lcol(lb, cc, Lc);
+    const double rs = lb[78 + cc];
+    sfor<0, 12>([&](auto i) { Yc[decltype(i)::value] = cw ? yb[c * 12 + decltype(i)::value] : 0.0; });
+    trsv_upper_t_neg_axpy(Lc, rs, Yc, Kc);  // lane c < 12: K[:, c]; lane 12: k
+    double* rj = Q.rec(jst);
+    if (l < 16 && cw)
+      sfor<0, 12>([&](auto i) { rj[kRK + decltype(i)::value * 13 + c] = Kc[decltype(i)::value]; });
+    for (int t = l; t < 90; t += 64) rj[kRL + t] = lb[t];
+    // [Acl | bcl][:, c] = [A | b~][:, c] + B [K | k][:, c]
+    double Ac[12], Bc[12];
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      const double av = sl[cv ? kSA + c * 12 + I : kSb + I];
+      Ac[I] = cw ? av : 0.0;
+      const double bv = sl[kSB + cc * 12 + I];
+      Bc[I] = cv ? bv : 0.0;
+    });
+    sfor<0, 12>([&](auto m) {
+      constexpr int M = decltype(m)::value;
+      fma_bcast_src<M>(Ac, Bc, Kc[M]);
+    });
+    if (l < 16 && cw)
+      sfor<0, 12>([&](auto i) { L.acl()[jst * 156 + decltype(i)::value * 13 + c] = Ac[decltype(i)::value]; });
+  };
+#pragma unroll 1
+  for (int k = N - 1; k >= 0; --k) {
+    if (wave == 0) {
+      const double* sl = slot(k);
+      double bo[3], ao[3];
+      sfor<0, 3>([&](auto kb) {
+        constexpr int KB = decltype(kb)::value;
+        const int m = 4 * KB + g;
+        const double bv = sl[kSB + cc * 12 + m];
+        bo[KB] = cv ? bv : 0.0;  // B[m][c]: B operand of P B; A operand (B') of B'WB, B'W
+        const double av = sl[cv ? kSA + c * 12 + m : kSb + m];
+        ao[KB] = cw ? av : 0.0;  // [A | b~][m][c]: B operand of P [A | b~]; A operand (A') of A'W
+      });
+      lat_d4 Rt, St, Qt;
+      sfor<0, 4>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        const bool rok = g + 4 * R < 12;
+        const int row = rok ? g + 4 * R : 11;
+        const double rv = sl[kSR + cc * 12 + row];
+        const double sv = sl[cv ? kSS + c * 12 + row : kSr + row];
+        const double qv = sl[cv ? kSQ + c * 12 + row : kSq + row];
+        Rt[R] = rok && cv ? rv : 0.0;
+        St[R] = rok && cw ? sv : 0.0;
+        Qt[R] = rok && cw ? qv : 0.0;
+      });
+      // WB = P B; G = R~ + B'WB (the critical path)
+      lat_d4 WB = {0.0, 0.0, 0.0, 0.0};
+      sfor<0, 3>([&](auto kb) { WB = lat_mfma(Pt[decltype(kb)::value], bo[decltype(kb)::value], WB); });
+      lat_d4 Gt = Rt;
+      sfor<0, 3>([&](auto kb) { Gt = lat_mfma(bo[decltype(kb)::value], WB[decltype(kb)::value], Gt); });
+      // W = P [A | b~] + [0 | p]; [H | g] = [S~ | r~] + B'W; [F | f] = [Q~ | q~] + A'W: one per pivot
+      lat_d4 Wt;
+      sfor<0, 4>([&](auto rr) { Wt[decltype(rr)::value] = c == 12 ? Pt[decltype(rr)::value] : 0.0; });
+      lat_d4 Ht = St, Ft = Qt;
+      auto wh = [&](auto kk) {
+        constexpr int K = decltype(kk)::value;
+        if constexpr (K < 3) {
+          Wt = lat_mfma(Pt[K], ao[K], Wt);
+        } else if constexpr (K < 9) {
+          constexpr int KB = (K - 3) / 2;
+          if constexpr ((K - 3) % 2 == 0) {
+            Ht = lat_mfma(bo[KB], Wt[KB], Ht);
+          } else {
+            Ft = lat_mfma(ao[KB], Wt[KB], Ft);
+          }
+        }
+      };
+      lds_wave_fence();
+      sfor<0, 3>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        if (cv) gh[c * 12 + g + 4 * R] = Gt[R];
+      });
+      lds_wave_fence();
+      double Gc[12], Lc[12], rs;
+      sfor<0, 12>([&](auto i) {
+        const double v = gh[cc * 12 + decltype(i)::value];
+        Gc[decltype(i)::value] = cv ? v : 0.0;
+      });
+      lat_chol<true>(Gc, c, a.reg, Lc, rs, wh);
+      // [Y | y] = L^-1 [H | g]
+      lds_wave_fence();
+      sfor<0, 3>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        if (cw) gh[c * 12 + g + 4 * R] = Ht[R];
+      });
+      lds_wave_fence();
+      double Yc[12];
+      sfor<0, 12>([&](auto i) {
+        const double v = gh[(cw ? c : 12) * 12 + decltype(i)::value];
+        Yc[decltype(i)::value] = cw ? v : 0.0;
+      });
+      trsv_lower(Lc, rs, Yc);
+      double* yb = ybuf + (k & 1) * 156;
+      double* lb = lbuf + (k & 1) * 90;
+      if (l < 16) {
+        if (cw) store12(yb + c * 12, Yc);
+        if (cv) {
+          store_packed_col(lb, c, Lc);
+          lb[78 + c] = rs;
+        }
+      }
+      lds_wave_fence();
+      // [P | p]_k = [F | f] + K'[H | g], K = -L^-T Y, P symmetrized by averaging: the oracle's
+      // and the batched kernels' form (ipm_box_impl.h).  The unconstrained
+      // kernel's F - Y'Y stalls the stationarity residual near 3e-7 on QPs whose barrier terms
+      // reach ~1e10 in the endgame (random C / D rows, tests/test_gpu_ipm_latency.py).
+      double Kc[12];
+      trsv_upper_t_neg_axpy(Lc, rs, Yc, Kc);  // lane c < 12: K[:, c]
+      lat_d4 Pn = Ft;
+      sfor<0, 3>([&](auto kb) {
+        constexpr int KB = decltype(kb)::value;
+        const double kv = g == 0 ? Kc[4 * KB] : g == 1 ? Kc[4 * KB + 1] : g == 2 ? Kc[4 * KB + 2] : Kc[4 * KB + 3];
+        Pn = lat_mfma(cv ? kv : 0.0, Ht[KB], Pn);  // A operand (K')[c][4 KB + g] = K[4 KB + g][c]
+      });
+      sfor<0, 3>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        if (cv) gh[c * 12 + g + 4 * R] = Pn[R];
+      });
+      lds_wave_fence();
+      sfor<0, 3>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        const double t = gh[(g + 4 * R) * 12 + cc];  // P[c][g + 4 R]
+        if (cv) Pn[R] = 0.5 * (Pn[R] + t);
+      });
+      lds_wave_fence();
+      Pt = Pn;
+      double* rk = Q.rec(k);
+      sfor<0, 3>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        const int row = g + 4 * R;
+        if (cv && row >= c) rk[kRP + packed_col(c) + row - c] = Pt[R];
+        if (c == 12) rk[kRp + row] = Pt[R];
+      });
+    } else if (wave == 1) {
+      if (k < N - 1) finish_stage(k + 1);
+    } else if (wave == 2) {
+      if (k > 0) load_slot(k - 1);
+    }
+    __syncthreads();
+  }
+  if (wave == 1) finish_stage(0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase: forward recursion dx_k+1 = Acl_k dx_k + bcl_k, dx_0 = 0 (wave 0, row-owned)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void forward(const Lds L, int N) {
+  if ((threadIdx.x >> 6) != 0) return;
+  const int c = opq(threadIdx.x & 15);
+  const bool cv = c < 12;
+  const int row = cv ? c : 11;
+  double xv = 0.0;
+  double Ar[12], bv;
+  auto load_row = [&](int k, double (&R)[12], double& b) {
+    const double* r = L.acl() + k * 156 + row * 13;
+    sfor<0, 12>([&](auto j) { R[decltype(j)::value] = r[decltype(j)::value]; });
+    b = r[12];
+  };
+  load_row(0, Ar, bv);
+#pragma unroll 1
+  for (int k = 0; k < N; ++k) {
+    if (threadIdx.x < 12) L.dx()[k * 12 + c] = xv;
+    double An[12], bn = 0.0;
+    if (k + 1 < N) {
+      load_row(k + 1, An, bn);
+    } else {
+      sfor<0, 12>([&](auto j) { An[decltype(j)::value] = 0.0; });
+    }
+    const double xn = dot_bcast(Ar, xv, bv);
+    xv = cv ? xn : 0.0;
+    sfor<0, 12>([&](auto j) { Ar[decltype(j)::value] = An[decltype(j)::value]; });
+    bv = bn;
+  }
+  if (threadIdx.x < 12) L.dx()[N * 12 + c] = xv;
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase: the step of every stage from dx (du = K dx + k, dpi = P dx + p, the bounds' dt /
+// dlam), the step ratios and the predictor's mu_aff sums.  CORR: k, p of the corrector (kv,
+// pv), dlam_aff dt_aff and sigma mu in the complementarity rows.
+// ---------------------------------------------------------------------------------------------
+template <bool CORR>
+__device__ __forceinline__ void step_pass(const Qp Q, const Lds L, double smu, bool final_step) {
+  const ProblemArgsT<double>& a = Q.a;
+  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
+  const bool el = j < 12;
+  const int jj = el ? j : 11;
+  double ap = 1e30, ad = 1e30, s1 = 0.0, s2 = 0.0;
+  bool bad = false;
+  for (int k = grp; k <= N; k += kGroups) {
+    const double* rk = Q.rec(k);
+    const double dxj = el ? L.dx()[k * 12 + j] : 0.0;
+    double duj = 0.0, dpij = 0.0;
+    if (k < N) {
+      double Kr[12];
+      sfor<0, 12>([&](auto i) { Kr[decltype(i)::value] = rk[kRK + jj * 13 + decltype(i)::value]; });
+      const double kvj = CORR ? L.kv()[k * 12 + jj] : rk[kRK + jj * 13 + 12];
+      duj = dot_bcast(Kr, dxj, kvj);
+      if (!el) duj = 0.0;
+    }
+    if (k > 0) {
+      double Pr[12];
+      load_packed_sym(rk + kRP, jj, Pr);
+      const double pvj = CORR ? L.pv()[k * 12 + jj] : rk[kRp + jj];
+      dpij = dot_bcast(Pr, dxj, pvj);
+      if (!el) dpij = 0.0;
+    }
+    if (el) {
+      L.du()[k * 12 + j] = duj;
+      L.dpi()[k * 12 + j] = dpij;
+    }
+    if (final_step) bad |= el && (huge(duj) || huge(dxj) || huge(dpij));
+    if (k < N && el) {
+      const Side s = side_u(Q, k, j);
+      const Bar b = ld_bar(L.bu() + k * 48, j);
+      double e1 = 0.0, e2 = 0.0;
+      if (CORR) {
+        const BarStep p = ld_step(L.su() + k * 48, j);
+        e1 = p.dll * p.dtl;
+        e2 = p.dlu * p.dtu;
+      }
+      const BarStep d = bar_step(s, b, L.u()[k * 12 + j], duj, e1, e2, CORR ? smu : 0.0);
+      ratio(s, b, d, ap, ad);
+      if (!CORR) aff_sums(s, b, d, s1, s2);
+      if (final_step) bad |= huge(d.dtl) || huge(d.dtu) || huge(d.dll) || huge(d.dlu);
+      st_step(L.su() + k * 48, j, d);
+    }
+    if (k > 0 && el) {
+      const Side s = side_x(Q, k, j);
+      const Bar b = ld_bar(L.bx() + k * 48, j);
+      double e1 = 0.0, e2 = 0.0;
+      if (CORR) {
+        const BarStep p = ld_step(L.sx() + k * 48, j);
+        e1 = p.dll * p.dtl;
+        e2 = p.dlu * p.dtu;
+      }
+      const BarStep d = bar_step(s, b, L.x()[k * 12 + j], dxj, e1, e2, CORR ? smu : 0.0);
+      ratio(s, b, d, ap, ad);
+      if (!CORR) aff_sums(s, b, d, s1, s2);
+      if (final_step) bad |= huge(d.dtl) || huge(d.dtu) || huge(d.dll) || huge(d.dlu);
+      st_step(L.sx() + k * 48, j, d);
+    }
+    for (int ch = 0; ch < L.nch; ++ch) {
+      const int r = ch * 12 + j;
+      const bool ok = el && r < a.ng;
+      double Dr[12], Cr[12];
+      load_strided(ok ? Q.Drow(k, r) : nullptr, a.ng, Dr);
+      load_strided(ok ? Q.Crow(k, r) : nullptr, a.ng, Cr);
+      const double dv = dot_bcast(Cr, dxj, dot_bcast(Dr, duj, 0.0));
+      if (ok) {
+        double* g = L.gb(k, ch);
+        const Side s = side_g(Q, k, r);
+        const Bar b = ld_bar(g, j);
+        double e1 = 0.0, e2 = 0.0;
+        if (CORR) {
+          const BarStep p = ld_step(g + 48, j);
+          e1 = p.dll * p.dtl;
+          e2 = p.dlu * p.dtu;
+        }
+        const BarStep d = bar_step(s, b, g[96 + j], dv, e1, e2, CORR ? smu : 0.0);
+        ratio(s, b, d, ap, ad);
+        if (!CORR) aff_sums(s, b, d, s1, s2);
+        if (final_step) bad |= huge(d.dtl) || huge(d.dtu) || huge(d.dll) || huge(d.dlu);
+        st_step(g + 48, j, d);
+      }
+    }
+  }
+  red_put(L, 0, g16min(ap));
+  red_put(L, 1, g16min(ad));
+  red_put(L, 2, g16sum(s1));
+  red_put(L, 3, g16sum(s2));
+  red_put(L, 4, g16max(bad ? 1.0 : 0.0));
+}
+
+// ---------------------------------------------------------------------------------------------
+// corrector right-hand side.  c_k = g~x_k + K_k' g~u_k + Acl_k' (P_k+1 b~_k) for every stage
+// (P_k+1 b~_k kept in dpi), then the recursion p_k = Acl_k' p_k+1 + c_k (wave 0), then per
+// stage g_k = B_k'(P_k+1 b~_k + p_k+1) + g~u_k, k_k = -(L L')^-1 g_k, bcl_k = b~_k + B_k k_k.
+// (The oracle's p_k = f + K'g with f = A'Pb + g~x, g = B'Pb + g~u, Pb = P b~ + p_k+1.)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void corr_rhs_stages(const Qp Q, const Lds L) {
+  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
+  const bool el = j < 12;
+  const int jj = el ? j : 11;
+  for (int k = grp; k <= N; k += kGroups) {
+    if (k == N) {
+      if (el) L.pv()[N * 12 + j] = L.gtx()[N * 12 + j];
+      continue;
+    }
+    double M[12];
+    load_packed_sym(Q.rec(k + 1) + kRP, jj, M);
+    const double bj = el ? L.rb()[k * 12 + j] : 0.0;
+    double pb = dot_bcast(M, bj, 0.0);
+    if (!el) pb = 0.0;
+    const double* rk = Q.rec(k);
+    sfor<0, 12>([&](auto i) { M[decltype(i)::value] = rk[kRK + decltype(i)::value * 13 + jj]; });
+    double ck = dot_bcast(M, el ? L.gtu()[k * 12 + j] : 0.0, el ? L.gtx()[k * 12 + j] : 0.0);
+    sfor<0, 12>([&](auto i) { M[decltype(i)::value] = L.acl()[k * 156 + decltype(i)::value * 13 + jj]; });
+    ck = dot_bcast(M, pb, ck);
+    if (el) {
+      L.dpi()[k * 12 + j] = pb;
+      L.pv()[k * 12 + j] = ck;
+    }
+  }
+}
+__device__ __forceinline__ void corr_rhs_chain(const Lds L, int N) {
+  if ((threadIdx.x >> 6) != 0) return;
+  const int c = opq(threadIdx.x & 15);
+  const bool cv = c < 12;
+  const int cc = cv ? c : 11;
+  double pv = cv ? L.pv()[N * 12 + c] : 0.0;
+  double M[12];
+  auto load_col = [&](int k, double (&C)[12]) {
+    sfor<0, 12>([&](auto i) { C[decltype(i)::value] = L.acl()[k * 156 + decltype(i)::value * 13 + cc]; });
+  };
+  load_col(N - 1, M);
+#pragma unroll 1
+  for (int k = N - 1; k >= 0; --k) {
+    double Mn[12];
+    if (k > 0) {
+      load_col(k - 1, Mn);
+    } else {
+      sfor<0, 12>([&](auto i) { Mn[decltype(i)::value] = 0.0; });
+    }
+    const double ck = cv ? L.pv()[k * 12 + c] : 0.0;
+    const double pn = dot_bcast(M, pv, ck);
+    pv = cv ? pn : 0.0;
+    if (threadIdx.x < 12) L.pv()[k * 12 + c] = pv;
+    sfor<0, 12>([&](auto i) { M[decltype(i)::value] = Mn[decltype(i)::value]; });
+  }
+}
+__device__ __forceinline__ void corr_k_stages(const Qp Q, const Lds L) {
+  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
+  const bool el = j < 12;
+  const int jj = el ? j : 11;
+  for (int k = grp; k < N; k += kGroups) {
+    double M[12];
+    load12(Q.B(k) + jj * 12, M);
+    const double w = el ? L.dpi()[k * 12 + j] + L.pv()[(k + 1) * 12 + j] : 0.0;
+    double gk = dot_bcast(M, w, el ? L.gtu()[k * 12 + j] : 0.0);
+    if (!el) gk = 0.0;
+    // k = -(L L')^-1 g: L's columns on lanes 0..11, the right-hand side on lane 12
+    const double* rk = Q.rec(k);
+    double Lc[12], Gv[12], Kc[12];
+    load_packed_lcol(rk + kRL, jj, Lc);
+    const double rs = rk[kRrs + jj];
+    sfor<0, 12>([&](auto i) { Gv[decltype(i)::value] = bc<decltype(i)::value>(gk); });
+    trsv_lower(Lc, rs, Gv);
+    trsv_upper_t_neg_axpy(Lc, rs, Gv, Kc);
+    double kk = 0.0;
+    sfor<0, 12>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      const double v = bc<12>(Kc[I]);
+      kk = j == I ? v : kk;
+    });
+    // bcl_k = b~_k + B_k k_k (row j of B)
+    load_strided(Q.B(k) + jj, 12, M);
+    const double bcl = dot_bcast(M, kk, el ? L.rb()[k * 12 + j] : 0.0);
+    if (el) {
+      L.kv()[k * 12 + j] = kk;
+      L.acl()[k * 156 + j * 13 + 12] = bcl;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase: apply the step (alpha_p on x, u, t; alpha_d on pi, lam)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void update(const Qp Q, const Lds L, double ap, double ad) {
+  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
+  if (j >= 12) return;
+  for (int k = grp; k <= N; k += kGroups) {
+    if (k < N) L.u()[k * 12 + j] = stepv(L.u()[k * 12 + j], ap, L.du()[k * 12 + j]);
+    if (k > 0) {
+      L.x()[k * 12 + j] = stepv(L.x()[k * 12 + j], ap, L.dx()[k * 12 + j]);
+      L.pi()[k * 12 + j] = stepv(L.pi()[k * 12 + j], ad, L.dpi()[k * 12 + j]);
+    }
+    auto upd = [&](double* bp, const double* sp) {
+      Bar b = ld_bar(bp, j);
+      const BarStep d = ld_step(sp, j);
+      b.tl = stepv(b.tl, ap, d.dtl);
+      b.tu = stepv(b.tu, ap, d.dtu);
+      b.ll = stepv(b.ll, ad, d.dll);
+      b.lu = stepv(b.lu, ad, d.dlu);
+      st_bar(bp, j, b);
+    };
+    upd(L.bu() + k * 48, L.su() + k * 48);
+    upd(L.bx() + k * 48, L.sx() + k * 48);
+    for (int ch = 0; ch < L.nch; ++ch) {
+      double* g = L.gb(k, ch);
+      upd(g, g + 48);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase: outputs (ipm_box_impl.h kPhOut): x, u, pi with the stage-0 rebuild
+// pi_0 = Q0 x0 + S0'u0 + q0 + A0'(P_1 res_b0 + pi_1) (ocp_qp_ipm_solver.cpp:347-373), and the
+// Riccati getters of the last factorization: P, K; p = pi - P x, k = u - K x
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void outputs(const Qp Q, const Lds L) {
+  const ProblemArgsT<double>& a = Q.a;
+  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
+  const bool el = j < 12;
+  const int jj = el ? j : 11;
+  const size_t q = (size_t)Q.q;
+  for (int k = grp; k <= N; k += kGroups) {
+    const double* rk = Q.rec(k);
+    const double xj = el ? L.x()[k * 12 + j] : 0.0;
+    const double uj = (el && k < N) ? L.u()[k * 12 + j] : 0.0;
+    double pij = el ? L.pi()[k * 12 + j] : 0.0;
+    if (k == 0) {
+      double M[12];
+      load_packed_sym(Q.rec(1) + kRP, jj, M);
+      double t = dot_bcast(M, el ? L.rb()[j] : 0.0, el ? L.pi()[12 + j] : 0.0);
+      if (!el) t = 0.0;
+      load12(Q.Q(0) + jj * 12, M);
+      double p0 = dot_bcast(M, xj, el ? Q.qv(0)[j] : 0.0);
+      load12(Q.S(0) + jj * 12, M);
+      p0 = dot_bcast(M, uj, p0);
+      load12(Q.A(0) + jj * 12, M);
+      p0 = dot_bcast(M, t, p0);
+      pij = el ? p0 : 0.0;
+    }
+    if (el) {
+      a.x[(q * (N + 1) + k) * 12 + j] = xj;
+      a.pi[(q * (N + 1) + k) * 12 + j] = pij;
+      if (k < N) a.u[(q * N + k) * 12 + j] = uj;
+    }
+    if (a.P || a.p) {
+      double Pr[12];
+      load_packed_sym(rk + kRP, jj, Pr);
+      const double px = dot_bcast(Pr, xj, 0.0);
+      if (el && a.P) store12(a.P + (q * (N + 1) + k) * 144 + (size_t)j * 12, Pr);
+      if (el && a.p) a.p[(q * (N + 1) + k) * 12 + j] = pij - px;
+    }
+    if (k < N && (a.K || a.k)) {
+      double Kr[12];
+      sfor<0, 12>([&](auto i) { Kr[decltype(i)::value] = rk[kRK + jj * 13 + decltype(i)::value]; });
+      const double kx = dot_bcast(Kr, xj, 0.0);
+      if (el && a.k) a.k[(q * N + k) * 12 + j] = uj - kx;
+      if (el && a.K) {
+        double Kc[12];
+        sfor<0, 12>([&](auto i) { Kc[decltype(i)::value] = rk[kRK + decltype(i)::value * 13 + j]; });
+        store12(a.K + (q * N + k) * 144 + (size_t)j * 12, Kc);
+      }
+    }
+  }
+}
+
+template <bool HAS_C>
+__global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<double> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  const int N = a.N;
+  const int nch = (a.ng + 11) / 12;
+  const Lds L = carve(reinterpret_cast<double*>(lds_raw), N, nch);
+  const Qp Q{a, (int)blockIdx.x, N};
+  const bool t0 = threadIdx.x == 0;
+  double* const stat = a.stat ? a.stat + (size_t)Q.q * a.stat_rows * kStatCols : nullptr;
+
+  init_point(Q, L);
+  __syncthreads();
+  const double nc = red_sum(L, 0);
+  const double nc_inv = nc > 0.0 ? 1.0 / nc : 0.0;
+  double last_amin = 1.0, res_g = 0.0, res_b = 0.0, res_d = 0.0, res_m = 0.0, obj = 0.0;
+  int iter = 0, status = -1;
+#pragma unroll 1
+  for (;;) {
+    __syncthreads();  // (red reuse)
+    residuals(Q, L);
+    __syncthreads();
+    res_g = red_max(L, 0);
+    res_b = red_max(L, 1);
+    res_d = red_max(L, 2);
+    res_m = red_max(L, 3);
+    const double musum = red_sum(L, 4);
+    obj = red_sum(L, 5);
+    const double mu = musum * nc_inv;
+    if (stat && t0) {
+      double* row = stat + (size_t)iter * kStatCols;
+      row[5] = mu;
+      row[6] = res_g;
+      row[7] = res_b;
+      row[8] = res_d;
+      row[9] = res_m;
+      row[10] = obj;
+    }
+    // exit test (HPIPM order: NaN / converged / iter_max / min step)
+    if (!(res_g == res_g) || !(res_b == res_b) || !(res_d == res_d) || !(res_m == res_m) || !(mu == mu) ||
+        res_g == __builtin_inf() || res_b == __builtin_inf()) {
+      status = 3;
+    } else if (res_g <= a.tol_stat && res_b <= a.tol_eq && res_d <= a.tol_ineq && res_m <= a.tol_comp) {
+      status = 0;
+    } else if (iter >= a.iter_max) {
+      status = 1;
+    } else if (iter > 0 && last_amin < a.alpha_min) {
+      status = 2;
+    }
+    if (status >= 0) break;
+    double* const next = (stat && t0) ? stat + (size_t)(iter + 1) * kStatCols : nullptr;
+
+    // ---- predictor ----
+    barrier_terms<false, HAS_C>(Q, L, 0.0);
+    __syncthreads();
+    factorize(Q, L);
+    __syncthreads();
+    forward(L, N);
+    __syncthreads();
+    const bool pc = a.pred_corr != 0;
+    step_pass<false>(Q, L, 0.0, !pc);
+    __syncthreads();
+    double ap = red_min(L, 0), ad = red_min(L, 1);
+    bool bad = red_max(L, 4) > 0.0;
+    if (pc) {
+      const double aa = fmin(1.0, fmin(ap, ad));
+      const double S1 = red_sum(L, 2), S2 = red_sum(L, 3);
+      const double mu_aff = (musum + aa * (S1 + aa * S2)) * nc_inv;
+      double sg = mu > 0.0 ? mu_aff / mu : 0.0;
+      sg = sg * sg * sg;
+      if (sg > 1.0) sg = 1.0;
+      const double smu = sg * mu;
+      if (next) {
+        next[0] = aa;
+        next[1] = mu_aff;
+        next[2] = sg;
+      }
+      // ---- corrector: same factors, new gradient ----
+      __syncthreads();
+      barrier_terms<true, HAS_C>(Q, L, smu);
+      __syncthreads();
+      corr_rhs_stages(Q, L);
+      __syncthreads();
+      corr_rhs_chain(L, N);
+      __syncthreads();
+      corr_k_stages(Q, L);
+      __syncthreads();
+      forward(L, N);
+      __syncthreads();
+      step_pass<true>(Q, L, smu, true);
+      __syncthreads();
+      ap = red_min(L, 0);
+      ad = red_min(L, 1);
+      bad = red_max(L, 4) > 0.0;
+    }
+    if (bad) {
+      ap = 0.0;
+      ad = 0.0;
+    }
+    if (!a.split_step) {
+      ap = fmin(ap, ad);
+      ad = ap;
+    }
+    const double alpha_p = fmin(1.0, kTau * ap), alpha_d = fmin(1.0, kTau * ad);
+    if (next) {
+      next[3] = alpha_p;
+      next[4] = alpha_d;
+    }
+    last_amin = fmin(alpha_p, alpha_d);
+    update(Q, L, alpha_p, alpha_d);
+    ++iter;
+  }
+  // converged at the initial point: the factorization of the returned iterate (HPIPM getters)
+  if (iter == 0 && status != 3) {
+    barrier_terms<false, HAS_C>(Q, L, 0.0);
+    __syncthreads();
+    factorize(Q, L);
+  }
+  __syncthreads();
+  outputs(Q, L);
+  if (t0) {
+    if (a.status) a.status[Q.q] = status;
+    if (a.iter) a.iter[Q.q] = nc > 0.0 ? iter : 0;
+    if (a.res) {
+      a.res[(size_t)Q.q * 4 + 0] = res_g;
+      a.res[(size_t)Q.q * 4 + 1] = res_b;
+      a.res[(size_t)Q.q * 4 + 2] = res_d;
+      a.res[(size_t)Q.q * 4 + 3] = res_m;
+    }
+    if (a.obj) a.obj[Q.q] = obj;
+  }
+}
+
+}  // namespace ipm_lat
+
+bool ipm_latency_ok(const ProblemArgsT<double>& a, int max_batch) {
+  if (a.batch < 1 || a.batch > max_batch) return false;
+  if (a.nx != 12 || a.nu != 12 || a.N < 1) return false;
+  if (a.ric_alg || a.itref_corr_max || a.lq_fact || a.warm_start > 1 || a.warm_bars || a.skip_last_rb)
+    return false;
+  const int nch = (a.ng + 11) / 12;
+  if (ipm_lat::lds_doubles(a.N, nch) * sizeof(double) > 160 * 1024) return false;
+  return a.ws && a.ws_qp >= (size_t)(a.N + 1) * ipm_lat::kRStage;
+}
+
+hipError_t launch_ipm_latency(const ProblemArgsT<double>& a, hipStream_t stream) {
+  const int nch = (a.ng + 11) / 12;
+  const size_t bytes = ipm_lat::lds_doubles(a.N, nch) * sizeof(double);
+  auto go = [&](auto kern) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(a.batch), dim3(ipm_lat::kThreads), bytes, stream, a);
+    return hipGetLastError();
+  };
+  return (a.C && a.ng > 0) ? go(&ipm_lat::ipm_latency_kernel<true>) : go(&ipm_lat::ipm_latency_kernel<false>);
+}
+
+}  // namespace srbd

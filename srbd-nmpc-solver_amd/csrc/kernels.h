@@ -121,6 +121,12 @@ constexpr int kGenChunk = 112;
 constexpr int kGenVec = 36;
 
 size_t ws_doubles_ipm(int N, int ng);  // elements per QP (either precision)
+// The one-launch latency IPM (ipm_latency.hip): fp64, classical Riccati, no refinement, up to
+// max_batch QPs (one workgroup each).  ipm_latency_ok says whether `a` runs there.
+constexpr int kIpmLatencyMaxBatch = 512;
+int ipm_latency_max_batch();
+bool ipm_latency_ok(const ProblemArgsT<double>& a, int max_batch);
+hipError_t launch_ipm_latency(const ProblemArgsT<double>& a, hipStream_t stream);
 template <typename T>
 hipError_t launch_ipm_box(const ProblemArgsT<T>& a, hipStream_t stream);
 

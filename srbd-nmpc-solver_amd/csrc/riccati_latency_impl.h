@@ -36,16 +36,12 @@
 // d_ocp_qp_fact_solve_kkt_unconstr), another summation order: the outputs match the batched
 // kernel's to rounding (tests/test_gpu_riccati.py), not bit for bit.
 
-typedef double lat_d4 __attribute__((ext_vector_type(4)));
-
 constexpr int kLatThreads = 512;  // wave 0: factorization, wave 1: records, all: the passes
 constexpr int kLatTile = 156;     // 13 columns x 12 rows, column-major (ld 12)
 constexpr int kLatL = 90;         // packed L (78) + 1 / diag (12)
 constexpr int kLatAcl = 156;      // [Acl | bcl]: 12 rows of 13
 
-__device__ __forceinline__ lat_d4 lat_mfma(double a, double b, lat_d4 c) {
-  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
+// (lat_d4, lat_mfma, lat_recip, lat_chol: mfma_lat.h, shared with ipm_latency.hip)
 
 // LDS of the kernel (doubles): the image, the closed-loop rows, then a region the backward
 // sweep uses as scratch (the G / H tile, two Y tiles and two L factors, double-buffered for
@@ -56,47 +52,8 @@ __host__ __device__ constexpr int lat_scr_size(int N) {
   return (3 * N + 2) * 12 > 3 * kLatTile + 2 * kLatL ? (3 * N + 2) * 12 : 3 * kLatTile + 2 * kLatL;
 }
 size_t lat_lds_bytes(int N) { return (size_t)(lat_scr_off(N) + lat_scr_size(N)) * sizeof(double); }
-
-// Column-owned Cholesky with the pivots' reciprocals by v_rcp_f64 and two Newton steps
-// (3 dependent FMAs instead of the IEEE division's ~10 instructions on the stage's critical
-// path); otherwise chol_cols (riccati.h): `reg` on each pivot, a non-positive pivot zeroes
-// its column (BLASFEO dpotrf_l).
-// (one Newton step measured within the call pattern's noise, 99.0 / 99.8 vs 100.2 / 99.9 us;
-// streaming the stages into LDS during the sweep measured slower: DESIGN.md 9.1)
-__device__ __forceinline__ double lat_recip(double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  double e = __builtin_fma(-d, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-d, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  return r;
-}
-// `hook(ic<K>)` runs at the top of pivot K: the caller issues its independent matrix-core
-// work there, one MFMA per pivot, so the MFMA pipe runs beside the pivots' VALU chain
-// instead of ahead of it (a wave cannot issue past an MFMA the pipe has not accepted).
-template <typename Hook>
-__device__ __forceinline__ void lat_chol(double (&G)[12], const int lane, const double reg, double (&Lc)[12],
-                                         double& rs, Hook&& hook) {
-  double dmine = 1.0;
-  sfor<0, 12>([&](auto kk) {
-    constexpr int K = decltype(kk)::value;
-    hook(kk);
-    const double dk = bc<K>(G[K]) + reg;
-    const double inv = dk > 0.0 ? lat_recip(dk) : 0.0;
-    const double s = lane > K ? G[K] * inv : 0.0;
-    sfor<K + 1, 12>([&](auto i) {
-      constexpr int I = decltype(i)::value;
-      G[I] = fmadd(-bc<K>(G[I]), s, G[I]);
-    });
-    dmine = lane == K ? dk : dmine;
-  });
-  double inv_l;
-  pivot_rs(dmine, rs, inv_l);
-  sfor<0, 12>([&](auto i) {
-    constexpr int I = decltype(i)::value;
-    Lc[I] = G[I] * inv_l;
-  });
-}
+// (one Newton step in lat_recip measured within the call pattern's noise, 99.0 / 99.8 vs
+// 100.2 / 99.9 us; streaming the stages into LDS during the sweep measured slower: DESIGN.md 9.1)
 
 template <bool RES>
 __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(ProblemArgsT<double> a) {

@@ -19,6 +19,7 @@
 // rebuild (K0 = -G0^-1 H0, P0 = Q0 - H0'G0^-1 H0 + A0'P1 A0, ...).
 #include "kernels.h"
 #include "riccati.h"
+#include "mfma_lat.h"
 
 #define SRBD_REAL double
 #define SRBD_NS ric_f64

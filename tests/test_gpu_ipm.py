@@ -188,9 +188,10 @@ def test_general_constraints_vs_oracle(pkg, oracle, dims, ric_alg):
         assert helpers.is_approx(out["pi"][i, 1:], ref["pi"][i, 1:], 1e-6), ("pi", i)
 
 
-@pytest.mark.parametrize("ric_alg,mode,min_ok", [(0, "Speed", 63), (1, "Speed", 44),
-                                                 (0, "Balance", 64), (1, "Balance", 64)])
-def test_degenerate_endgame_family(pkg, oracle, ric_alg, mode, min_ok):
+@pytest.mark.parametrize("ric_alg,mode,min_ok,path", [(0, "Speed", 63, "batched"), (0, "Speed", 60, "latency"),
+                                                      (1, "Speed", 44, "auto"), (0, "Balance", 64, "auto"),
+                                                      (1, "Balance", 64, "auto")])
+def test_degenerate_endgame_family(pkg, oracle, ric_alg, mode, min_ok, path, monkeypatch):
     """The near-degenerate QP above (#12 of (12, 4, 14) seed 200) as 64 copies with Q, R, S,
     A, B, q, r, b perturbed at 1e-15 relative.  Without iterative refinement (Speed) whether a
     copy converges is a race between res_comp falling and the unrefined step's linear residual
@@ -200,7 +201,14 @@ def test_degenerate_endgame_family(pkg, oracle, ric_alg, mode, min_ok):
     GPU on 64 and 48.  The count of the square-root variant is held to the oracle's within 8
     (equivalent summation orders move it by about that much).  With HPIPM's refinement of the
     corrector (Balance: 2 corrections at most) both converge on 64 / 64.  The x, u
-    of every copy are held to the oracle's at 1e-6 (converged) or 1e-3 (min step)."""
+    of every copy are held to the oracle's at 1e-6 (converged) or 1e-3 (min step).  Speed with
+    ric_alg 0 runs on both IPM paths: the batched kernels (SRBD_IPM_LATENCY_MAX=0) and the
+    one-launch latency IPM (ipm_latency.hip, the default for 64 QPs), whose matrix-core
+    factorization sums in another order."""
+    if path == "batched":
+        monkeypatch.setenv("SRBD_IPM_LATENCY_MAX", "0")
+    elif path == "latency":
+        monkeypatch.setenv("SRBD_IPM_LATENCY_MAX", "512")
     qp, x0 = helpers.random_constrained(20, 12, 12, 4, 14, 200, pkg.OcpQpBatch)
     M = 64
     rng = np.random.default_rng(7)
