@@ -767,6 +767,7 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
 #pragma unroll 1
   for (int k = N - 1; k >= 0; --k) {
     if (wave == 0) {
+      tstamp(70);
       const double* sl = slot(k);
       double bo[3], ao[3];
       sfor<0, 3>([&](auto kb) {
@@ -822,7 +823,9 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
         const double v = gh[cc * 12 + decltype(i)::value];
         Gc[decltype(i)::value] = cv ? v : 0.0;
       });
-      lat_chol<true>(Gc, c, a.reg, Lc, rs, wh);
+      tstamp(71);
+      lat_chol(Gc, c, a.reg, Lc, rs, wh);
+      tstamp(72);
       // [Y | y] = L^-1 [H | g]
       lds_wave_fence();
       sfor<0, 3>([&](auto rr) {
@@ -836,6 +839,7 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
         Yc[decltype(i)::value] = cw ? v : 0.0;
       });
       trsv_lower(Lc, rs, Yc);
+      tstamp(73);
       double* yb = ybuf + (k & 1) * 156;
       double* lb = lbuf + (k & 1) * 90;
       if (l < 16) {
@@ -846,17 +850,19 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
         }
       }
       lds_wave_fence();
-      // [P | p]_k = [F | f] + K'[H | g], K = -L^-T Y, P symmetrized by averaging: the oracle's
-      // and the batched kernels' form (ipm_box_impl.h).  The unconstrained
-      // kernel's F - Y'Y stalls the stationarity residual near 3e-7 on QPs whose barrier terms
-      // reach ~1e10 in the endgame (random C / D rows, tests/test_gpu_ipm_latency.py).
-      double Kc[12];
-      trsv_upper_t_neg_axpy(Lc, rs, Yc, Kc);  // lane c < 12: K[:, c]
+      // [P | p]_k = [F | f] - Y'[Y | y], P symmetrized by averaging (the oracle's and the batched
+      // kernels' symmetrization): unsymmetrized, the next stage's products read P
+      // as A operand (P') and as B operand (P), and the endgame stalls the stationarity residual
+      // near 3e-7 on QPs whose barrier terms reach ~1e10 (random C / D rows), 61 / 64 on the
+      // degenerate family; symmetrized 64 / 64.  (F + K'H with K = -L^-T Y on the chain, the
+      // batched kernels' form, measured 61 / 64 here and 4% slower.)
       lat_d4 Pn = Ft;
       sfor<0, 3>([&](auto kb) {
         constexpr int KB = decltype(kb)::value;
-        const double kv = g == 0 ? Kc[4 * KB] : g == 1 ? Kc[4 * KB + 1] : g == 2 ? Kc[4 * KB + 2] : Kc[4 * KB + 3];
-        Pn = lat_mfma(cv ? kv : 0.0, Ht[KB], Pn);  // A operand (K')[c][4 KB + g] = K[4 KB + g][c]
+        const double yv = yb[(cw ? c : 12) * 12 + 4 * KB + g];
+        const double yB = cw ? yv : 0.0;
+        const double yA = cv ? -yv : 0.0;
+        Pn = lat_mfma(yA, yB, Pn);
       });
       sfor<0, 3>([&](auto rr) {
         constexpr int R = decltype(rr)::value;
@@ -869,6 +875,7 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
         if (cv) Pn[R] = 0.5 * (Pn[R] + t);
       });
       lds_wave_fence();
+      tstamp(75);
       Pt = Pn;
       double* rk = Q.rec(k);
       sfor<0, 3>([&](auto rr) {
@@ -1204,8 +1211,10 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
   const bool t0 = threadIdx.x == 0;
   double* const stat = a.stat ? a.stat + (size_t)Q.q * a.stat_rows * kStatCols : nullptr;
 
+  tstamp(63);
   init_point(Q, L);
   __syncthreads();
+  tstamp(64);
   const double nc = red_sum(L, 0);
   const double nc_inv = nc > 0.0 ? 1.0 / nc : 0.0;
   double last_amin = 1.0, res_g = 0.0, res_b = 0.0, res_d = 0.0, res_m = 0.0, obj = 0.0;
@@ -1213,8 +1222,10 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
 #pragma unroll 1
   for (;;) {
     __syncthreads();  // (red reuse)
+    tstamp(50);
     residuals(Q, L);
     __syncthreads();
+    tstamp(51);
     res_g = red_max(L, 0);
     res_b = red_max(L, 1);
     res_d = red_max(L, 2);
@@ -1248,13 +1259,17 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
     // ---- predictor ----
     barrier_terms<false, HAS_C>(Q, L, 0.0);
     __syncthreads();
+    tstamp(52);
     factorize(Q, L);
     __syncthreads();
+    tstamp(53);
     forward(L, N);
     __syncthreads();
+    tstamp(54);
     const bool pc = a.pred_corr != 0;
     step_pass<false>(Q, L, 0.0, !pc);
     __syncthreads();
+    tstamp(55);
     double ap = red_min(L, 0), ad = red_min(L, 1);
     bool bad = red_max(L, 4) > 0.0;
     if (pc) {
@@ -1274,16 +1289,22 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
       __syncthreads();
       barrier_terms<true, HAS_C>(Q, L, smu);
       __syncthreads();
+      tstamp(56);
       corr_rhs_stages(Q, L);
       __syncthreads();
+      tstamp(57);
       corr_rhs_chain(L, N);
       __syncthreads();
+      tstamp(58);
       corr_k_stages(Q, L);
       __syncthreads();
+      tstamp(59);
       forward(L, N);
       __syncthreads();
+      tstamp(60);
       step_pass<true>(Q, L, smu, true);
       __syncthreads();
+      tstamp(61);
       ap = red_min(L, 0);
       ad = red_min(L, 1);
       bad = red_max(L, 4) > 0.0;
@@ -1303,6 +1324,7 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
     }
     last_amin = fmin(alpha_p, alpha_d);
     update(Q, L, alpha_p, alpha_d);
+    tstamp(62);
     ++iter;
   }
   // converged at the initial point: the factorization of the returned iterate (HPIPM getters)
@@ -1312,7 +1334,10 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
     factorize(Q, L);
   }
   __syncthreads();
+  tstamp(65);
   outputs(Q, L);
+  __syncthreads();
+  tstamp(66);
   if (t0) {
     if (a.status) a.status[Q.q] = status;
     if (a.iter) a.iter[Q.q] = nc > 0.0 ? iter : 0;
@@ -1352,3 +1377,19 @@ hipError_t launch_ipm_latency(const ProblemArgsT<double>& a, hipStream_t stream)
 }
 
 }  // namespace srbd
+
+#if SRBD_TSTAMP
+// Diagnostic builds only: this translation unit's stamp buffer (the latency IPM), as
+// srbd_qp_diag_tstamps does for the unconstrained kernels.
+extern "C" int srbd_qp_diag_tstamps_lat(unsigned long long* out, int cap) {
+  unsigned n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(srbd::g_tstamp_n), sizeof n) != hipSuccess) return -1;
+  if (n > (unsigned)srbd::kTstampCap) n = srbd::kTstampCap;
+  if ((int)n > cap) n = (unsigned)cap;
+  if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(srbd::g_tstamp), 2 * sizeof(unsigned long long) * n) != hipSuccess)
+    return -1;
+  const unsigned zero = 0;
+  hipMemcpyToSymbol(HIP_SYMBOL(srbd::g_tstamp_n), &zero, sizeof zero);
+  return (int)n;
+}
+#endif

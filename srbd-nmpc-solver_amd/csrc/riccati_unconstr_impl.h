@@ -254,22 +254,6 @@ __device__ __forceinline__ void fwd_sweep(const ProblemArgsT<real>& a, const Src
   }
 }
 
-#ifndef SRBD_DATA_NT
-#define SRBD_DATA_NT 0
-#endif
-// A/B switch: data blocks read with non-temporal loads from HBM (1: Q, S, R, q, r, which only
-// the backward sweep reads; 2: also A, B, b of stages >= kRecHotStages)
-template <class Src>
-__device__ __forceinline__ void load_blk(const real* p, real (&v)[12], bool nt) {
-  if constexpr (std::is_same_v<Src, HbmSrc>) {
-    if (nt) {
-      load12_nt(p, v);
-      return;
-    }
-  }
-  load12(p, v);
-}
-
 // ---- the solve of one QP by its 16-lane group, blocks and records through `src` ----
 // SQRT: ric_alg = 1, the square-root recursion (riccati.h riccati_step_sqrt); the records
 // and outputs are the same (P_k = F - Y'Y of the stage, which Lx factors).
@@ -298,29 +282,27 @@ __device__ __forceinline__ void solve_qp(const ProblemArgsT<real>& a, const Src&
 #pragma unroll 1
   for (int k = N - 1; k >= 0; --k) {
     // A, B (VL: b) of stage k, column-owned
-    constexpr bool ntq = SRBD_DATA_NT >= 1;
-    const bool nta = SRBD_DATA_NT >= 2 && k >= kRecHotStages;
     if (isv) {
-      load_blk<Src>(src.b(k), A_, nta);
+      load12(src.b(k), A_);
       sfor<0, 12>([&](auto i) { B_[decltype(i)::value] = real(0.0); });
     } else {
-      load_blk<Src>(src.A(k) + col * 12, A_, nta);
-      load_blk<Src>(src.B(k) + col * 12, B_, nta);
+      load12(src.A(k) + col * 12, A_);
+      load12(src.B(k) + col * 12, B_);
     }
     auto loadR = [&](real (&Rc)[12]) {
       if (isv) {
         sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] = real(0.0); });
       } else {
-        load_blk<Src>(src.R(k) + col * 12, Rc, ntq);
+        load12(src.R(k) + col * 12, Rc);
       }
     };
     auto loadSQ = [&](real (&Sc)[12], real (&Qc)[12]) {
       if (isv) {
-        load_blk<Src>(src.r(k), Sc, ntq);
-        load_blk<Src>(src.q(k), Qc, ntq);
+        load12(src.r(k), Sc);
+        load12(src.q(k), Qc);
       } else {
-        load_blk<Src>(src.S(k) + col * 12, Sc, ntq);
-        load_blk<Src>(src.Q(k) + col * 12, Qc, ntq);
+        load12(src.S(k) + col * 12, Sc);
+        load12(src.Q(k) + col * 12, Qc);
       }
     };
     StageFactor<real> f;

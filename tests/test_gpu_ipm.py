@@ -188,7 +188,7 @@ def test_general_constraints_vs_oracle(pkg, oracle, dims, ric_alg):
         assert helpers.is_approx(out["pi"][i, 1:], ref["pi"][i, 1:], 1e-6), ("pi", i)
 
 
-@pytest.mark.parametrize("ric_alg,mode,min_ok,path", [(0, "Speed", 63, "batched"), (0, "Speed", 60, "latency"),
+@pytest.mark.parametrize("ric_alg,mode,min_ok,path", [(0, "Speed", 63, "batched"), (0, "Speed", 63, "latency"),
                                                       (1, "Speed", 44, "auto"), (0, "Balance", 64, "auto"),
                                                       (1, "Balance", 64, "auto")])
 def test_degenerate_endgame_family(pkg, oracle, ric_alg, mode, min_ok, path, monkeypatch):
