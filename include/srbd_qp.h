@@ -248,7 +248,14 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device,
  * that settings->f64_rescue / f32_iters wait once for their first pass.
  * Every data/solution pointer is device memory.  With settings->warm_start the
  * x/u buffers are read as the warm start.  One handle serves one solve at a
- * time (its workspace); several handles run concurrently.                  */
+ * time (its workspace); several handles run concurrently.
+ * Cost of the asynchronous stop: the batched IPM enqueues all iter_max
+ * iterations up front; the iterations after the device has stopped the solve
+ * cost their dispatch only (about 2 to 6 launches per iteration, a few
+ * microseconds each, so ~0.1 ms for the NMPC's iter_max 30).  fp64 Speed solves
+ * with the classical Riccati (ric_alg 0) of up to 512 QPs run as one launch
+ * instead (the latency IPM), which stops where it converges.
+ * SRBD_IPM_LATENCY_MAX (environment, QPs; 0 = off) moves that switch.     */
 int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
                       const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol,
                       void* stream);

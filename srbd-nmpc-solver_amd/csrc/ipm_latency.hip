@@ -1364,16 +1364,27 @@ bool ipm_latency_ok(const ProblemArgsT<double>& a, int max_batch) {
 }
 
 hipError_t launch_ipm_latency(const ProblemArgsT<double>& a, hipStream_t stream) {
+  // (the LDS limit is set once per device: prepare_ipm_latency_device, srbd_qp_create)
   const int nch = (a.ng + 11) / 12;
   const size_t bytes = ipm_lat::lds_doubles(a.N, nch) * sizeof(double);
-  auto go = [&](auto kern) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(a.batch), dim3(ipm_lat::kThreads), bytes, stream, a);
-    return hipGetLastError();
-  };
-  return (a.C && a.ng > 0) ? go(&ipm_lat::ipm_latency_kernel<true>) : go(&ipm_lat::ipm_latency_kernel<false>);
+  if (a.C && a.ng > 0) {
+    hipLaunchKernelGGL(ipm_lat::ipm_latency_kernel<true>, dim3(a.batch), dim3(ipm_lat::kThreads), bytes, stream, a);
+  } else {
+    hipLaunchKernelGGL(ipm_lat::ipm_latency_kernel<false>, dim3(a.batch), dim3(ipm_lat::kThreads), bytes, stream, a);
+  }
+  return hipGetLastError();
+}
+
+// Per-device attribute (hipFuncSetAttribute costs tens of microseconds: once per handle, on
+// the handle's device, like prepare_riccati_device)
+hipError_t prepare_ipm_latency_device() {
+  constexpr int kBytes = 160 * 1024;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<true>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, kBytes);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kBytes);
+  return e;
 }
 
 }  // namespace srbd

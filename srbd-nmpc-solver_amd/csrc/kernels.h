@@ -127,6 +127,7 @@ constexpr int kIpmLatencyMaxBatch = 512;
 int ipm_latency_max_batch();
 bool ipm_latency_ok(const ProblemArgsT<double>& a, int max_batch);
 hipError_t launch_ipm_latency(const ProblemArgsT<double>& a, hipStream_t stream);
+hipError_t prepare_ipm_latency_device();  // srbd_qp_create, on the handle's device
 template <typename T>
 hipError_t launch_ipm_box(const ProblemArgsT<T>& a, hipStream_t stream);
 

@@ -195,6 +195,7 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srb
   h->ws_bytes = h->ws_qp * sizeof(double) * (size_t)batch_capacity;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = srbd::prepare_riccati_device();  // per-device kernel attributes
+  if (e == hipSuccess) e = srbd::prepare_ipm_latency_device();
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&h->ws), h->ws_bytes);
   if (e == hipSuccess && constrained(*dims)) {
     e = hipMalloc(reinterpret_cast<void**>(&h->ctl), sizeof(int) * srbd::kCtlInts);

@@ -10,12 +10,36 @@
 #include "hpipm-cpp/ocp_qp_ipm_solver.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <string>
 
 #include "srbd_qp.h"
+
+namespace {
+// SRBD_SHIM_PROFILE=1: host time of the staged one-QP path by piece (staging pointers, packing,
+// the C-ABI solve, unpacking), summed over the process and printed to stderr at exit.
+struct ShimProfile {
+  bool on = std::getenv("SRBD_SHIM_PROFILE") != nullptr;
+  double t[4] = {0, 0, 0, 0};
+  long n = 0;
+  ~ShimProfile() {
+    if (on && n)
+      std::fprintf(stderr, "{\"shim_profile_us\": {\"calls\": %ld, \"staging\": %.2f, \"pack\": %.2f, "
+                           "\"solve_host\": %.2f, \"unpack\": %.2f}}\n",
+                   n, t[0] / n, t[1] / n, t[2] / n, t[3] / n);
+  }
+};
+ShimProfile g_prof;
+using PClock = std::chrono::steady_clock;
+inline double us_since(PClock::time_point t0) {
+  return std::chrono::duration<double, std::micro>(PClock::now() - t0).count();
+}
+}  // namespace
 
 namespace hpipm {
 
@@ -544,7 +568,9 @@ std::vector<HpipmStatus> OcpQpIpmSolver::solveBatch(
     d.A = d.B = d.b = d.Q = d.S = d.R = d.q = d.r = d.x0 = mk;
     o.x = o.u = o.pi = o.P = o.p = o.K = o.k = o.res = o.obj = o.stat = mo;
     o.status = o.iter = reinterpret_cast<int*>(16);
+    auto tp = PClock::now();
     staged = srbd_qp_host_staging_f64(m.handle, nb, &st, &d, &o) == SRBD_QP_OK;
+    if (g_prof.on) g_prof.t[0] += us_since(tp);
     if (staged) {
       Impl::Bufs bs;
       bs.A = const_cast<double*>(d.A); bs.B = const_cast<double*>(d.B); bs.b = const_cast<double*>(d.b);
@@ -552,10 +578,20 @@ std::vector<HpipmStatus> OcpQpIpmSolver::solveBatch(
       bs.q = const_cast<double*>(d.q); bs.r = const_cast<double*>(d.r); bs.x0 = const_cast<double*>(d.x0);
       bs.x = o.x; bs.u = o.u; bs.pi = o.pi; bs.P = o.P; bs.p = o.p; bs.K = o.K; bs.k = o.k;
       bs.res = o.res; bs.obj = o.obj; bs.stat = o.stat; bs.status = o.status; bs.iter = o.iter;
+      tp = PClock::now();
       m.pack(x0, ocp_qp, m.settings.warm_start ? &qp_sol : nullptr, &bs);
+      if (g_prof.on) g_prof.t[1] += us_since(tp);
+      tp = PClock::now();
       if (srbd_qp_solve_host_f64(m.handle, nb, &st, &d, &o) != SRBD_QP_OK)
         abi_error("OcpQpIpmSolver::solve");
-      return m.unpack(qp_sol);
+      if (g_prof.on) g_prof.t[2] += us_since(tp);
+      tp = PClock::now();
+      std::vector<HpipmStatus> res = m.unpack(qp_sol);
+      if (g_prof.on) {
+        g_prof.t[3] += us_since(tp);
+        ++g_prof.n;
+      }
+      return res;
     }
     d = srbd_qp_data_f64{};
     o = srbd_qp_solution_f64{};
