@@ -744,11 +744,8 @@ bool use_lds_kernel(const ProblemArgsT<real>& a) {
 }
 
 // The fp64 classical solve of small batches runs on the matrix-core latency kernel
-// (riccati_latency_impl.h; -DSRBD_LATENCY_MFMA=0 builds without it).
-#ifndef SRBD_LATENCY_MFMA
-#define SRBD_LATENCY_MFMA 1
-#endif
-#if SRBD_WITH_LATENCY && SRBD_LATENCY_MFMA
+// (riccati_latency_impl.h).
+#if SRBD_WITH_LATENCY
 #include "riccati_latency_impl.h"
 bool lat_eligible(const ProblemArgsT<real>& a) { return use_lds_kernel(a) && lat_fits(a.N); }
 #else
@@ -768,7 +765,7 @@ bool reads_once(const ProblemArgsT<real>& a) {
 
 template <bool SQRT>
 static hipError_t launch_alg(const ProblemArgsT<real>& a, hipStream_t stream) {
-#if SRBD_WITH_LATENCY && SRBD_LATENCY_MFMA
+#if SRBD_WITH_LATENCY
   if (!SQRT && lat_eligible(a)) {
     if (fused_residuals(a)) {
       hipLaunchKernelGGL(riccati_latency_kernel<true>, dim3((unsigned)a.batch), dim3(kLatThreads),
@@ -816,7 +813,7 @@ hipError_t prepare_device() {
   if (e == hipSuccess)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_unconstr_lds_res_kernel<true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
-#if SRBD_WITH_LATENCY && SRBD_LATENCY_MFMA
+#if SRBD_WITH_LATENCY
   if (e == hipSuccess)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_latency_kernel<false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
