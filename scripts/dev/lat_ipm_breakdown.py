@@ -21,10 +21,10 @@ qp, x0 = pkg.srbd_model.generate_batch(1, N=20, seed=11, constraints=cons)
 st = dict(mode="Speed", iter_max=30, ric_alg=0, split_step=1, tol_stat=1e-4, tol_eq=1e-4,
           tol_ineq=1e-4, tol_comp=1e-4)
 buf = (C.c_ulonglong * 8192)()
-names = {63: "start", 64: "init", 50: "iter top", 51: "residuals", 52: "barrier terms (pred)",
-         53: "factorize", 54: "forward (pred)", 55: "step pass (pred)", 56: "barrier terms (corr)",
+names = {63: "start", 64: "init", 50: "iter top", 51: "stage pass (step, residuals, predictor blocks)",
+         53: "factorize", 54: "forward (pred)", 55: "step pass (pred)", 56: "corrector gradient",
          57: "corr rhs stages", 58: "corr rhs chain", 59: "corr k stages", 60: "forward (corr)",
-         61: "step pass (corr)", 62: "update", 65: "after loop", 66: "outputs",
+         61: "step pass (corr)", 65: "after loop", 66: "outputs",
          70: "fact: barrier / stage top", 71: "fact: operands, G = R~ + B'PB, G to columns",
          72: "fact: chol(G) (+ W, H, F MFMAs)", 73: "fact: Y = L^-1 [H | g]",
          75: "fact: P = F - Y'Y, symmetrize"}

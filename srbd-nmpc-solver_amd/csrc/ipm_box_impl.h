@@ -133,6 +133,13 @@ __device__ __forceinline__ real* group_lds_blocks() {
   return blocks + (threadIdx.x / kGroup) * kGroupLds<GEN>;
 }
 
+// B2 takes P_{k+1} b~_k from the record (kRecPb, written by RB) instead of reading P_{k+1}
+// back: classical Riccati in fp64 (box-u 77.16 -> 76.35 ms same-box); the fp32 general-row RB
+// is at its register limit and spilled 12 B/lane more for it (cone fp32 +1.1%), the square root
+// records Lp and multiplies it out in B2 as before.
+template <bool SQRT>
+constexpr bool kRecPbOn = !SQRT && sizeof(real) == 8;
+
 // A factor record from the group's LDS image to the workspace as whole 16-byte pieces
 // (16 lanes x 16 B per instruction; box-u 79.3 -> 76.5 ms same-box).  Plain stores: F1, B2
 // and F2 read the record again within the iteration (non-temporal stores of stages >= 4
@@ -1281,6 +1288,11 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
         }
         rgu += sxu;
         rb = finish_b(rb);
+        // P_{k+1} b~_k, kept in the record for B2: the corrector's b~ is the predictor's, so
+        // B2 reads these 12 values instead of P_{k+1} (78) back (classical Riccati; the square
+        // root's record holds Lp, B2 multiplies it out as before)
+        real pbk = real(0.0);
+        if constexpr (kRecPbOn<SQRT>) pbk = dot_bcast(P, rb, real(0.0));
         real bv[12];
         gather12(rb, bv);
         sfor<0, 12>([&](auto i) {
@@ -1354,6 +1366,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           store12(img + kRecK + lane * 12, f.Kc);
           if constexpr (!kRecFactor) store_packed_col(img + kRecP, lane, f.F);
           img[kRecRs + lane] = f.rs;
+          if constexpr (kRecPbOn<SQRT>) img[kRecPb + lane] = pbk;
         }
         if (c.isv) {
           store12(img + kRecKv, f.Kc);
@@ -1786,7 +1799,7 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
           tstamp(40);
           real* stk = c.st(k);
           real* rec = stk + par * kRecSize;
-          const real* recn = c.st(k + 1) + par * kRecSize;
+          [[maybe_unused]] const real* recn = c.st(k + 1) + par * kRecSize;
           // the stage's element-owned loads, all issued before any is waited for (valid
           // addresses on every lane, masked after; a load under a lane condition would be a
           // branch that waits for it)
@@ -1820,9 +1833,14 @@ __device__ __forceinline__ void ipm_phase(const ProblemArgsT<real>& a) {
             if (lane < kMaxDim && uel) rt += ra;
             if (lane < kMaxDim && xel) qt += qa;
           }
-          const real bt = lane < kMaxDim ? b_ld : real(0.0);
-          // w = P_{k+1} b~ + p_{k+1}
-          const real w = rec_P_mul(recn, bt, pnext);
+          [[maybe_unused]] const real bt = lane < kMaxDim ? b_ld : real(0.0);
+          // w = P_{k+1} b~ + p_{k+1} (P_{k+1} b~ from RB, classical Riccati)
+          real w;
+          if constexpr (kRecPbOn<SQRT>) {
+            w = rec[kRecPb + li] + pnext;
+          } else {
+            w = rec_P_mul(recn, bt, pnext);
+          }
           // g = r~ + B'w ; f = q~ + A'w
           real Bc[12], Ac[12];
           c.col(c.B() + (size_t)k * c.nxu(), nx, col, uel, Bc);

@@ -54,7 +54,7 @@ constexpr int kSlot = 756;
 static_assert(kSb - kSA == 2 * 144 && kRR - kRb == kSR - kSb && kRq - kRb == kSq - kSb, "ring = A, B, record blocks");
 
 __host__ __device__ constexpr size_t lds_doubles(int N, int nch) {
-  return (size_t)29 * (N + 1) * 12 + (size_t)nch * (N + 1) * kGenChunk + (size_t)N * 156 + 648 +
+  return (size_t)31 * (N + 1) * 12 + (size_t)nch * (N + 1) * kGenChunk + (size_t)N * 156 + 648 +
          (size_t)kGroups * kRedSlots + 3 * kSlot;
 }
 
@@ -65,11 +65,14 @@ struct Lds {
   double* base;
   int S;    // (N + 1) * 12
   int N, nch;
-  // [N+1][12]: iterate, step, residuals, corrector gradients, corrector k and p
+  int cur;  // which of the two x / pi buffers holds the current iterate (stage_pass writes the other)
+  // [N+1][12]: iterate (x, pi double-buffered), step, residuals, corrector gradients, k and p
   __device__ double* v12(int i) const { return base + i * S; }
-  __device__ double* x() const { return v12(0); }
+  __device__ double* xb(int b) const { return v12(b ? 13 : 0); }
+  __device__ double* pib(int b) const { return v12(b ? 14 : 2); }
+  __device__ double* x() const { return xb(cur); }
+  __device__ double* pi() const { return pib(cur); }
   __device__ double* u() const { return v12(1); }
-  __device__ double* pi() const { return v12(2); }
   __device__ double* dx() const { return v12(3); }
   __device__ double* du() const { return v12(4); }
   __device__ double* dpi() const { return v12(5); }
@@ -82,13 +85,13 @@ struct Lds {
   __device__ double* pv() const { return v12(12); }
   // [N+1][48]: box barrier state of u / x (lam_l, lam_u, t_l, t_u) and its step
   // (dt_l, dt_u, dlam_l, dlam_u)
-  __device__ double* bu() const { return base + 13 * S; }
-  __device__ double* bx() const { return base + 17 * S; }
-  __device__ double* su() const { return base + 21 * S; }
-  __device__ double* sx() const { return base + 25 * S; }
+  __device__ double* bu() const { return base + 15 * S; }
+  __device__ double* bx() const { return base + 19 * S; }
+  __device__ double* su() const { return base + 23 * S; }
+  __device__ double* sx() const { return base + 27 * S; }
   // general rows, [N+1][nch][kGenChunk]
-  __device__ double* gb(int k, int ch) const { return base + 29 * S + (k * nch + ch) * kGenChunk; }
-  __device__ double* acl() const { return base + 29 * S + (N + 1) * nch * kGenChunk; }  // [N][156]
+  __device__ double* gb(int k, int ch) const { return base + 31 * S + (k * nch + ch) * kGenChunk; }
+  __device__ double* acl() const { return base + 31 * S + (N + 1) * nch * kGenChunk; }  // [N][156]
   // factorization hand-over: G/H tile, two Y tiles, two L factors
   __device__ double* scr() const { return acl() + N * 156; }
   __device__ double* red() const { return scr() + 648; }  // [kGroups][kRedSlots]
@@ -101,6 +104,7 @@ __device__ __forceinline__ Lds carve(double* base, int N, int nch) {
   L.S = (N + 1) * 12;
   L.N = N;
   L.nch = nch;
+  L.cur = 0;
   return L;
 }
 
@@ -269,6 +273,14 @@ __device__ __forceinline__ void aff_sums(const Side& s, const Bar& b, const BarS
 __device__ __forceinline__ double nabs(double v) { return v == v ? fabs(v) : __builtin_inf(); }
 __device__ __forceinline__ bool huge(double v) { return !(fabs(v) < 1.3e150); }
 __device__ __forceinline__ double stepv(double v, double a, double d) { return a != 0.0 ? fma(a, d, v) : v; }
+// A value every lane holds the same copy of (the block reductions), moved to SGPRs: the kernel
+// loop keeps ~10 such scalars live across the factorization, which needs every VGPR.
+__device__ __forceinline__ double uni(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 
 __device__ __forceinline__ double g16sum(double v) {
   v += __shfl_xor(v, 8, kGroup);
@@ -404,156 +416,17 @@ __device__ __forceinline__ void init_point(const Qp Q, const Lds L) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// phase: residuals at the iterate (oracle compute_residuals; HPIPM d_ocp_qp_res_compute)
+// phase: the previous step applied (alpha_p on x, u, t; alpha_d on pi, lam), the residuals at the
+// new iterate (oracle compute_residuals; HPIPM d_ocp_qp_res_compute) and, with PRED, the
+// predictor's barrier-augmented stage blocks R~, S~, Q~, r~, q~, b~ for the factorization -- one
+// pass per stage, the R, S, Q columns loaded once for both.  x and pi are double-buffered:
+// stage k reads the old x_k+1, pi_k+1 and their steps and forms the new values itself, so no
+// stage waits for its neighbour's update (the new iterate goes to buffer cur ^ 1).
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void residuals(const Qp Q, const Lds L) {
-  const ProblemArgsT<double>& a = Q.a;
-  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
-  const bool el = j < 12;
-  const int jj = el ? j : 11;
-  double mg = 0.0, mb = 0.0, md = 0.0, mm = 0.0, musum = 0.0, objl = 0.0;
-  for (int k = grp; k <= N; k += kGroups) {
-    const double uj = (el && k < N) ? L.u()[k * 12 + j] : 0.0;
-    const double xj = el ? L.x()[k * 12 + j] : 0.0;
-    const double pij = el ? L.pi()[k * 12 + j] : 0.0;
-    const double pinj = (el && k < N) ? L.pi()[(k + 1) * 12 + j] : 0.0;
-    double gu = 0.0, gx;
-    double Mc[12];
-    double sx = 0.0;  // (S x)_j
-    if (k < N) {
-      load12(Q.R(k) + jj * 12, Mc);
-      const double t1 = dot_bcast(Mc, uj, 0.0);
-      load_strided(Q.S(k) + jj, 12, Mc);
-      sx = dot_bcast(Mc, xj, 0.0);
-      const double rj = el ? Q.rv(k)[j] : 0.0;
-      load12(Q.B(k) + jj * 12, Mc);
-      const double bpi = dot_bcast(Mc, pinj, 0.0);
-      gu = t1 + sx + rj + bpi;
-      double o = uj * (0.5 * t1 + rj);
-      if (k == 0) o += uj * sx;
-      objl += el ? o : 0.0;
-    }
-    {
-      load12(Q.Q(k) + jj * 12, Mc);
-      const double t1 = dot_bcast(Mc, xj, 0.0);
-      const double qj = el ? Q.qv(k)[j] : 0.0;
-      gx = t1 + qj - pij;
-      if (k > 0) {
-        double o = xj * (0.5 * t1 + qj);
-        if (k < N) o += uj * sx;
-        objl += el ? o : 0.0;
-      }
-      if (k < N) {
-        load12(Q.S(k) + jj * 12, Mc);
-        gx += dot_bcast(Mc, uj, 0.0);
-        load12(Q.A(k) + jj * 12, Mc);
-        gx += dot_bcast(Mc, pinj, 0.0);
-      }
-    }
-    // box rows
-    if (k < N) {
-      const Side s = side_u(Q, k, j);
-      const Bar b = el ? ld_bar(L.bu() + k * 48, j) : Bar{0, 0, 1, 1};
-      gu -= (s.ml != 0.0 ? b.ll : 0.0) - (s.mu != 0.0 ? b.lu : 0.0);
-      if (s.ml != 0.0) {
-        const double rd = uj - s.lb - b.tl, rm = b.ll * b.tl;
-        md = fmax(md, nabs(rd));
-        mm = fmax(mm, nabs(rm));
-        musum += rm;
-      }
-      if (s.mu != 0.0) {
-        const double rd = s.ub - uj - b.tu, rm = b.lu * b.tu;
-        md = fmax(md, nabs(rd));
-        mm = fmax(mm, nabs(rm));
-        musum += rm;
-      }
-    }
-    if (k > 0) {
-      const Side s = side_x(Q, k, j);
-      const Bar b = el ? ld_bar(L.bx() + k * 48, j) : Bar{0, 0, 1, 1};
-      gx -= (s.ml != 0.0 ? b.ll : 0.0) - (s.mu != 0.0 ? b.lu : 0.0);
-      if (s.ml != 0.0) {
-        const double rd = xj - s.lb - b.tl, rm = b.ll * b.tl;
-        md = fmax(md, nabs(rd));
-        mm = fmax(mm, nabs(rm));
-        musum += rm;
-      }
-      if (s.mu != 0.0) {
-        const double rd = s.ub - xj - b.tu, rm = b.lu * b.tu;
-        md = fmax(md, nabs(rd));
-        mm = fmax(mm, nabs(rm));
-        musum += rm;
-      }
-    }
-    // general rows (lane j = row ch * 12 + j of the chunk): values, rd / rm, gradient terms
-    for (int ch = 0; ch < L.nch; ++ch) {
-      const int r = ch * 12 + j;
-      const bool ok = el && r < a.ng;
-      double Dr[12], Cr[12];
-      load_strided(ok ? Q.Drow(k, r) : nullptr, a.ng, Dr);
-      load_strided(ok ? Q.Crow(k, r) : nullptr, a.ng, Cr);
-      const double v = dot_bcast(Cr, xj, dot_bcast(Dr, uj, 0.0));
-      const Side s = ok ? side_g(Q, k, r) : Side{0, 0, 0, 0};
-      double* g = L.gb(k, ch);
-      const Bar b = el ? ld_bar(g, j) : Bar{0, 0, 1, 1};
-      if (el) g[96 + j] = v;
-      if (s.ml != 0.0) {
-        const double rd = v - s.lb - b.tl, rm = b.ll * b.tl;
-        md = fmax(md, nabs(rd));
-        mm = fmax(mm, nabs(rm));
-        musum += rm;
-      }
-      if (s.mu != 0.0) {
-        const double rd = s.ub - v - b.tu, rm = b.lu * b.tu;
-        md = fmax(md, nabs(rd));
-        mm = fmax(mm, nabs(rm));
-        musum += rm;
-      }
-      const double cr = (s.ml != 0.0 ? b.ll : 0.0) - (s.mu != 0.0 ? b.lu : 0.0);
-      // gu -= D' c, gx -= C' c: column j of D / C against the chunk's row-owned c
-      const int rr = ch * 12;
-      double Dc[12], Cc[12];
-      const bool okc = el && rr < a.ng;
-      sfor<0, 12>([&](auto i) {
-        constexpr int I = decltype(i)::value;
-        const double* dp = Q.Drow(k, rr + I);
-        const double* cp = Q.Crow(k, rr + I);
-        const bool iok = okc && rr + I < a.ng;
-        Dc[I] = (iok && dp) ? dp[(size_t)a.ng * jj] : 0.0;
-        Cc[I] = (iok && cp) ? cp[(size_t)a.ng * jj] : 0.0;
-      });
-      gu -= dot_bcast(Dc, cr, 0.0);
-      gx -= dot_bcast(Cc, cr, 0.0);
-    }
-    if (k < N) mg = fmax(mg, el ? nabs(gu) : 0.0);
-    if (k > 0) mg = fmax(mg, el ? nabs(gx) : 0.0);
-    double rbj = 0.0;
-    if (k < N) {
-      double Ar[12], Br[12];
-      load_strided(Q.A(k) + jj, 12, Ar);
-      load_strided(Q.B(k) + jj, 12, Br);
-      const double t1 = dot_bcast(Ar, xj, 0.0), t2 = dot_bcast(Br, uj, 0.0);
-      const double xn = el ? L.x()[(k + 1) * 12 + j] : 0.0;
-      rbj = t1 + t2 + (el ? Q.b(k)[j] : 0.0) - xn;
-      mb = fmax(mb, el ? nabs(rbj) : 0.0);
-    }
-    if (el) {
-      L.rgu()[k * 12 + j] = gu;
-      L.rgx()[k * 12 + j] = gx;
-      L.rb()[k * 12 + j] = rbj;
-    }
-  }
-  red_put(L, 0, g16max(mg));
-  red_put(L, 1, g16max(mb));
-  red_put(L, 2, g16max(md));
-  red_put(L, 3, g16max(mm));
-  red_put(L, 4, g16sum(el ? musum : 0.0));
-  red_put(L, 5, g16sum(objl));
-}
+template <bool HAS_C, bool PRED>
+__device__ __forceinline__ void stage_pass(const Qp Q, const Lds L, double ap, double ad);
 
-// ---------------------------------------------------------------------------------------------
 // column j of chunk ch's rows of D_k (or C_k): v[i] = D[ch * 12 + i][j], 0 past ng / when absent
-// ---------------------------------------------------------------------------------------------
 template <bool ISC>
 __device__ __forceinline__ void gen_col(const Qp& Q, int k, int ch, int jj, bool el, double (&v)[12]) {
   const int rr = ch * 12, ng = Q.a.ng;
@@ -574,7 +447,7 @@ __device__ __forceinline__ void gen_row(const Qp& Q, int k, int ch, int j, bool 
 // C[i] += sum_r X[r][i] Gamma_r Y[r][j] over the general rows (column j of X'Gamma Y; X = D or C
 // row-owned on the chunk's lanes, Y's column j on lane j, Gamma from the chunk's LDS slot)
 template <bool XC, bool YC>
-__device__ __forceinline__ void gen_syrk(const Qp Q, const Lds L, int k, int j, int jj, bool el,
+__device__ __forceinline__ void gen_syrk(const Qp& Q, const Lds& L, int k, int j, int jj, bool el,
                                          double (&C)[12]) {
   for (int ch = 0; ch < L.nch; ++ch) {
     double Xr[12], Yc[12];
@@ -588,61 +461,246 @@ __device__ __forceinline__ void gen_syrk(const Qp Q, const Lds L, int k, int j, 
   }
 }
 
+template <bool HAS_C, bool PRED>
+__device__ __forceinline__ void stage_pass(const Qp Q, const Lds L, double ap, double ad) {
+  const ProblemArgsT<double>& a = Q.a;
+  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
+  const bool el = j < 12;
+  const int jj = el ? j : 11;
+  const double* xo = L.xb(L.cur);
+  const double* po = L.pib(L.cur);
+  double* xw = L.xb(L.cur ^ 1);
+  double* pw = L.pib(L.cur ^ 1);
+  double mg = 0.0, mb = 0.0, md = 0.0, mm = 0.0, musum = 0.0, objl = 0.0;
+  auto upd = [&](double* bp, const double* sp) {
+    Bar b = ld_bar(bp, j);
+    const BarStep d = ld_step(sp, j);
+    b.tl = stepv(b.tl, ap, d.dtl);
+    b.tu = stepv(b.tu, ap, d.dtu);
+    b.ll = stepv(b.ll, ad, d.dll);
+    b.lu = stepv(b.lu, ad, d.dlu);
+    st_bar(bp, j, b);
+    return b;
+  };
+  for (int k = grp; k <= N; k += kGroups) {
+    // ---- the step: stage k's own state in place, x_k+1 / pi_k+1 from the old buffer ----
+    double uj = 0.0, xj = 0.0, pij = 0.0, xnj = 0.0, pinj = 0.0;
+    Bar bu{0, 0, 1, 1}, bx{0, 0, 1, 1};
+    if (el) {
+      if (k < N) {
+        uj = stepv(L.u()[k * 12 + j], ap, L.du()[k * 12 + j]);
+        L.u()[k * 12 + j] = uj;
+        xnj = stepv(xo[(k + 1) * 12 + j], ap, L.dx()[(k + 1) * 12 + j]);
+        pinj = stepv(po[(k + 1) * 12 + j], ad, L.dpi()[(k + 1) * 12 + j]);
+      }
+      xj = xo[k * 12 + j];
+      pij = po[k * 12 + j];
+      if (k > 0) {  // (x_0 = x0 is fixed; pi_0 is not an iterate)
+        xj = stepv(xj, ap, L.dx()[k * 12 + j]);
+        pij = stepv(pij, ad, L.dpi()[k * 12 + j]);
+      }
+      xw[k * 12 + j] = xj;
+      pw[k * 12 + j] = pij;
+      bu = upd(L.bu() + k * 48, L.su() + k * 48);
+      bx = upd(L.bx() + k * 48, L.sx() + k * 48);
+    }
+    // ---- residuals (the R, S, Q columns are loaded again, from L1 / L2, for the Hessian
+    // blocks below: kept live across the general rows they spilled) ----
+    double gu = 0.0, gx;
+    double M[12];
+    double sx = 0.0;  // (S x)_j
+    if (k < N) {
+      load12(Q.R(k) + jj * 12, M);
+      const double t1 = dot_bcast(M, uj, 0.0);
+      load_strided(Q.S(k) + jj, 12, M);
+      sx = dot_bcast(M, xj, 0.0);
+      const double rj = el ? Q.rv(k)[j] : 0.0;
+      load12(Q.B(k) + jj * 12, M);
+      const double bpi = dot_bcast(M, pinj, 0.0);
+      gu = t1 + sx + rj + bpi;
+      double o = uj * (0.5 * t1 + rj);
+      if (k == 0) o += uj * sx;
+      objl += el ? o : 0.0;
+    }
+    load12(Q.Q(k) + jj * 12, M);
+    {
+      const double t1 = dot_bcast(M, xj, 0.0);
+      const double qj = el ? Q.qv(k)[j] : 0.0;
+      gx = t1 + qj - pij;
+      if (k > 0) {
+        double o = xj * (0.5 * t1 + qj);
+        if (k < N) o += uj * sx;
+        objl += el ? o : 0.0;
+      }
+      if (k < N) {
+        load12(Q.S(k) + jj * 12, M);
+        gx += dot_bcast(M, uj, 0.0);
+        load12(Q.A(k) + jj * 12, M);
+        gx += dot_bcast(M, pinj, 0.0);
+      }
+    }
+    // box rows: gradient terms, rd / rm; Gamma, gamma of the predictor
+    double Gu = 0.0, gam_u = 0.0, Gx = 0.0, gam_x = 0.0;
+    if (k < N) {
+      const Side s = side_u(Q, k, j);
+      gu -= (s.ml != 0.0 ? bu.ll : 0.0) - (s.mu != 0.0 ? bu.lu : 0.0);
+      if (s.ml != 0.0) {
+        const double rd = uj - s.lb - bu.tl, rm = bu.ll * bu.tl;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (s.mu != 0.0) {
+        const double rd = s.ub - uj - bu.tu, rm = bu.lu * bu.tu;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (PRED && el) gamma_of(s, bu, uj, 0.0, 0.0, 0.0, Gu, gam_u);
+    }
+    if (k > 0) {
+      const Side s = side_x(Q, k, j);
+      gx -= (s.ml != 0.0 ? bx.ll : 0.0) - (s.mu != 0.0 ? bx.lu : 0.0);
+      if (s.ml != 0.0) {
+        const double rd = xj - s.lb - bx.tl, rm = bx.ll * bx.tl;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (s.mu != 0.0) {
+        const double rd = s.ub - xj - bx.tu, rm = bx.lu * bx.tu;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (PRED && el) gamma_of(s, bx, xj, 0.0, 0.0, 0.0, Gx, gam_x);
+    }
+    // general rows (lane j = row ch * 12 + j of the chunk): the step, values, rd / rm, gradient
+    // terms; the predictor's Gamma (kept for the Hessian passes) and gamma
+    double gpu = 0.0, gpx = 0.0;  // D'gamma, C'gamma
+    for (int ch = 0; ch < L.nch; ++ch) {
+      const int r = ch * 12 + j;
+      const bool ok = el && r < a.ng;
+      double* g = L.gb(k, ch);
+      const Bar b = el ? upd(g, g + 48) : Bar{0, 0, 1, 1};
+      double Dr[12], Cr[12];
+      gen_row<false>(Q, k, ch, j, el, Dr);
+      if constexpr (HAS_C) {
+        gen_row<true>(Q, k, ch, j, el, Cr);
+      } else {
+        sfor<0, 12>([&](auto i) { Cr[decltype(i)::value] = 0.0; });
+      }
+      const double v = dot_bcast(Cr, xj, dot_bcast(Dr, uj, 0.0));
+      const Side sg = ok ? side_g(Q, k, r) : Side{0, 0, 0, 0};
+      if (el) g[96 + j] = v;
+      if (sg.ml != 0.0) {
+        const double rd = v - sg.lb - b.tl, rm = b.ll * b.tl;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      if (sg.mu != 0.0) {
+        const double rd = sg.ub - v - b.tu, rm = b.lu * b.tu;
+        md = fmax(md, nabs(rd));
+        mm = fmax(mm, nabs(rm));
+        musum += rm;
+      }
+      const double cr = (sg.ml != 0.0 ? b.ll : 0.0) - (sg.mu != 0.0 ? b.lu : 0.0);
+      double G = 0.0, gam = 0.0;
+      if (PRED && ok) gamma_of(sg, b, v, 0.0, 0.0, 0.0, G, gam);
+      if (PRED && el) g[108 + j] = G;
+      double Yc[12];
+      gen_col<false>(Q, k, ch, jj, el, Yc);
+      gu -= dot_bcast(Yc, cr, 0.0);
+      if (PRED) gpu = dot_bcast(Yc, gam, gpu);
+      if constexpr (HAS_C) {
+        gen_col<true>(Q, k, ch, jj, el, Yc);
+        gx -= dot_bcast(Yc, cr, 0.0);
+        if (PRED) gpx = dot_bcast(Yc, gam, gpx);
+      }
+    }
+    if (k < N) mg = fmax(mg, el ? nabs(gu) : 0.0);
+    if (k > 0) mg = fmax(mg, el ? nabs(gx) : 0.0);
+    double rbj = 0.0;
+    if (k < N) {
+      double Br[12];
+      load_strided(Q.A(k) + jj, 12, M);
+      load_strided(Q.B(k) + jj, 12, Br);
+      const double t1 = dot_bcast(M, xj, 0.0), t2 = dot_bcast(Br, uj, 0.0);
+      rbj = t1 + t2 + (el ? Q.b(k)[j] : 0.0) - xnj;
+      mb = fmax(mb, el ? nabs(rbj) : 0.0);
+    }
+    if (el) {
+      L.rgu()[k * 12 + j] = gu;
+      L.rgx()[k * 12 + j] = gx;
+      L.rb()[k * 12 + j] = rbj;
+    }
+    if (!PRED) continue;
+    // ---- the predictor's stage blocks into the record ----
+    double* rk = Q.rec(k);
+    double Rc[12], Sc[12], Qc[12];
+    if (k < N) {
+      load12(Q.R(k) + jj * 12, Rc);
+      load12(Q.S(k) + jj * 12, Sc);
+      sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] += decltype(i)::value == j ? Gu : 0.0; });
+      gen_syrk<false, false>(Q, L, k, j, jj, el, Rc);  // R~ = R + diag(Gamma_u) + D'Gamma D
+      if constexpr (HAS_C) gen_syrk<false, true>(Q, L, k, j, jj, el, Sc);  // S~ = S + D'Gamma C
+      if (el) {
+        store12(rk + kRR + j * 12, Rc);
+        store12(rk + kRS + j * 12, Sc);
+        rk[kRr + j] = gu + gam_u + gpu;
+        rk[kRb + j] = rbj;
+      }
+    }
+    load12(Q.Q(k) + jj * 12, Qc);
+    sfor<0, 12>([&](auto i) { Qc[decltype(i)::value] += decltype(i)::value == j ? Gx : 0.0; });
+    if constexpr (HAS_C) gen_syrk<true, true>(Q, L, k, j, jj, el, Qc);  // Q~ = Q + diag(Gamma_x) + C'Gamma C
+    if (el) {
+      store12(rk + kRQ + j * 12, Qc);
+      rk[kRq + j] = gx + gam_x + gpx;
+    }
+  }
+  red_put(L, 0, g16max(mg));
+  red_put(L, 1, g16max(mb));
+  red_put(L, 2, g16max(md));
+  red_put(L, 3, g16max(mm));
+  red_put(L, 4, g16sum(el ? musum : 0.0));
+  red_put(L, 5, g16sum(objl));
+}
+
 // ---------------------------------------------------------------------------------------------
-// phase: barrier terms of the predictor (CORR false: Gamma, gamma; the stage blocks R~, S~,
-// Q~, r~, q~, b~ into the workspace for the factorization) or of the corrector (CORR true:
-// gamma with the predictor's dlam dt and sigma mu, into gtu / gtx).  HAS_C: the problem has C
-// (C-free general rows -- the friction cone -- skip every C product).  One pass per Hessian
-// block, so no more than one 12 x 12 accumulator is live.
+// phase: the corrector's gradient: gamma with the predictor's dlam dt and sigma mu (HPIPM's
+// res_m = lam t + dlam_aff dt_aff - sigma mu), g~ = res_g + gamma terms into gtu / gtx
 // ---------------------------------------------------------------------------------------------
-template <bool CORR, bool HAS_C>
-__device__ __forceinline__ void barrier_terms(const Qp Q, const Lds L, double smu) {
+template <bool HAS_C>
+__device__ __forceinline__ void corr_terms(const Qp Q, const Lds L, double smu) {
   const ProblemArgsT<double>& a = Q.a;
   const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
   const bool el = j < 12;
   const int jj = el ? j : 11;
   for (int k = grp; k <= N; k += kGroups) {
-    double Gu = 0.0, gam_u = 0.0, Gx = 0.0, gam_x = 0.0;
+    double gam_u = 0.0, gam_x = 0.0, G = 0.0;
     if (k < N && el) {
-      const Side s = side_u(Q, k, j);
-      const Bar b = ld_bar(L.bu() + k * 48, j);
-      double e1 = 0.0, e2 = 0.0;
-      if (CORR) {
-        const BarStep d = ld_step(L.su() + k * 48, j);
-        e1 = d.dll * d.dtl;
-        e2 = d.dlu * d.dtu;
-      }
-      gamma_of(s, b, L.u()[k * 12 + j], e1, e2, CORR ? smu : 0.0, Gu, gam_u);
+      const BarStep d = ld_step(L.su() + k * 48, j);
+      gamma_of(side_u(Q, k, j), ld_bar(L.bu() + k * 48, j), L.u()[k * 12 + j], d.dll * d.dtl, d.dlu * d.dtu, smu,
+               G, gam_u);
     }
     if (k > 0 && el) {
-      const Side s = side_x(Q, k, j);
-      const Bar b = ld_bar(L.bx() + k * 48, j);
-      double e1 = 0.0, e2 = 0.0;
-      if (CORR) {
-        const BarStep d = ld_step(L.sx() + k * 48, j);
-        e1 = d.dll * d.dtl;
-        e2 = d.dlu * d.dtu;
-      }
-      gamma_of(s, b, L.x()[k * 12 + j], e1, e2, CORR ? smu : 0.0, Gx, gam_x);
+      const BarStep d = ld_step(L.sx() + k * 48, j);
+      gamma_of(side_x(Q, k, j), ld_bar(L.bx() + k * 48, j), L.x()[k * 12 + j], d.dll * d.dtl, d.dlu * d.dtu, smu,
+               G, gam_x);
     }
     double gu = (el ? L.rgu()[k * 12 + j] : 0.0) + gam_u;
     double gx = (el ? L.rgx()[k * 12 + j] : 0.0) + gam_x;
-    // general rows: Gamma (kept for the Hessian passes), gradient D'gamma / C'gamma
     for (int ch = 0; ch < L.nch; ++ch) {
       const int r = ch * 12 + j;
       const bool ok = el && r < a.ng;
-      double* g = L.gb(k, ch);
-      double G = 0.0, gam = 0.0;
+      const double* g = L.gb(k, ch);
+      double gam = 0.0;
       if (ok) {
-        double e1 = 0.0, e2 = 0.0;
-        if (CORR) {
-          const BarStep d = ld_step(g + 48, j);
-          e1 = d.dll * d.dtl;
-          e2 = d.dlu * d.dtu;
-        }
-        gamma_of(side_g(Q, k, r), ld_bar(g, j), g[96 + j], e1, e2, CORR ? smu : 0.0, G, gam);
+        const BarStep d = ld_step(g + 48, j);
+        gamma_of(side_g(Q, k, r), ld_bar(g, j), g[96 + j], d.dll * d.dtl, d.dlu * d.dtu, smu, G, gam);
       }
-      if (!CORR && el) g[108 + j] = G;
       double Mc[12];
       gen_col<false>(Q, k, ch, jj, el, Mc);
       gu = dot_bcast(Mc, gam, gu);
@@ -651,35 +709,9 @@ __device__ __forceinline__ void barrier_terms(const Qp Q, const Lds L, double sm
         gx = dot_bcast(Mc, gam, gx);
       }
     }
-    if (CORR) {
-      if (el) {
-        L.gtu()[k * 12 + j] = gu;
-        L.gtx()[k * 12 + j] = gx;
-      }
-      continue;
-    }
-    // predictor: the barrier-augmented blocks of stage k into its record
-    double* rk = Q.rec(k);
-    double C[12];
-    if (k < N) {
-      load12(Q.R(k) + jj * 12, C);  // R~ = R + diag(Gamma_u) + D'Gamma D
-      sfor<0, 12>([&](auto i) { C[decltype(i)::value] += decltype(i)::value == j ? Gu : 0.0; });
-      gen_syrk<false, false>(Q, L, k, j, jj, el, C);
-      if (el) store12(rk + kRR + j * 12, C);
-      load12(Q.S(k) + jj * 12, C);  // S~ = S + D'Gamma C
-      if constexpr (HAS_C) gen_syrk<false, true>(Q, L, k, j, jj, el, C);
-      if (el) {
-        store12(rk + kRS + j * 12, C);
-        rk[kRr + j] = gu;
-        rk[kRb + j] = L.rb()[k * 12 + j];
-      }
-    }
-    load12(Q.Q(k) + jj * 12, C);  // Q~ = Q + diag(Gamma_x) + C'Gamma C
-    sfor<0, 12>([&](auto i) { C[decltype(i)::value] += decltype(i)::value == j ? Gx : 0.0; });
-    if constexpr (HAS_C) gen_syrk<true, true>(Q, L, k, j, jj, el, C);
     if (el) {
-      store12(rk + kRQ + j * 12, C);
-      rk[kRq + j] = gx;
+      L.gtu()[k * 12 + j] = gu;
+      L.gtx()[k * 12 + j] = gx;
     }
   }
 }
@@ -1117,36 +1149,6 @@ __device__ __forceinline__ void corr_k_stages(const Qp Q, const Lds L) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// phase: apply the step (alpha_p on x, u, t; alpha_d on pi, lam)
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void update(const Qp Q, const Lds L, double ap, double ad) {
-  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
-  if (j >= 12) return;
-  for (int k = grp; k <= N; k += kGroups) {
-    if (k < N) L.u()[k * 12 + j] = stepv(L.u()[k * 12 + j], ap, L.du()[k * 12 + j]);
-    if (k > 0) {
-      L.x()[k * 12 + j] = stepv(L.x()[k * 12 + j], ap, L.dx()[k * 12 + j]);
-      L.pi()[k * 12 + j] = stepv(L.pi()[k * 12 + j], ad, L.dpi()[k * 12 + j]);
-    }
-    auto upd = [&](double* bp, const double* sp) {
-      Bar b = ld_bar(bp, j);
-      const BarStep d = ld_step(sp, j);
-      b.tl = stepv(b.tl, ap, d.dtl);
-      b.tu = stepv(b.tu, ap, d.dtu);
-      b.ll = stepv(b.ll, ad, d.dll);
-      b.lu = stepv(b.lu, ad, d.dlu);
-      st_bar(bp, j, b);
-    };
-    upd(L.bu() + k * 48, L.su() + k * 48);
-    upd(L.bx() + k * 48, L.sx() + k * 48);
-    for (int ch = 0; ch < L.nch; ++ch) {
-      double* g = L.gb(k, ch);
-      upd(g, g + 48);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // phase: outputs (ipm_box_impl.h kPhOut): x, u, pi with the stage-0 rebuild
 // pi_0 = Q0 x0 + S0'u0 + q0 + A0'(P_1 res_b0 + pi_1) (ocp_qp_ipm_solver.cpp:347-373), and the
 // Riccati getters of the last factorization: P, K; p = pi - P x, k = u - K x
@@ -1206,7 +1208,7 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int N = a.N;
   const int nch = (a.ng + 11) / 12;
-  const Lds L = carve(reinterpret_cast<double*>(lds_raw), N, nch);
+  Lds L = carve(reinterpret_cast<double*>(lds_raw), N, nch);
   const Qp Q{a, (int)blockIdx.x, N};
   const bool t0 = threadIdx.x == 0;
   double* const stat = a.stat ? a.stat + (size_t)Q.q * a.stat_rows * kStatCols : nullptr;
@@ -1215,24 +1217,26 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
   init_point(Q, L);
   __syncthreads();
   tstamp(64);
-  const double nc = red_sum(L, 0);
-  const double nc_inv = nc > 0.0 ? 1.0 / nc : 0.0;
+  const double nc = uni(red_sum(L, 0));
+  const double nc_inv = uni(nc > 0.0 ? 1.0 / nc : 0.0);
   double last_amin = 1.0, res_g = 0.0, res_b = 0.0, res_d = 0.0, res_m = 0.0, obj = 0.0;
+  double alpha_p = 0.0, alpha_d = 0.0;  // the step the next stage pass applies (none at first)
   int iter = 0, status = -1;
 #pragma unroll 1
   for (;;) {
     __syncthreads();  // (red reuse)
     tstamp(50);
-    residuals(Q, L);
+    stage_pass<HAS_C, true>(Q, L, alpha_p, alpha_d);
     __syncthreads();
+    L.cur ^= 1;  // the new iterate
     tstamp(51);
-    res_g = red_max(L, 0);
-    res_b = red_max(L, 1);
-    res_d = red_max(L, 2);
-    res_m = red_max(L, 3);
-    const double musum = red_sum(L, 4);
-    obj = red_sum(L, 5);
-    const double mu = musum * nc_inv;
+    res_g = uni(red_max(L, 0));
+    res_b = uni(red_max(L, 1));
+    res_d = uni(red_max(L, 2));
+    res_m = uni(red_max(L, 3));
+    const double musum = uni(red_sum(L, 4));
+    obj = uni(red_sum(L, 5));
+    const double mu = uni(musum * nc_inv);
     if (stat && t0) {
       double* row = stat + (size_t)iter * kStatCols;
       row[5] = mu;
@@ -1256,10 +1260,7 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
     if (status >= 0) break;
     double* const next = (stat && t0) ? stat + (size_t)(iter + 1) * kStatCols : nullptr;
 
-    // ---- predictor ----
-    barrier_terms<false, HAS_C>(Q, L, 0.0);
-    __syncthreads();
-    tstamp(52);
+    // ---- predictor (the stage blocks are in the records: stage_pass) ----
     factorize(Q, L);
     __syncthreads();
     tstamp(53);
@@ -1270,16 +1271,16 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
     step_pass<false>(Q, L, 0.0, !pc);
     __syncthreads();
     tstamp(55);
-    double ap = red_min(L, 0), ad = red_min(L, 1);
-    bool bad = red_max(L, 4) > 0.0;
+    double ap = uni(red_min(L, 0)), ad = uni(red_min(L, 1));
+    bool bad = uni(red_max(L, 4)) > 0.0;
     if (pc) {
       const double aa = fmin(1.0, fmin(ap, ad));
-      const double S1 = red_sum(L, 2), S2 = red_sum(L, 3);
+      const double S1 = uni(red_sum(L, 2)), S2 = uni(red_sum(L, 3));
       const double mu_aff = (musum + aa * (S1 + aa * S2)) * nc_inv;
       double sg = mu > 0.0 ? mu_aff / mu : 0.0;
       sg = sg * sg * sg;
       if (sg > 1.0) sg = 1.0;
-      const double smu = sg * mu;
+      const double smu = uni(sg * mu);
       if (next) {
         next[0] = aa;
         next[1] = mu_aff;
@@ -1287,7 +1288,7 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
       }
       // ---- corrector: same factors, new gradient ----
       __syncthreads();
-      barrier_terms<true, HAS_C>(Q, L, smu);
+      corr_terms<HAS_C>(Q, L, smu);
       __syncthreads();
       tstamp(56);
       corr_rhs_stages(Q, L);
@@ -1305,9 +1306,9 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
       step_pass<true>(Q, L, smu, true);
       __syncthreads();
       tstamp(61);
-      ap = red_min(L, 0);
-      ad = red_min(L, 1);
-      bad = red_max(L, 4) > 0.0;
+      ap = uni(red_min(L, 0));
+      ad = uni(red_min(L, 1));
+      bad = uni(red_max(L, 4)) > 0.0;
     }
     if (bad) {
       ap = 0.0;
@@ -1317,22 +1318,18 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
       ap = fmin(ap, ad);
       ad = ap;
     }
-    const double alpha_p = fmin(1.0, kTau * ap), alpha_d = fmin(1.0, kTau * ad);
+    alpha_p = uni(fmin(1.0, kTau * ap));
+    alpha_d = uni(fmin(1.0, kTau * ad));
     if (next) {
       next[3] = alpha_p;
       next[4] = alpha_d;
     }
-    last_amin = fmin(alpha_p, alpha_d);
-    update(Q, L, alpha_p, alpha_d);
-    tstamp(62);
+    last_amin = uni(fmin(alpha_p, alpha_d));
     ++iter;
   }
-  // converged at the initial point: the factorization of the returned iterate (HPIPM getters)
-  if (iter == 0 && status != 3) {
-    barrier_terms<false, HAS_C>(Q, L, 0.0);
-    __syncthreads();
-    factorize(Q, L);
-  }
+  // converged at the initial point: the factorization of the returned iterate (HPIPM getters;
+  // its stage blocks are in the records: stage_pass)
+  if (iter == 0 && status != 3) factorize(Q, L);
   __syncthreads();
   tstamp(65);
   outputs(Q, L);

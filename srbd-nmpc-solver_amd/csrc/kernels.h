@@ -104,7 +104,8 @@ constexpr int kRecP = 222;   // P packed lower triangle (78)
 constexpr int kRecRs = 300;  // 1 / diag(L)
 constexpr int kRecKv = 312;  // k
 constexpr int kRecPv = 324;  // p
-constexpr int kRecSize = 336;
+constexpr int kRecPb = 336;  // P_{k+1} b~_k (classical Riccati: B2's right-hand side, from RB)
+constexpr int kRecSize = 348;
 constexpr int kStLam = 2 * kRecSize;  // 8 x 12: lam_l,u / lam_u,u / t_l,u / t_u,u / same for x
 constexpr int kStRes = kStLam + 96;   // 3 x 12: res_g,u / res_g,x / res_b
 constexpr int kStStep = kStRes + 36;  // 3 x 12: du / dx / dpi
