@@ -169,3 +169,23 @@ def test_nan_and_batch_one(pkg):
     one = pkg.capi.solve(qp.subset(np.array([5])), x0[5:6], NMPC)
     for key in ("x", "u", "pi", "iter", "status"):
         assert np.array_equal(one[key][0], ok[key][5]), key
+
+
+@pytest.mark.parametrize("N", [1, 10, 30, 40])
+def test_horizons_and_lds_fallback(pkg, oracle, N):
+    """Horizons around the LDS budget: N = 1, 10 and 30 run the latency IPM (30: 155 KB of LDS),
+    N = 40 does not fit (197 KB) and falls back to the batched kernels; every one solves the
+    oracle's QP at 1e-7 in its iterations +-1."""
+    qp, x0 = pkg.srbd_model.generate_batch(4, N=N, seed=900 + N, constraints="box_u")
+    out = pkg.capi.solve(qp, x0, NMPC)
+    ref = oracle.solve(qp, NMPC, x0=x0)
+    _check_vs_oracle(out, ref, qp.batch)
+
+
+def test_many_general_rows(pkg, oracle):
+    """ng = 40 (four 12-row chunks per stage, C and D) with boxes on u and x, N = 8."""
+    qp, x0 = helpers.random_constrained(6, 8, 12, 12, 40, 77, pkg.OcpQpBatch)
+    st = dict(NMPC, iter_max=40)
+    out = pkg.capi.solve(qp, x0, st)
+    ref = oracle.solve(qp, st, x0=x0)
+    _check_vs_oracle(out, ref, qp.batch, oracle_misses=1)
