@@ -76,7 +76,7 @@
 extern "C" {
 #endif
 
-#define SRBD_QP_ABI_VERSION 11
+#define SRBD_QP_ABI_VERSION 12
 #define SRBD_QP_MAX_NX 12
 #define SRBD_QP_MAX_NU 12
 #define SRBD_QP_MAX_NG 64
@@ -266,6 +266,20 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* setti
  * into it.                                                                  */
 int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
                            const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol);
+
+/* srbd_qp_solve_host_f64 that hands the caller the Riccati outputs early:
+ * `on_factors(ctx)` runs once on the calling thread, before the call returns
+ * and only if the solve succeeds, as soon as sol->P, p, K, k are final in the
+ * caller's buffers.  On the zero-copy single-QP path (above; fp64 classical
+ * Riccati, N <= 20) that is while the kernel still runs its forward sweep,
+ * u / pi and residual passes, so a caller can unpack the factors (the bulk of
+ * the outputs) under the kernel's tail; elsewhere it runs after the solve.
+ * The callback must not call into the handle.  Replaces the
+ * d_ocp_qp_ipm_get_ric_P / _p / _K / _k reads of ocp_qp_ipm_solver.cpp:342-345
+ * for the hpipm-cpp shim.  (ABI 12)                                          */
+int srbd_qp_solve_host_cb_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
+                              const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol,
+                              void (*on_factors)(void* ctx), void* ctx);
 
 /* The handle's pinned host staging for a srbd_qp_solve_host_f64 call of `batch`
  * QPs with `settings`: every field that *data / *sol have non-NULL (any value,

@@ -55,6 +55,10 @@ class Solution(C.Structure):
     _fields_ = [(n, _dp) for n in SOL_FIELDS]
 
 
+# srbd_qp_solve_host_cb_f64's callback: void (*)(void* ctx)
+FACTORS_CB = C.CFUNCTYPE(None, C.c_void_p)
+
+
 # fp32 twins (srbd_qp_data_f32 / srbd_qp_solution_f32): same field order
 class Data32(C.Structure):
     _fields_ = [(n, _dp) for n in DATA_FIELDS]
@@ -111,6 +115,10 @@ def lib():
         L.srbd_qp_solve_host_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings),
                                              C.POINTER(Data), C.POINTER(Solution)]
         L.srbd_qp_solve_host_f64.restype = C.c_int
+        if hasattr(L, "srbd_qp_solve_host_cb_f64"):  # ABI 12
+            L.srbd_qp_solve_host_cb_f64.argtypes = [C.c_void_p, C.c_int, C.POINTER(Settings), C.POINTER(Data),
+                                                    C.POINTER(Solution), FACTORS_CB, C.c_void_p]
+            L.srbd_qp_solve_host_cb_f64.restype = C.c_int
         if hasattr(L, "srbd_qp_multi_create"):  # ABI 10
             L.srbd_qp_multi_create.argtypes = [C.POINTER(Dims), C.c_int, C.POINTER(C.c_int), C.c_int,
                                                C.POINTER(C.c_void_p)]
@@ -266,7 +274,14 @@ class Handle:
         check(lib().srbd_qp_host_staging_f64(self._h, int(batch), C.byref(settings), C.byref(data),
                                              C.byref(sol)), "srbd_qp_host_staging_f64")
 
-    def solve_host(self, batch: int, settings: Settings, data, sol) -> None:
+    def solve_host(self, batch: int, settings: Settings, data, sol, on_factors=None) -> None:
+        """srbd_qp_solve_host_*; with `on_factors` (fp64), srbd_qp_solve_host_cb_f64: the
+        callable runs once P, p, K, k are final in `sol`'s buffers."""
+        if on_factors is not None:
+            cb = FACTORS_CB(lambda _ctx: on_factors())
+            check(lib().srbd_qp_solve_host_cb_f64(self._h, int(batch), C.byref(settings), C.byref(data),
+                                                  C.byref(sol), cb, None), "srbd_qp_solve_host_cb_f64")
+            return
         f = lib().srbd_qp_solve_host_f32 if isinstance(data, Data32) else lib().srbd_qp_solve_host_f64
         check(f(self._h, int(batch), C.byref(settings), C.byref(data), C.byref(sol)), f.__name__)
 

@@ -61,6 +61,10 @@ struct ProblemArgsT {
   // warm_start 2 only (internal: the fp64 continuation of srbd_qp_settings.f64_rescue):
   // per QP and stage the barrier state [kStLam block 96][nch chunks x 48], see ipm_box.hip
   const T* warm_bars;
+  // internal (srbd_qp_solve_host_cb_f64, zero-copy single-QP path): mapped host flags [batch]
+  // the latency kernel sets to 1 once P, p, K, k of that QP are in host memory (system
+  // scope), while its forward sweep still runs; null = those outputs are written at the end
+  int* factors_ready;
   // internal (srbd_qp_settings.f32_iters): end the IPM launch loop after the last corrector
   // step without the sweep that would apply it; the step is handed to the fp64 continuation
   int skip_last_rb;

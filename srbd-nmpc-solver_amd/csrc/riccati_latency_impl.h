@@ -51,7 +51,9 @@ __host__ __device__ constexpr int lat_scr_off(int N) { return lat_acl_off(N) + N
 __host__ __device__ constexpr int lat_scr_size(int N) {
   return (3 * N + 2) * 12 > 3 * kLatTile + 2 * kLatL ? (3 * N + 2) * 12 : 3 * kLatTile + 2 * kLatL;
 }
-size_t lat_lds_bytes(int N) { return (size_t)(lat_scr_off(N) + lat_scr_size(N)) * sizeof(double); }
+// (+ one double: the early-factor writers' arrival counter, an int)
+__host__ __device__ constexpr int lat_cnt_off(int N) { return lat_scr_off(N) + lat_scr_size(N); }
+size_t lat_lds_bytes(int N) { return (size_t)(lat_cnt_off(N) + 2) * sizeof(double); }
 // (one Newton step in lat_recip measured within the call pattern's noise, 99.0 / 99.8 vs
 // 100.2 / 99.9 us; streaming the stages into LDS during the sweep measured slower: DESIGN.md 9.1)
 
@@ -74,6 +76,33 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
   const bool cw = c <= 12;          // ... or the vector column
   const int cc = cv ? c : 11;       // clamped column for addressing
   auto rec = [&](int k) { return a.ws + ((size_t)k * a.batch + qp) * kWsStage; };
+  // hpipm-cpp's Riccati getters from stage k's record by one 16-lane group (lane = row of P,
+  // column of K): P (symmetric: column = row), p; [K | k] for k < N
+  auto put_P = [&](int k, int lane) {
+    if (lane >= 12) return;
+    const double* rk = rec(k);
+    double Pr[12];
+    load_packed_sym(rk + kWsP, lane, Pr);
+    if (a.P) store12(a.P + ((size_t)qp * (N + 1) + k) * 144 + (size_t)lane * 12, Pr);
+    if (a.p) a.p[((size_t)qp * (N + 1) + k) * 12 + lane] = rk[kWsp + lane];
+  };
+  auto put_K = [&](int k, int lane) {
+    if (lane >= 12) return;
+    const double* rk = rec(k);
+    if (a.k) a.k[((size_t)qp * N + k) * 12 + lane] = rk[kWsK + lane * kWsRow + 12];
+    if (a.K) {  // column `lane` of K (nu x nx, column-major)
+      double Kc[12];
+      sfor<0, 12>([&](auto i) { Kc[decltype(i)::value] = rk[kWsK + decltype(i)::value * kWsRow + lane]; });
+      store12(a.K + ((size_t)qp * N + k) * 144 + (size_t)lane * 12, Kc);
+    }
+  };
+  // Early factors (a.factors_ready): while wave 0 runs the forward sweep, waves 1.. copy the
+  // records to the host outputs and then set the QP's host flag -- the caller unpacks P and K
+  // under the kernel's tail (the forward sweep, u, pi, the residual pass).
+  const bool early = a.factors_ready != nullptr;
+  const int egrp = (threadIdx.x >> 4) - 4;  // 16-lane group among waves 1.. (0 = wave 1's first)
+  int* const ecnt = reinterpret_cast<int*>(img + lat_cnt_off(N));
+  if (threadIdx.x == 0) *ecnt = 0;  // (lds_copy_qp's barrier orders it before any arrival)
   tstamp(16);
   lds_copy_qp(a, img, qp);
 
@@ -241,6 +270,20 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
   if (wave == 1) finish_stage(0);
   __syncthreads();  // records and closed-loop rows complete; the scratch region is free
   tstamp(12);
+  if (early && wave >= 1) {
+    // stage items: P_0..P_N, then [K | k]_0..N-1, one per 16-lane group of waves 1..
+    for (int it = egrp; it <= 2 * N; it += kLatThreads / 16 - 4) {
+      if (it <= N)
+        put_P(it, l & 15);
+      else
+        put_K(it - N - 1, l & 15);
+    }
+    // each writer wave's stores out to host memory, then one arrival per wave; the last
+    // arrival sets the QP's host flag (system scope: a vector store past the caches)
+    __threadfence_system();
+    if ((l & 63) == 0 && atomicAdd(ecnt, 1) == kLatThreads / 64 - 2)
+      __hip_atomic_store(a.factors_ready + qp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 
   // ---------------- forward sweep: x_k+1 = Acl x_k + bcl (wave 0, row-owned) ----------------
   if (wave == 0) {
@@ -297,9 +340,10 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
         a.pi[((size_t)qp * (N + 1) + k) * 12 + lane] = piv;
         bad |= !(xk == xk);
       }
-      // hpipm-cpp's Riccati getters (P column = row: symmetric; p), when asked for
-      if (a.P && lane < 12) store12(a.P + ((size_t)qp * (N + 1) + k) * 144 + (size_t)lane * 12, Pr);
-      if (a.p && lane < 12) a.p[((size_t)qp * (N + 1) + k) * 12 + lane] = pv;
+      // hpipm-cpp's Riccati getters (P column = row: symmetric; p), when asked for and not
+      // written early
+      if (!early && a.P && lane < 12) store12(a.P + ((size_t)qp * (N + 1) + k) * 144 + (size_t)lane * 12, Pr);
+      if (!early && a.p && lane < 12) a.p[((size_t)qp * (N + 1) + k) * 12 + lane] = pv;
       if (k < N) {
         double Kr[12];
         sfor<0, 12>([&](auto j) { Kr[decltype(j)::value] = rk[kWsK + row * kWsRow + decltype(j)::value]; });
@@ -309,8 +353,8 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
           so[(N + 1) * 12 + k * 12 + lane] = uv;
           a.u[((size_t)qp * N + k) * 12 + lane] = uv;
           bad |= !(uv == uv);
-          if (a.k) a.k[((size_t)qp * N + k) * 12 + lane] = kv;
-          if (a.K) {  // column `lane` of K (nu x nx, column-major)
+          if (!early && a.k) a.k[((size_t)qp * N + k) * 12 + lane] = kv;
+          if (!early && a.K) {  // column `lane` of K (nu x nx, column-major)
             double Kc[12];
             sfor<0, 12>([&](auto i) { Kc[decltype(i)::value] = rk[kWsK + decltype(i)::value * kWsRow + lane]; });
             store12(a.K + ((size_t)qp * N + k) * 144 + (size_t)lane * 12, Kc);

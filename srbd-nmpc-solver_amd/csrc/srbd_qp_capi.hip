@@ -13,6 +13,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <chrono>
@@ -76,6 +77,10 @@ struct srbd_qp_handle_s {
   // control words, decided on the device (the host never waits on them)
   int* ctl = nullptr;
   int* qp_buf = nullptr;  // active-QP list of the IPM sweeps: capacity + 1 ints
+  // srbd_qp_solve_host_cb_f64: per-QP "factors written" flags (pinned, coherent, first use)
+  // and, for the one launch that arms them, their device address (ProblemArgsT::factors_ready)
+  int* fac_flags = nullptr;
+  int* fac_arm = nullptr;
 };
 
 extern "C" {
@@ -229,6 +234,7 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   if (h->resc2) hipFree(h->resc2);
   if (h->mixed) hipFree(h->mixed);
   if (h->resc_count_host) hipHostFree(h->resc_count_host);
+  if (h->fac_flags) hipHostFree(h->fac_flags);
   if (h->ctl) hipFree(h->ctl);
   if (h->qp_buf) hipFree(h->qp_buf);
   if (h->stream) hipStreamDestroy(h->stream);
@@ -366,6 +372,7 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   a.tol_eq = st->tol_eq;
   a.tol_ineq = st->tol_ineq;
   a.tol_comp = st->tol_comp;
+  if constexpr (std::is_same_v<T, double>) a.factors_ready = h->fac_arm;
   if (h->ctl) {
     a.ctl = h->ctl;
     a.ctl_cap = srbd::kCtlCap;
@@ -747,6 +754,8 @@ inline void spin_pause() {
 // (the blocking wait's wake-up costs about as much as the kernel), for at most this long; a
 // longer solve (or a hung one) falls back to the blocking wait, so no host core spins for more.
 constexpr auto kSpinBudget = std::chrono::milliseconds(2);
+// flags of srbd_qp_solve_host_cb_f64's early factors: the single-QP kernels' batch limit
+constexpr int kFacFlagsMax = 256;
 // host solves whose staged bytes fit this go through the handle's pinned buffer
 constexpr size_t kPinnedMaxBytes = size_t(8) << 20;
 struct Field {
@@ -759,10 +768,13 @@ struct Field {
 // stage_d / stage_s set (srbd_qp_host_staging_*): only lay out the pinned staging buffer for
 // the fields d / s mark and return pointers into it, so a caller can pack its QPs in place.
 // A host pointer that already is its field's place in the staging buffer is not copied.
+// on_factors (srbd_qp_solve_host_cb_f64): called once, on success, as soon as P, p, K, k are
+// in the caller's buffers -- mid-kernel on the zero-copy single-QP path, else at the end.
 template <typename T, typename DataT, typename SolT>
 static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                            const DataT* d, const SolT* s, DataT* stage_d = nullptr,
-                           SolT* stage_s = nullptr) {
+                           SolT* stage_s = nullptr, void (*on_factors)(void*) = nullptr,
+                           void* ctx = nullptr) {
   int rc = validate_call(h, batch, st, d, s);
   if (rc) return rc;
   if (batch == 0) return SRBD_QP_OK;
@@ -888,6 +900,23 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
     e = hipHostGetDevicePointer(&dev, pin, 0);
     if (e == hipSuccess) base = reinterpret_cast<char*>(dev);
   }
+  // early factors: the latency kernel sets fac_flags[qp] once the QP's P, p, K, k are written
+  // (system scope), and the caller's callback runs on them while the kernel finishes
+  bool arm = false;
+  if constexpr (std::is_same_v<T, double>) {
+    if (e == hipSuccess && zero_copy && on_factors && (s->P || s->p || s->K || s->k)) {
+      if (!h->fac_flags)
+        e = hipHostMalloc(reinterpret_cast<void**>(&h->fac_flags), sizeof(int) * kFacFlagsMax,
+                          hipHostMallocCoherent | hipHostMallocMapped);
+      void* dev = nullptr;
+      if (e == hipSuccess) e = hipHostGetDevicePointer(&dev, h->fac_flags, 0);
+      if (e == hipSuccess && batch <= kFacFlagsMax) {
+        for (int i = 0; i < batch; ++i) reinterpret_cast<volatile int*>(h->fac_flags)[i] = 0;
+        h->fac_arm = reinterpret_cast<int*>(dev);
+        arm = true;
+      }
+    }
+  }
   if (e == hipSuccess && small) {
     for (const Field& f : in)
       if (f.host != pin + f.off) std::memmove(pin + f.off, f.host, f.bytes);  // (staged in place: no copy)
@@ -932,6 +961,7 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
   ss.stat = dp(ostat);
   hipSetDevice(prev);
   rc = solve_impl<T>(h, batch, st, &dd, &ss, nullptr);
+  h->fac_arm = nullptr;
   if (rc) {
     // copies from the pinned buffer may still be queued: the next call must not
     // overwrite (or free) it under a pending DMA
@@ -943,20 +973,39 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
     if (e == hipSuccess && in_end < off && !zero_copy)
       e = hipMemcpyAsync(pin + in_end, base + in_end, off - in_end, hipMemcpyDeviceToHost, h->stream);
     // poll for the single-QP launch for at most kSpinBudget, then block (spin_pause above)
+    auto is_fac = [&](size_t o) { return o == oP || o == op || o == oK || o == ok; };
+    bool fired = false;
     if (e == hipSuccess && zero_copy) {
       const auto t_end = std::chrono::steady_clock::now() + kSpinBudget;
       hipError_t q;
-      while ((q = hipStreamQuery(h->stream)) == hipErrorNotReady && std::chrono::steady_clock::now() < t_end)
+      int seen = 0;  // QPs whose flag is up
+      while ((q = hipStreamQuery(h->stream)) == hipErrorNotReady && std::chrono::steady_clock::now() < t_end) {
+        if (arm && !fired) {
+          const volatile int* f = h->fac_flags;
+          while (seen < batch && f[seen]) ++seen;
+          if (seen == batch) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            for (const OutF& o : outs)
+              if (is_fac(o.off) && o.host != pin + o.off) std::memmove(o.host, pin + o.off, o.bytes);
+            on_factors(ctx);
+            fired = true;
+            continue;
+          }
+        }
         spin_pause();
+      }
       if (q != hipSuccess && q != hipErrorNotReady) e = q;
     }
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)
-      if (outs[i].host != pin + outs[i].off) std::memmove(outs[i].host, pin + outs[i].off, outs[i].bytes);
+      if (outs[i].host != pin + outs[i].off && !(fired && is_fac(outs[i].off)))
+        std::memmove(outs[i].host, pin + outs[i].off, outs[i].bytes);
+    if (e == hipSuccess && on_factors && !fired) on_factors(ctx);
   } else {
     for (size_t i = 0; e == hipSuccess && i < outs.size(); ++i)
       e = hipMemcpyAsync(outs[i].host, base + outs[i].off, outs[i].bytes, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess && on_factors) on_factors(ctx);
   }
   hipSetDevice(prev);
   if (e != hipSuccess) return fail(SRBD_QP_EDEVICE, std::string("device->host copy: ") + hipGetErrorString(e));
@@ -972,6 +1021,12 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
 int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                            const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s) {
   return solve_host_impl<double>(h, batch, st, d, s);
+}
+int srbd_qp_solve_host_cb_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
+                              const srbd_qp_data_f64* d, const srbd_qp_solution_f64* s,
+                              void (*on_factors)(void* ctx), void* ctx) {
+  return solve_host_impl<double, srbd_qp_data_f64, srbd_qp_solution_f64>(h, batch, st, d, s, nullptr, nullptr,
+                                                                       on_factors, ctx);
 }
 int srbd_qp_host_staging_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                              srbd_qp_data_f64* d, srbd_qp_solution_f64* s) {

@@ -87,6 +87,11 @@ void copy_mat(std::vector<double>& dst, size_t off, size_t ld, const double* src
 }
 // the leading rows x cols block of a column-major ld x * src into dst (ld = rows)
 void take_mat(double* dst, const double* src, size_t ld, size_t rows, size_t cols) {
+  if (rows == ld) {  // the whole block: one copy (the one-QP call's unpack is bound by these
+                     // reads of the pinned buffer the kernel wrote)
+    if (rows && cols) std::memcpy(dst, src, rows * cols * sizeof(double));
+    return;
+  }
   for (size_t c = 0; c < cols; ++c)
     if (rows) std::memcpy(dst + c * rows, src + c * ld, rows * sizeof(double));
 }
@@ -261,7 +266,9 @@ struct OcpQpIpmSolver::Impl {
 
   void pack(const std::vector<VectorXd>& x0s, const std::vector<std::vector<OcpQp>>& qps,
             const std::vector<std::vector<OcpQpSolution>>* warm, const Bufs* staged = nullptr);
-  std::vector<HpipmStatus> unpack(std::vector<std::vector<OcpQpSolution>>& sols);
+  // parts: kFactors (P, p, K, k), kRest (x, u, pi, statistics), or both
+  static constexpr int kFactors = 1, kRest = 2;
+  std::vector<HpipmStatus> unpack(std::vector<std::vector<OcpQpSolution>>& sols, int parts = kFactors | kRest);
 };
 
 void OcpQpIpmSolver::Impl::pack(const std::vector<VectorXd>& x0s,
@@ -415,35 +422,50 @@ void OcpQpIpmSolver::Impl::pack(const std::vector<VectorXd>& x0s,
 }
 
 std::vector<HpipmStatus> OcpQpIpmSolver::Impl::unpack(
-    std::vector<std::vector<OcpQpSolution>>& sols) {
+    std::vector<std::vector<OcpQpSolution>>& sols, int parts) {
   const size_t nb = sols.size(), N = shape.N, nx = shape.nx, nu = shape.nu;
   const size_t rows = static_cast<size_t>(settings.iter_max) + 2;
-  std::vector<HpipmStatus> out(nb);
+  std::vector<HpipmStatus> out;
+  if (parts & kFactors) {
+    for (size_t bi = 0; bi < nb; ++bi) {
+      std::vector<OcpQpSolution>& sol = sols[bi];
+      for (size_t kk = 0; kk <= N; ++kk) {
+        OcpQpSolution& s = sol[kk];
+        const size_t sk = bi * (N + 1) + kk;
+        const size_t xk = static_cast<size_t>(dim.nx[kk]);  // the stage's own dimensions
+        s.P.resize(xk, xk);
+        s.p.resize(xk);
+        take_mat(s.P.data(), buf.P + sk * nx * nx, nx, xk, xk);
+        std::memcpy(s.p.data(), buf.p + sk * nx, xk * sizeof(double));
+        if (kk < N) {
+          const size_t si = bi * N + kk, uk = static_cast<size_t>(dim.nu[kk]);
+          s.K.resize(uk, xk);
+          s.k.resize(uk);
+          take_mat(s.K.data(), buf.K + si * nu * nx, nu, uk, xk);
+          std::memcpy(s.k.data(), buf.k + si * nu, uk * sizeof(double));
+        } else {
+          s.k.resize(0);  // nu[N] = 0 (ocp_qp_ipm_solver.cpp:221-223)
+        }
+      }
+    }
+  }
+  if (!(parts & kRest)) return out;
+  out.resize(nb);
   batch_stats.resize(nb);
   for (size_t bi = 0; bi < nb; ++bi) {
     std::vector<OcpQpSolution>& sol = sols[bi];
     for (size_t kk = 0; kk <= N; ++kk) {
       OcpQpSolution& s = sol[kk];
       const size_t sk = bi * (N + 1) + kk;
-      const size_t xk = static_cast<size_t>(dim.nx[kk]);  // the stage's own dimensions
+      const size_t xk = static_cast<size_t>(dim.nx[kk]);
       s.x.resize(xk);
       s.pi.resize(xk);
-      s.P.resize(xk, xk);
-      s.p.resize(xk);
       std::memcpy(s.x.data(), buf.x + sk * nx, xk * sizeof(double));
       std::memcpy(s.pi.data(), buf.pi + sk * nx, xk * sizeof(double));
-      take_mat(s.P.data(), buf.P + sk * nx * nx, nx, xk, xk);
-      std::memcpy(s.p.data(), buf.p + sk * nx, xk * sizeof(double));
       if (kk < N) {
         const size_t si = bi * N + kk, uk = static_cast<size_t>(dim.nu[kk]);
         s.u.resize(uk);
-        s.K.resize(uk, xk);
-        s.k.resize(uk);
         std::memcpy(s.u.data(), buf.u + si * nu, uk * sizeof(double));
-        take_mat(s.K.data(), buf.K + si * nu * nx, nu, uk, xk);
-        std::memcpy(s.k.data(), buf.k + si * nu, uk * sizeof(double));
-      } else {
-        s.k.resize(0);  // nu[N] = 0 (ocp_qp_ipm_solver.cpp:221-223)
       }
     }
     OcpQpIpmSolverStatistics& st = batch_stats[bi];
@@ -581,12 +603,22 @@ std::vector<HpipmStatus> OcpQpIpmSolver::solveBatch(
       tp = PClock::now();
       m.pack(x0, ocp_qp, m.settings.warm_start ? &qp_sol : nullptr, &bs);
       if (g_prof.on) g_prof.t[1] += us_since(tp);
+      // the factors (P, p, K, k: most of the outputs) are unpacked by the callback, while
+      // the kernel still runs its forward sweep (srbd_qp_solve_host_cb_f64)
+      struct Ctx {
+        Impl* m;
+        std::vector<std::vector<OcpQpSolution>>* sol;
+      } cx{&m, &qp_sol};
+      auto on_factors = [](void* p) {
+        Ctx* c = static_cast<Ctx*>(p);
+        c->m->unpack(*c->sol, Impl::kFactors);
+      };
       tp = PClock::now();
-      if (srbd_qp_solve_host_f64(m.handle, nb, &st, &d, &o) != SRBD_QP_OK)
+      if (srbd_qp_solve_host_cb_f64(m.handle, nb, &st, &d, &o, on_factors, &cx) != SRBD_QP_OK)
         abi_error("OcpQpIpmSolver::solve");
       if (g_prof.on) g_prof.t[2] += us_since(tp);
       tp = PClock::now();
-      std::vector<HpipmStatus> res = m.unpack(qp_sol);
+      std::vector<HpipmStatus> res = m.unpack(qp_sol, Impl::kRest);
       if (g_prof.on) {
         g_prof.t[3] += us_since(tp);
         ++g_prof.n;

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol(pkg):
 
 def test_abi_version_and_strings(pkg):
     L = pkg.capi.lib()
-    assert L.srbd_qp_abi_version() == 11
+    assert L.srbd_qp_abi_version() == 12
     # hpipm::to_string (ocp_qp_ipm_solver.cpp:19-33)
     assert pkg.capi.status_string(0) == "HpipmStatus::Success"
     assert pkg.capi.status_string(1) == "HpipmStatus::MaxIterReached"

@@ -398,3 +398,76 @@ def test_host_staging_in_place(pkg):
             assert np.all(arr(o.status, (nb,), C.c_int) == 0)
         finally:
             h.close()
+
+
+def test_host_solve_early_factors(pkg):
+    """srbd_qp_solve_host_cb_f64 (ABI 12): the callback runs exactly once, and at that point
+    P, p, K, k in the staged outputs already hold their final values (on the zero-copy
+    single-QP path the latency kernel writes them and raises a flag per QP before its forward
+    sweep ends); every output equals the plain host solve's bit for bit.  N = 20 takes the
+    early path (batch 1 and 8 flags); N = 26 (zero copy, not the latency kernel) and staging
+    through non-pinned caller buffers call back after the solve."""
+    import ctypes as C
+    capi = pkg.capi
+    keys_in = ("A", "B", "b", "Q", "S", "R", "q", "r", "x0")
+    keys_out = ("x", "u", "pi", "P", "p", "K", "k", "status", "iter", "res", "obj")
+
+    def arr(ptr, n, ct=C.c_double):
+        return np.ctypeslib.as_array((ct * n).from_address(ptr)).copy()
+
+    for N, nb in ((20, 1), (20, 8), (26, 2)):
+        qp, x0 = pkg.srbd_model.generate_batch(nb, N=N, seed=90 + N + nb, constraints="none")
+        p = qp.packed()
+        p["x0"] = np.ascontiguousarray(x0)
+        sizes = dict(x=nb * (N + 1) * 12, u=nb * N * 12, pi=nb * (N + 1) * 12, P=nb * (N + 1) * 144,
+                     p=nb * (N + 1) * 12, K=nb * N * 144, k=nb * N * 12, res=nb * 4, obj=nb)
+        results = []
+        for early in (False, True):
+            h = capi.Handle(N, 12, 12, capacity=nb)
+            try:
+                s = capi.settings_struct(dict(ric_alg=0))
+                d = capi.Data(**{k: 16 for k in keys_in})
+                o = capi.Solution(**{k: 16 for k in keys_out})
+                h.host_staging(nb, s, d, o)
+                for k in keys_in:
+                    src = np.ascontiguousarray(p[k], dtype=np.float64)
+                    C.memmove(getattr(d, k), src.ctypes.data, src.nbytes)
+                seen = []
+                if early:
+                    h.solve_host(nb, s, d, o, on_factors=lambda: seen.append(
+                        {k: arr(getattr(o, k), sizes[k]) for k in ("P", "p", "K", "k")}))
+                else:
+                    h.solve_host(nb, s, d, o)
+                out = {k: arr(getattr(o, k), n) for k, n in sizes.items()}
+                out["status"] = arr(o.status, nb, C.c_int)
+                if early:
+                    assert len(seen) == 1, (N, nb)
+                    for k, v in seen[0].items():
+                        assert np.array_equal(v, out[k]), (N, nb, k)
+                results.append(out)
+            finally:
+                h.close()
+        for k in results[0]:
+            assert np.array_equal(results[0][k], results[1][k]), (N, nb, k)
+        assert np.all(results[1]["status"] == 0)
+
+    # caller-owned (non-staged) output buffers: the factors are copied out before the callback
+    qp, x0 = pkg.srbd_model.generate_batch(1, N=20, seed=7, constraints="none")
+    ref = capi.solve(qp, x0, dict(ric_alg=0), riccati=True)
+    p = qp.packed()
+    p["x0"] = np.ascontiguousarray(x0)
+    ins = {k: np.ascontiguousarray(p[k], dtype=np.float64) for k in keys_in}
+    outs = dict(x=np.zeros(21 * 12), u=np.zeros(20 * 12), pi=np.zeros(21 * 12), P=np.zeros(21 * 144),
+                p=np.zeros(21 * 12), K=np.zeros(20 * 144), k=np.zeros(20 * 12))
+    h = capi.Handle(20, 12, 12, capacity=1)
+    try:
+        s = capi.settings_struct(dict(ric_alg=0))
+        d = capi.Data(**{k: v.ctypes.data for k, v in ins.items()})
+        o = capi.Solution(**{k: v.ctypes.data for k, v in outs.items()})
+        seen = []
+        h.solve_host(1, s, d, o, on_factors=lambda: seen.append(outs["K"].copy()))
+        assert len(seen) == 1 and np.array_equal(seen[0], outs["K"])
+        assert np.array_equal(np.swapaxes(outs["K"].reshape(1, 20, 12, 12), -1, -2), ref["K"])
+        assert np.array_equal(outs["u"].reshape(ref["u"].shape), ref["u"])
+    finally:
+        h.close()
