@@ -24,3 +24,21 @@ for kind in ("kernel_stats", "hip_api_stats"):
     for x in csv.DictReader(open(fs[0])):
         print(kind, x["Name"][:60], x["Calls"], "avg %.1f us" % (float(x["AverageNs"]) / 1e3), "tot %.0f us" % (float(x["TotalDurationNs"]) / 1e3))
 PY
+python3 - <<'PY'
+# per-call timeline (medians): launch API, launch end -> kernel start, kernel, kernel end -> the
+# host's last stream query / synchronize of that call
+import csv, glob, statistics as stt
+kt = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in
+            csv.DictReader(open(glob.glob("gpurun_out/prof_call/**/*kernel_trace.csv", recursive=True)[0])))
+api = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"]), x["Function"]) for x in
+             csv.DictReader(open(glob.glob("gpurun_out/prof_call/**/*hip_api_trace.csv", recursive=True)[0])))
+launches = [a for a in api if a[2] == "hipLaunchKernel"]
+waits = [a for a in api if a[2] in ("hipStreamQuery", "hipStreamSynchronize")]
+rows = []
+for (ls, le, _), (ks, ke) in zip(launches, kt):
+    after = [w for w in waits if w[0] >= ke]
+    if not after: continue
+    rows.append((le - ls, ks - le, ke - ks, after[0][1] - ke))
+for i, name in enumerate(("launch API", "launch end -> kernel start", "kernel", "kernel end -> host sees it")):
+    print("timeline %-28s median %.1f us" % (name, stt.median(r[i] for r in rows) / 1e3))
+PY

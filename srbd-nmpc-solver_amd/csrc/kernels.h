@@ -155,6 +155,22 @@ bool unconstr_fused_residuals(const ProblemArgsT<T>& a);
 template <typename T>
 bool unconstr_reads_once(const ProblemArgsT<T>& a);
 
+// The one-QP host call's resident server (riccati_latency_impl.h): the mailbox lives in
+// mapped, coherent host memory; the host writes seq / quit, the kernel done / exited.
+struct LatMailbox {
+  int seq;     // host: number of the request posted last
+  int quit;    // host: leave now
+  int done;    // device: number of the request finished last
+  int exited;  // device: epoch of the server launch that has left
+};
+// true when launch_riccati_unconstr(a) would be one latency-kernel workgroup reading its QP
+// once (batch 1, classical Riccati, N <= 20): the server can take the call instead
+bool latency_server_ok(const ProblemArgsT<double>& a);
+// the server on `stream` (dedicated: it stays until quit or idle_ticks of wall clock with no
+// request); requests after last_done are served
+hipError_t launch_latency_server(const ProblemArgsT<double>& a, LatMailbox* mb, int epoch, int last_done,
+                                 long long idle_ticks, hipStream_t stream);
+
 // nx < 12 or nu < 12: embed the problem in 12 x 12 stages (pad.hip).  pad_elems
 // is the pad buffer size (elements of T); pad_problem fills it from `a` and
 // returns the padded arguments in `o` (solution pointers into the buffer);

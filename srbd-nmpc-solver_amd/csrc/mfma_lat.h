@@ -19,6 +19,14 @@ __device__ __forceinline__ lat_d4 lat_mfma(double a, double b, lat_d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// An opaque copy of an index: the resident server (riccati_latency_impl.h) runs the solve in a
+// loop, and the compiler would otherwise hoist the solve's address arithmetic out of it and
+// keep it live across the whole solve (620 B/lane of scratch).
+__device__ __forceinline__ int lat_opq(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // 1 / d by v_rcp_f64 and two Newton steps (3 dependent FMAs instead of the IEEE division's
 // ~10 instructions on the stage's critical path)
 __device__ __forceinline__ double lat_recip(double d) {

@@ -57,9 +57,9 @@ size_t lat_lds_bytes(int N) { return (size_t)(lat_cnt_off(N) + 2) * sizeof(doubl
 // (one Newton step in lat_recip measured within the call pattern's noise, 99.0 / 99.8 vs
 // 100.2 / 99.9 us; streaming the stages into LDS during the sweep measured slower: DESIGN.md 9.1)
 
+// One QP (blockIdx.x) of `a` by the whole workgroup, LDS at lds_raw (lat_lds_bytes(N)).
 template <bool RES>
-__global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(ProblemArgsT<double> a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+__device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigned char* lds_raw) {
   double* const img = reinterpret_cast<double*>(lds_raw);
   const int N = a.N;
   double* const acl = img + lat_acl_off(N);
@@ -68,9 +68,10 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
   double* const ybuf = scr + kLatTile;      // [Y | y] of stages k (k & 1)
   double* const lbuf = scr + 3 * kLatTile;  // L packed + 1 / diag (k & 1)
   double* const so = scr;                   // after the sweep: x [N+1][12], u [N][12], pi [N+1][12]
-  const int qp = blockIdx.x;
-  const int wave = threadIdx.x >> 6;
-  const int l = threadIdx.x & 63;
+  const int qp = lat_opq(blockIdx.x);
+  const int tid = lat_opq(threadIdx.x);
+  const int wave = tid >> 6;
+  const int l = tid & 63;
   const int g = l >> 4, c = l & 15;  // tile row block, column
   const bool cv = c < 12;           // a column of a 12 x 12 block
   const bool cw = c <= 12;          // ... or the vector column
@@ -100,11 +101,13 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
   // records to the host outputs and then set the QP's host flag -- the caller unpacks P and K
   // under the kernel's tail (the forward sweep, u, pi, the residual pass).
   const bool early = a.factors_ready != nullptr;
-  const int egrp = (threadIdx.x >> 4) - 4;  // 16-lane group among waves 1.. (0 = wave 1's first)
+  const int egrp = (tid >> 4) - 4;  // 16-lane group among waves 1.. (0 = wave 1's first)
   int* const ecnt = reinterpret_cast<int*>(img + lat_cnt_off(N));
-  if (threadIdx.x == 0) *ecnt = 0;  // (lds_copy_qp's barrier orders it before any arrival)
+  if (tid == 0) *ecnt = 0;  // (the copy's barrier orders it before any arrival)
   tstamp(16);
-  lds_copy_qp(a, img, qp);
+  lds_copy_range(a, img, qp, 0, (N + 1) * kImgStage, tid, kLdsCopyThreads);  // (lds_copy_qp)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
   // ---------------- backward sweep ----------------
   lat_d4 Pt;  // [P | p]_k+1 (wave 0)
@@ -278,9 +281,10 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
       else
         put_K(it - N - 1, l & 15);
     }
-    // each writer wave's stores out to host memory, then one arrival per wave; the last
-    // arrival sets the QP's host flag (system scope: a vector store past the caches)
-    __threadfence_system();
+    // each writer wave waits for its stores to reach the cache, then arrives; the last
+    // arrival writes the cache back to host memory and sets the QP's host flag (the system-
+    // scope release store: one L2 write-back for all waves, then a vector store)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if ((l & 63) == 0 && atomicAdd(ecnt, 1) == kLatThreads / 64 - 2)
       __hip_atomic_store(a.factors_ready + qp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -325,8 +329,8 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
   // ---------------- every stage at once: u_k = K x_k + k, pi_k = P x_k + p ----------------
   bool bad = false;
   {
-    const int grp = threadIdx.x >> 4;  // one 16-lane group per stage
-    const int lane = threadIdx.x & 15;
+    const int grp = tid >> 4;  // one 16-lane group per stage
+    const int lane = tid & 15;
     const int row = lane < 12 ? lane : 11;
     for (int k = grp; k <= N; k += kLatThreads / 16) {
       const double* rk = rec(k);
@@ -364,7 +368,7 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
     }
   }
   const int any_bad = __syncthreads_or(bad);
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     if (a.status) a.status[qp] = any_bad ? 3 : 0;
     if (a.iter) a.iter[qp] = 0;
   }
@@ -373,9 +377,61 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
     acc.img = img;
     acc.so = so;
     acc.N = N;
-    unconstr_residuals_body(a, acc, qp);
+    unconstr_residuals_body(a, acc, qp, tid);
   }
+}
+
+template <bool RES>
+__global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(ProblemArgsT<double> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  lat_solve<RES>(a, lds_raw);
+}
+
+// The same solve as a resident server for the one-QP host call (srbd_qp_capi.hip, the
+// reference's call pattern): one workgroup stays on its CU and polls the mailbox in mapped
+// host memory, so a call costs no launch, no dispatch and no completion signal -- the host
+// posts a request number, the kernel solves the QP from the (fixed) staging buffer `a` points
+// into and writes the number back.  It leaves on `quit`, or after idle_ticks (wall clock) with
+// no request, recording its epoch in `exited`; the host relaunches it then.
+template <bool RES>
+__global__ void __launch_bounds__(kLatThreads, 1)
+    riccati_latency_server_kernel(ProblemArgsT<double> a, LatMailbox* mb, int epoch, int last_done,
+                                  long long idle_ticks) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  int* const req = reinterpret_cast<int*>(reinterpret_cast<double*>(lds_raw) + lat_cnt_off(a.N)) + 1;
+  long long t0 = wall_clock64();
+  for (;;) {
+    if (threadIdx.x == 0) {
+      int r = -1;
+      for (;;) {
+        const int sq = __hip_atomic_load(&mb->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (sq != last_done) {
+          r = sq;
+          break;
+        }
+        if (__hip_atomic_load(&mb->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        if (wall_clock64() - t0 > idle_ticks) break;
+        __builtin_amdgcn_s_sleep(8);
+      }
+      // the request's inputs: drop any cached copy of the mapped staging buffer
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      *req = r;
+    }
+    __syncthreads();
+    const int r = *req;
+    if (r < 0) break;
+    lat_solve<RES>(a, lds_raw);
+    // every wave's outputs in the cache, then one write-back to host memory with the answer
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&mb->done, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    last_done = r;
+    t0 = wall_clock64();
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&mb->exited, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // the latency kernel's LDS fits the device (N <= 20 at fp64)
 bool lat_fits(int N) { return lat_lds_bytes(N) + kLdsResStatic <= kLdsBytesMax; }
+
+// (LatMailbox, the server's launch and its eligibility: kernels.h)

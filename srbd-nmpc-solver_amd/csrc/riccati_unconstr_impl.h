@@ -465,18 +465,19 @@ struct ResLds : LdsSrc {
 // workgroup reduction).  Threads >= kResStages * 12 only take part in the reduction, so a
 // 512-thread workgroup sums the same partial results in the same order as a 256-thread one.
 template <class Acc>
-__device__ __forceinline__ void unconstr_residuals_body(const ProblemArgsT<real>& a, const Acc& acc, int qp) {
+// (t: the thread's index in the workgroup, passed in so a caller can make it opaque)
+__device__ __forceinline__ void unconstr_residuals_body(const ProblemArgsT<real>& a, const Acc& acc, int qp, int t) {
   const int N = a.N, nx = a.nx, nu = a.nu;
   if (a.stat) {  // the QP's stat table is cleared here (no separate memset), row 0 filled below
     real* tab = a.stat + (size_t)qp * a.stat_rows * kStatCols;
-    for (int i = threadIdx.x; i < a.stat_rows * kStatCols; i += blockDim.x) tab[i] = real(0);
+    for (int i = t; i < a.stat_rows * kStatCols; i += blockDim.x) tab[i] = real(0);
   }
   const real* x = acc.x();
   const real* u = acc.u();
   const real* pi = acc.pi();
-  const int i = threadIdx.x % 12;
+  const int i = t % 12;
   real mg = real(0), mb = real(0), ob = real(0);
-  for (int k = threadIdx.x / 12; threadIdx.x < kResStages * 12 && k <= N; k += kResStages) {
+  for (int k = t / 12; t < kResStages * 12 && k <= N; k += kResStages) {
     const real* xk = x + (size_t)k * nx;
     if (k < N) {
       const real* uk = u + (size_t)k * nu;
@@ -529,14 +530,14 @@ __device__ __forceinline__ void unconstr_residuals_body(const ProblemArgsT<real>
     ob += __shfl_xor(ob, m);
   }
   __shared__ real part[3][kResWavesMax];
-  const int w = threadIdx.x / 64;
-  if ((threadIdx.x & 63) == 0) {
+  const int w = t / 64;
+  if ((t & 63) == 0) {
     part[0][w] = mg;
     part[1][w] = mb;
     part[2][w] = ob;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     // (waves past the stage-parallel ones hold 0 and add nothing)
     mg = part[0][0], mb = part[1][0], ob = part[2][0];
     for (int j = 1; j < kResThreads / 64; ++j) {
@@ -562,7 +563,7 @@ __device__ __forceinline__ void unconstr_residuals_body(const ProblemArgsT<real>
 }
 
 __global__ void __launch_bounds__(kResThreads) unconstr_residuals_kernel(ProblemArgsT<real> a) {
-  unconstr_residuals_body(a, ResGlobal{a, (int)blockIdx.x}, (int)blockIdx.x);
+  unconstr_residuals_body(a, ResGlobal{a, (int)blockIdx.x}, (int)blockIdx.x, (int)threadIdx.x);
 }
 
 // The reference's call pattern in one launch (one QP per workgroup, the C-ABI's small
@@ -590,7 +591,7 @@ __global__ void __launch_bounds__(kLdsCopyThreads, 1) riccati_unconstr_lds_res_k
   acc.img = img;
   acc.so = so;
   acc.N = a.N;
-  unconstr_residuals_body(a, acc, qp);
+  unconstr_residuals_body(a, acc, qp, (int)threadIdx.x);
 }
 
 // The same residuals for large batches, on the solve's layout: one 16-lane group per QP
@@ -797,6 +798,25 @@ static hipError_t launch_alg(const ProblemArgsT<real>& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+#if SRBD_WITH_LATENCY
+// the launch of `a` is one latency-kernel workgroup that reads its QP once (the resident
+// server can take it: one QP, classical Riccati, residuals fused or not asked for)
+bool server_ok(const ProblemArgsT<real>& a) {
+  return a.batch == 1 && !a.ric_alg && lat_eligible(a) && reads_once(a);
+}
+hipError_t launch_server(const ProblemArgsT<real>& a, LatMailbox* mb, int epoch, int last_done,
+                         long long idle_ticks, hipStream_t stream) {
+  if (!server_ok(a)) return hipErrorInvalidValue;
+  if (fused_residuals(a))
+    hipLaunchKernelGGL(riccati_latency_server_kernel<true>, dim3(1), dim3(kLatThreads), lat_lds_bytes(a.N), stream,
+                       a, mb, epoch, last_done, idle_ticks);
+  else
+    hipLaunchKernelGGL(riccati_latency_server_kernel<false>, dim3(1), dim3(kLatThreads), lat_lds_bytes(a.N), stream,
+                       a, mb, epoch, last_done, idle_ticks);
+  return hipGetLastError();
+}
+#endif
+
 // Per-device launch attributes, set on the current device (srbd_qp_create calls this
 // after selecting the handle's device; hipFuncSetAttribute is per device, and every
 // handle sets it, so concurrent handles on any device need no shared flag).
@@ -819,6 +839,12 @@ hipError_t prepare_device() {
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
   if (e == hipSuccess)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_latency_kernel<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_latency_server_kernel<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&riccati_latency_server_kernel<true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytesMax - kLdsResStatic));
 #endif
   return e;

@@ -471,3 +471,59 @@ def test_host_solve_early_factors(pkg):
         assert np.array_equal(outs["u"].reshape(ref["u"].shape), ref["u"])
     finally:
         h.close()
+
+
+def test_host_solve_resident_server(pkg, monkeypatch):
+    """The one-QP host call's resident server (riccati_latency_server_kernel): a sequence of
+    different QPs through one handle -- back to back, after the server has idled out (5 ms),
+    across a change of settings (the server is relaunched with the new arguments) and with the
+    early-factor callback -- gives the launched kernel's results bit for bit
+    (SRBD_LAT_SERVER=0: every call launches)."""
+    import ctypes as C
+    import time
+    capi = pkg.capi
+    keys_in = ("A", "B", "b", "Q", "S", "R", "q", "r", "x0")
+    keys_out = ("x", "u", "pi", "P", "p", "K", "k", "status", "iter", "res", "obj")
+    sizes = dict(x=21 * 12, u=20 * 12, pi=21 * 12, P=21 * 144, p=21 * 12, K=20 * 144, k=20 * 12, res=4, obj=1)
+
+    def run(server, seeds, gaps, cfgs, cbs):
+        monkeypatch.setenv("SRBD_LAT_SERVER", "1" if server else "0")
+        h = capi.Handle(20, 12, 12, capacity=1)
+        outs = []
+        try:
+            for seed, gap, cfg, cb in zip(seeds, gaps, cfgs, cbs):
+                time.sleep(gap)
+                qp, x0 = pkg.srbd_model.generate_batch(1, N=20, seed=seed, constraints="none")
+                p = qp.packed()
+                p["x0"] = np.ascontiguousarray(x0)
+                s = capi.settings_struct(cfg)
+                d = capi.Data(**{k: 16 for k in keys_in})
+                o = capi.Solution(**{k: 16 for k in keys_out})
+                h.host_staging(1, s, d, o)
+                for k in keys_in:
+                    src = np.ascontiguousarray(p[k], dtype=np.float64)
+                    C.memmove(getattr(d, k), src.ctypes.data, src.nbytes)
+                calls = []
+                h.solve_host(1, s, d, o, on_factors=(lambda: calls.append(1)) if cb else None)
+                r = {k: np.ctypeslib.as_array((C.c_double * n).from_address(getattr(o, k))).copy()
+                     for k, n in sizes.items() if getattr(o, k)}
+                r["status"] = np.ctypeslib.as_array((C.c_int * 1).from_address(o.status)).copy()
+                assert len(calls) == (1 if cb else 0)
+                outs.append(r)
+        finally:
+            h.close()
+        return outs
+
+    seeds = [11, 12, 13, 14, 15, 16, 17]
+    gaps = [0, 0, 0, 0.03, 0, 0, 0.03]
+    cfgs = [dict(ric_alg=0)] * 3 + [dict(ric_alg=0, compute_residuals=0), dict(ric_alg=0)] * 2
+    cbs = [False, True, True, False, True, False, False]
+    a = run(True, seeds, gaps, cfgs, cbs)
+    b = run(False, seeds, gaps, cfgs, cbs)
+    for i, (ra, rb) in enumerate(zip(a, b)):
+        assert ra.keys() == rb.keys()
+        for k in ra:
+            assert np.array_equal(ra[k], rb[k]), (i, k)
+        assert ra["status"][0] == 0
+    # distinct QPs gave distinct answers (no stale staging data)
+    assert not np.array_equal(a[0]["u"], a[1]["u"])
