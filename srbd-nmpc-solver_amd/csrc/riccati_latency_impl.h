@@ -77,28 +77,8 @@ __device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigne
   const bool cw = c <= 12;          // ... or the vector column
   const int cc = cv ? c : 11;       // clamped column for addressing
   auto rec = [&](int k) { return a.ws + ((size_t)k * a.batch + qp) * kWsStage; };
-  // hpipm-cpp's Riccati getters from stage k's record by one 16-lane group (lane = row of P,
-  // column of K): P (symmetric: column = row), p; [K | k] for k < N
-  auto put_P = [&](int k, int lane) {
-    if (lane >= 12) return;
-    const double* rk = rec(k);
-    double Pr[12];
-    load_packed_sym(rk + kWsP, lane, Pr);
-    if (a.P) store12(a.P + ((size_t)qp * (N + 1) + k) * 144 + (size_t)lane * 12, Pr);
-    if (a.p) a.p[((size_t)qp * (N + 1) + k) * 12 + lane] = rk[kWsp + lane];
-  };
-  auto put_K = [&](int k, int lane) {
-    if (lane >= 12) return;
-    const double* rk = rec(k);
-    if (a.k) a.k[((size_t)qp * N + k) * 12 + lane] = rk[kWsK + lane * kWsRow + 12];
-    if (a.K) {  // column `lane` of K (nu x nx, column-major)
-      double Kc[12];
-      sfor<0, 12>([&](auto i) { Kc[decltype(i)::value] = rk[kWsK + decltype(i)::value * kWsRow + lane]; });
-      store12(a.K + ((size_t)qp * N + k) * 144 + (size_t)lane * 12, Kc);
-    }
-  };
-  // Early factors (a.factors_ready): while wave 0 runs the forward sweep, waves 1.. copy the
-  // records to the host outputs and then set the QP's host flag -- the caller unpacks P and K
+  // Early factors (a.factors_ready): the Riccati getters' outputs are written while wave 0 runs
+  // the forward sweep (below), then the QP's host flag is set -- the caller unpacks P and K
   // under the kernel's tail (the forward sweep, u, pi, the residual pass).
   const bool early = a.factors_ready != nullptr;
   const int egrp = (tid >> 4) - 4;  // 16-lane group among waves 1.. (0 = wave 1's first)
@@ -106,8 +86,10 @@ __device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigne
   if (tid == 0) *ecnt = 0;  // (the copy's barrier orders it before any arrival)
   tstamp(16);
   lds_copy_range(a, img, qp, 0, (N + 1) * kImgStage, tid, kLdsCopyThreads);  // (lds_copy_qp)
+  tstamp(14);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  tstamp(15);
 
   // ---------------- backward sweep ----------------
   lat_d4 Pt;  // [P | p]_k+1 (wave 0)
@@ -273,20 +255,46 @@ __device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigne
   if (wave == 1) finish_stage(0);
   __syncthreads();  // records and closed-loop rows complete; the scratch region is free
   tstamp(12);
-  if (early && wave >= 1) {
-    // stage items: P_0..P_N, then [K | k]_0..N-1, one per 16-lane group of waves 1..
-    for (int it = egrp; it <= 2 * N; it += kLatThreads / 16 - 4) {
-      if (it <= N)
-        put_P(it, l & 15);
-      else
-        put_K(it - N - 1, l & 15);
+
+  // ---- the factors' rows, by waves 1.. while wave 0 runs the forward sweep: items P_0..P_N,
+  // then [K | k]_0..N-1, at most two per 16-lane group (lane = row; lanes 12..15 repeat row
+  // 11).  Each is written to the Riccati getters' outputs (P symmetric: row = column; K is
+  // nu x nx column-major, so a row is 12 strided stores, each contiguous across the group's
+  // lanes) and kept for u_k = K x_k + k, pi_k = P x_k + p after the sweep. ----
+  constexpr int kItemGroups = kLatThreads / 16 - 4;  // waves 1..7
+  static_assert(2 * kItemGroups >= 2 * 20 + 1, "two items per group cover N <= 20 (lat_fits)");
+  const int lane = l & 15, row = lane < 12 ? lane : 11;
+  double V[2][12], vv[2];
+  if (wave >= 1) {
+    sfor<0, 2>([&](auto ss) {
+      constexpr int S = decltype(ss)::value;
+      const int it = egrp + S * kItemGroups;
+      if (it <= N) {
+        const double* rk = rec(it);
+        load_packed_sym(rk + kWsP, row, V[S]);
+        vv[S] = rk[kWsp + row];
+        if (a.P && lane < 12) store12(a.P + ((size_t)qp * (N + 1) + it) * 144 + (size_t)lane * 12, V[S]);
+        if (a.p && lane < 12) a.p[((size_t)qp * (N + 1) + it) * 12 + lane] = vv[S];
+      } else if (it <= 2 * N) {
+        const int k = it - N - 1;
+        const double* rk = rec(k);
+        sfor<0, 12>([&](auto j) { V[S][decltype(j)::value] = rk[kWsK + row * kWsRow + decltype(j)::value]; });
+        vv[S] = rk[kWsK + row * kWsRow + 12];
+        if (a.k && lane < 12) a.k[((size_t)qp * N + k) * 12 + lane] = vv[S];
+        if (a.K && lane < 12) {
+          double* ko = a.K + ((size_t)qp * N + k) * 144 + lane;
+          sfor<0, 12>([&](auto j) { ko[decltype(j)::value * 12] = V[S][decltype(j)::value]; });
+        }
+      }
+    });
+    if (early) {
+      // each writer wave waits for its stores to reach the cache, then arrives; the last
+      // arrival writes the cache back to host memory and sets the QP's host flag (the system-
+      // scope release store: one L2 write-back for all waves, then a vector store)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if ((l & 63) == 0 && atomicAdd(ecnt, 1) == kLatThreads / 64 - 2)
+        __hip_atomic_store(a.factors_ready + qp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    // each writer wave waits for its stores to reach the cache, then arrives; the last
-    // arrival writes the cache back to host memory and sets the QP's host flag (the system-
-    // scope release store: one L2 write-back for all waves, then a vector store)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if ((l & 63) == 0 && atomicAdd(ecnt, 1) == kLatThreads / 64 - 2)
-      __hip_atomic_store(a.factors_ready + qp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 
   // ---------------- forward sweep: x_k+1 = Acl x_k + bcl (wave 0, row-owned) ----------------
@@ -328,46 +336,30 @@ __device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigne
 
   // ---------------- every stage at once: u_k = K x_k + k, pi_k = P x_k + p ----------------
   bool bad = false;
-  {
-    const int grp = tid >> 4;  // one 16-lane group per stage
-    const int lane = tid & 15;
-    const int row = lane < 12 ? lane : 11;
-    for (int k = grp; k <= N; k += kLatThreads / 16) {
-      const double* rk = rec(k);
-      const double xk = lane < 12 ? so[k * 12 + lane] : 0.0;
-      double Pr[12];
-      load_packed_sym(rk + kWsP, row, Pr);
-      const double pv = rk[kWsp + row];
-      const double piv = dot_bcast(Pr, xk, pv);
-      if (lane < 12) {
-        so[(2 * N + 1) * 12 + k * 12 + lane] = piv;
-        a.pi[((size_t)qp * (N + 1) + k) * 12 + lane] = piv;
-        bad |= !(xk == xk);
-      }
-      // hpipm-cpp's Riccati getters (P column = row: symmetric; p), when asked for and not
-      // written early
-      if (!early && a.P && lane < 12) store12(a.P + ((size_t)qp * (N + 1) + k) * 144 + (size_t)lane * 12, Pr);
-      if (!early && a.p && lane < 12) a.p[((size_t)qp * (N + 1) + k) * 12 + lane] = pv;
-      if (k < N) {
-        double Kr[12];
-        sfor<0, 12>([&](auto j) { Kr[decltype(j)::value] = rk[kWsK + row * kWsRow + decltype(j)::value]; });
-        const double kv = rk[kWsK + row * kWsRow + 12];
-        const double uv = dot_bcast(Kr, xk, kv);
+  if (wave >= 1) {
+    sfor<0, 2>([&](auto ss) {
+      constexpr int S = decltype(ss)::value;
+      const int it = egrp + S * kItemGroups;
+      if (it <= 2 * N) {
+        const int k = it <= N ? it : it - N - 1;
+        const double xk = lane < 12 ? so[k * 12 + lane] : 0.0;
+        const double v = dot_bcast(V[S], xk, vv[S]);
         if (lane < 12) {
-          so[(N + 1) * 12 + k * 12 + lane] = uv;
-          a.u[((size_t)qp * N + k) * 12 + lane] = uv;
-          bad |= !(uv == uv);
-          if (!early && a.k) a.k[((size_t)qp * N + k) * 12 + lane] = kv;
-          if (!early && a.K) {  // column `lane` of K (nu x nx, column-major)
-            double Kc[12];
-            sfor<0, 12>([&](auto i) { Kc[decltype(i)::value] = rk[kWsK + decltype(i)::value * kWsRow + lane]; });
-            store12(a.K + ((size_t)qp * N + k) * 144 + (size_t)lane * 12, Kc);
+          if (it <= N) {
+            so[(2 * N + 1) * 12 + k * 12 + lane] = v;
+            a.pi[((size_t)qp * (N + 1) + k) * 12 + lane] = v;
+            bad |= !(xk == xk);
+          } else {
+            so[(N + 1) * 12 + k * 12 + lane] = v;
+            a.u[((size_t)qp * N + k) * 12 + lane] = v;
+            bad |= !(v == v);
           }
         }
       }
-    }
+    });
   }
   const int any_bad = __syncthreads_or(bad);
+  tstamp(17);
   if (tid == 0) {
     if (a.status) a.status[qp] = any_bad ? 3 : 0;
     if (a.iter) a.iter[qp] = 0;
@@ -377,8 +369,9 @@ __device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigne
     acc.img = img;
     acc.so = so;
     acc.N = N;
-    unconstr_residuals_body(a, acc, qp, tid);
+    unconstr_residuals_body<ResLds, 12>(a, acc, qp, tid);
   }
+  tstamp(18);
 }
 
 template <bool RES>

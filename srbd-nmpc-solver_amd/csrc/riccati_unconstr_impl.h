@@ -464,10 +464,11 @@ struct ResLds : LdsSrc {
 // The residual pass of one QP by the whole workgroup (every thread calls it: it ends with a
 // workgroup reduction).  Threads >= kResStages * 12 only take part in the reduction, so a
 // 512-thread workgroup sums the same partial results in the same order as a 256-thread one.
-template <class Acc>
-// (t: the thread's index in the workgroup, passed in so a caller can make it opaque)
+// (t: the thread's index in the workgroup, passed in so a caller can make it opaque; DIM > 0:
+// nx = nu = DIM known at compile time, the same sums in the same order, unrolled)
+template <class Acc, int DIM = 0>
 __device__ __forceinline__ void unconstr_residuals_body(const ProblemArgsT<real>& a, const Acc& acc, int qp, int t) {
-  const int N = a.N, nx = a.nx, nu = a.nu;
+  const int N = a.N, nx = DIM ? DIM : a.nx, nu = DIM ? DIM : a.nu;
   if (a.stat) {  // the QP's stat table is cleared here (no separate memset), row 0 filled below
     real* tab = a.stat + (size_t)qp * a.stat_rows * kStatCols;
     for (int i = t; i < a.stat_rows * kStatCols; i += blockDim.x) tab[i] = real(0);
