@@ -157,9 +157,9 @@ bool unconstr_reads_once(const ProblemArgsT<T>& a);
 
 // The one-QP host call's resident server (riccati_latency_impl.h): the mailbox lives in
 // mapped, coherent host memory; the host writes seq / quit, the kernel done / exited.
-struct LatMailbox {
+struct alignas(8) LatMailbox {
   int seq;     // host: number of the request posted last
-  int quit;    // host: leave now
+  int quit;    // host: leave now (seq and quit: one 8-byte word the server polls)
   int done;    // device: number of the request finished last
   int exited;  // device: epoch of the server launch that has left
 };

@@ -395,15 +395,40 @@ __global__ void __launch_bounds__(kLatThreads, 1)
   long long t0 = wall_clock64();
   for (;;) {
     if (threadIdx.x == 0) {
+      // seq and quit in one 8-byte read of the mailbox, four reads in flight (one issued
+      // every ~0.2 us, each checked a PCIe round trip later): a post is seen about one round
+      // trip after it lands
+      auto poll = [&]() {
+        return __hip_atomic_load(reinterpret_cast<unsigned long long*>(mb), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+      };
       int r = -1;
-      for (;;) {
-        const int sq = __hip_atomic_load(&mb->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (sq != last_done) {
-          r = sq;
-          break;
+      auto seen = [&](unsigned long long v) {  // true: leave the poll (r = the request, or -1)
+        if ((int)(unsigned)v != last_done) {
+          r = (int)(unsigned)v;
+          return true;
         }
-        if (__hip_atomic_load(&mb->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
-        if (wall_clock64() - t0 > idle_ticks) break;
+        return (v >> 32) != 0 || wall_clock64() - t0 > idle_ticks;
+      };
+      unsigned long long p0 = poll();
+      __builtin_amdgcn_s_sleep(8);
+      unsigned long long p1 = poll();
+      __builtin_amdgcn_s_sleep(8);
+      unsigned long long p2 = poll();
+      __builtin_amdgcn_s_sleep(8);
+      unsigned long long p3 = poll();
+      for (;;) {
+        if (seen(p0)) break;
+        p0 = poll();
+        __builtin_amdgcn_s_sleep(8);
+        if (seen(p1)) break;
+        p1 = poll();
+        __builtin_amdgcn_s_sleep(8);
+        if (seen(p2)) break;
+        p2 = poll();
+        __builtin_amdgcn_s_sleep(8);
+        if (seen(p3)) break;
+        p3 = poll();
         __builtin_amdgcn_s_sleep(8);
       }
       // the request's inputs: drop any cached copy of the mapped staging buffer
