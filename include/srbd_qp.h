@@ -263,7 +263,13 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* setti
 /* Host-buffer batch solve: copies to device, solves, copies back, waits.
  * Small unconstrained batches (<= 256 QPs, nx = nu = 12, N <= 26) are zero copy:
  * the kernel reads the handle's pinned staging buffer and writes the outputs
- * into it.                                                                  */
+ * into it.  A single such QP with the classical Riccati (ric_alg 0, N <= 20:
+ * the reference's call pattern) goes to the handle's resident server: a
+ * one-workgroup kernel on its own stream that polls a mailbox in mapped host
+ * memory, so a call costs no launch; it leaves its CU after 5 ms without a
+ * request (or at srbd_qp_destroy / process exit) and the next call relaunches
+ * it.  While it is up it holds one CU, and a device-wide synchronize waits
+ * for it to leave.  SRBD_LAT_SERVER=0 (environment) launches per call.   */
 int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
                            const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol);
 
