@@ -238,8 +238,9 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srb
 namespace {
 // wall-clock idle time after which a server leaves its CU (the next call relaunches it)
 constexpr int kServerIdleMs = 5;
-// a request not answered in this long is a device failure
-constexpr auto kServerTimeout = std::chrono::seconds(2);
+// a request not answered in this long is a device failure (generous: a server launch can
+// queue behind long kernels of other streams before it reaches a CU)
+constexpr auto kServerTimeout = std::chrono::seconds(30);
 std::mutex g_srv_mu;
 std::vector<srbd_qp_handle> g_srv_live;  // handles whose server may be running
 // at exit: ask every live server to leave and give it a moment to drain (no HIP calls: the
