@@ -297,39 +297,58 @@ __device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigne
     }
   }
 
-  // ---------------- forward sweep: x_k+1 = Acl x_k + bcl (wave 0, row-owned) ----------------
+  // ---------------- forward sweep: x_k+1 = Acl x_k + bcl (wave 0, matrix cores) ----------------
+  // x rides in column 0 of an MFMA tile: the product's C/D registers are the next product's B
+  // operand (lane (g, c) register kb = D[4 kb + g][c]), so the chain is three MFMAs per stage.
+  // Columns 1.. of x, bcl and rows 12.. of Acl are zero, so D keeps them zero.
   if (wave == 0) {
-    const int row = cv ? c : 11;
-    double xv = cv ? a.x0[(size_t)qp * 12 + c] : 0.0;
     double* xo = a.x + (size_t)qp * (N + 1) * 12;
-    double Ar[12], bv;
-    auto load_row = [&](int k) {
-      const double* r = acl + k * kLatAcl + row * 13;
-      sfor<0, 12>([&](auto j) { Ar[decltype(j)::value] = r[decltype(j)::value]; });
-      bv = r[12];
+    lat_d4 X;
+    sfor<0, 4>([&](auto rr) {
+      constexpr int R = decltype(rr)::value;
+      const int row = g + 4 * R < 12 ? g + 4 * R : 11;
+      const double v = a.x0[(size_t)qp * 12 + row];
+      X[R] = (c == 0 && g + 4 * R < 12) ? v : 0.0;
+    });
+    double Ao[3], An[3];
+    lat_d4 Ct, Cn;
+    // stage k's A operand (lane (g, c), k-block kb: Acl[c][4 kb + g]) and C (bcl in column 0)
+    auto load_ops = [&](int k, double (&A3)[3], lat_d4& C4) {
+      const double* r = acl + k * kLatAcl + cc * 13;
+      sfor<0, 3>([&](auto kb) {
+        const double v = r[4 * decltype(kb)::value + g];
+        A3[decltype(kb)::value] = cv ? v : 0.0;
+      });
+      const double* bc = acl + k * kLatAcl + 12;
+      sfor<0, 4>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        const int row = g + 4 * R < 12 ? g + 4 * R : 11;
+        const double v = bc[row * 13];
+        C4[R] = (c == 0 && g + 4 * R < 12) ? v : 0.0;
+      });
     };
-    load_row(0);
+    load_ops(0, Ao, Ct);
 #pragma unroll 1
     for (int k = 0; k < N; ++k) {
-      if (l < 12) {
-        so[k * 12 + l] = xv;
-        xo[(size_t)k * 12 + l] = xv;
-      }
-      double An[12], bn = 0.0;
-      if (k + 1 < N) {
-        const double* r = acl + (k + 1) * kLatAcl + row * 13;
-        sfor<0, 12>([&](auto j) { An[decltype(j)::value] = r[decltype(j)::value]; });
-        bn = r[12];
-      }
-      const double xn = dot_bcast(Ar, xv, bv);
-      xv = cv ? xn : 0.0;
-      sfor<0, 12>([&](auto j) { Ar[decltype(j)::value] = An[decltype(j)::value]; });
-      bv = bn;
+      if (c == 0)
+        sfor<0, 3>([&](auto rr) {
+          constexpr int R = decltype(rr)::value;
+          so[k * 12 + g + 4 * R] = X[R];
+          xo[(size_t)k * 12 + g + 4 * R] = X[R];
+        });
+      if (k + 1 < N) load_ops(k + 1, An, Cn);
+      lat_d4 D = Ct;
+      sfor<0, 3>([&](auto kb) { D = lat_mfma(Ao[decltype(kb)::value], X[decltype(kb)::value], D); });
+      X = D;
+      sfor<0, 3>([&](auto kb) { Ao[decltype(kb)::value] = An[decltype(kb)::value]; });
+      Ct = Cn;
     }
-    if (l < 12) {
-      so[N * 12 + l] = xv;
-      xo[(size_t)N * 12 + l] = xv;
-    }
+    if (c == 0)
+      sfor<0, 3>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        so[N * 12 + g + 4 * R] = X[R];
+        xo[(size_t)N * 12 + g + 4 * R] = X[R];
+      });
   }
   __syncthreads();
   tstamp(13);
