@@ -871,8 +871,14 @@ def roofline(constraints, achieved_gbs, traffic, kernel_ms, bytes_qp, flops_qp, 
     the 12 x 12 blocks run on the FP vector pipe)."""
     if constraints == "none":
         prof, prof_ns = pmc_profile("unconstr_n20" if batch == 65536 else "", batch)
+        ceil = unconstr_ceiling(bytes_qp, batch)
         return {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                # what bounds frac for this algorithm (DESIGN 4.2): the two-sweep Riccati must
+                # move the algorithmic bytes + its stage records (written, read back) + the A, B, b
+                # the forward sweep reads again; at the guide's achievable rate that caps frac
+                "ceiling": ceil["ceiling"], "frac_of_ceiling": (achieved_gbs / HBM_PEAK_GBS) / ceil["ceiling"],
+                "ceiling_derivation": ceil,
                 "traffic_profile": prof, "profile_kernel_avg_ms": None if prof_ns is None else prof_ns * 1e-6,
                 # template argument = square-root Riccati (ric_alg; NMPC_solver.cpp:81 sets 0)
                 "kernel": "riccati_unconstr_kernel<%s>" % ("true" if NMPC_SETTINGS["ric_alg"] else "false"),
@@ -887,6 +893,24 @@ def roofline(constraints, achieved_gbs, traffic, kernel_ms, bytes_qp, flops_qp, 
             "kernel": "ipm_phase_kernel<*> (init, RB+F1, B2+F2, out; whole solve)",
             "kernel_avg_ms": kernel_ms, "alg_bytes_per_qp_iter": bytes_qp, "mean_iters": it,
             "fp_vector_frac": tf / peak}
+
+
+HBM_ACHIEVABLE_GBS = 6300.0  # MI355X_MICROARCH.md: "8 TB/s peak (spec); ~6.3 TB/s achievable"
+
+
+def unconstr_ceiling(bytes_qp, batch, N=20, nx=12, nu=12):
+    """The roofline fraction the two-sweep Riccati can reach.  Per QP it moves
+    the algorithmic bytes (inputs once, x / u / pi once) plus, per stage, its record
+    ([K | k], P packed, p: csrc/kernels.h kWsStage = 246 doubles) written by the backward
+    sweep and read back by the forward sweep, plus the A, B, b the forward sweep reads again
+    (x+ = A x + B u + b).  At the achievable HBM rate the fraction of the 8 TB/s peak that
+    counts as algorithmic is then bytes_qp / min_traffic x achievable / peak."""
+    rec = N * 246 * 8 * 2
+    fwd = N * (nx * nx + nx * nu + nx) * 8
+    min_traffic = bytes_qp + rec + fwd
+    return {"alg_bytes_per_qp": bytes_qp, "record_round_trip_per_qp": rec, "forward_reread_per_qp": fwd,
+            "min_traffic_per_qp": min_traffic, "achievable_gbs": HBM_ACHIEVABLE_GBS,
+            "ceiling": bytes_qp / min_traffic * HBM_ACHIEVABLE_GBS / HBM_PEAK_GBS}
 
 
 def settings_dict(s):

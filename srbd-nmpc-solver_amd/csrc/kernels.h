@@ -162,14 +162,18 @@ struct alignas(8) LatMailbox {
   int quit;    // host: leave now (seq and quit: one 8-byte word the server polls)
   int done;    // device: number of the request finished last
   int exited;  // device: epoch of the server launch that has left
+  int arm;     // host, per request: write the early factors and set factors_ready (the
+               // launch's fixed flags pointer); written before seq
+  int pad;
 };
 // true when launch_riccati_unconstr(a) would be one latency-kernel workgroup reading its QP
 // once (batch 1, classical Riccati, N <= 20): the server can take the call instead
 bool latency_server_ok(const ProblemArgsT<double>& a);
-// the server on `stream` (dedicated: it stays until quit or idle_ticks of wall clock with no
-// request); requests after last_done are served
+// the server on `stream` (dedicated: it stays until quit, idle_ticks of wall clock with no
+// request, or the first answer after life_ticks since its launch); the first mailbox seq that
+// differs from last_done is served
 hipError_t launch_latency_server(const ProblemArgsT<double>& a, LatMailbox* mb, int epoch, int last_done,
-                                 long long idle_ticks, hipStream_t stream);
+                                 long long idle_ticks, long long life_ticks, hipStream_t stream);
 
 // nx < 12 or nu < 12: embed the problem in 12 x 12 stages (pad.hip).  pad_elems
 // is the pad buffer size (elements of T); pad_problem fills it from `a` and

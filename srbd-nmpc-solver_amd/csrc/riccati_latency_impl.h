@@ -58,8 +58,11 @@ size_t lat_lds_bytes(int N) { return (size_t)(lat_cnt_off(N) + 2) * sizeof(doubl
 // 100.2 / 99.9 us; streaming the stages into LDS during the sweep measured slower: DESIGN.md 9.1)
 
 // One QP (blockIdx.x) of `a` by the whole workgroup, LDS at lds_raw (lat_lds_bytes(N)).
+// early_req: the request asks for the early factors (the server's per-request mailbox word;
+// a launched kernel passes true and arms them by a.factors_ready alone)
 template <bool RES>
-__device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigned char* lds_raw) {
+__device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigned char* lds_raw,
+                                          bool early_req = true) {
   double* const img = reinterpret_cast<double*>(lds_raw);
   const int N = a.N;
   double* const acl = img + lat_acl_off(N);
@@ -80,7 +83,7 @@ __device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigne
   // Early factors (a.factors_ready): the Riccati getters' outputs are written while wave 0 runs
   // the forward sweep (below), then the QP's host flag is set -- the caller unpacks P and K
   // under the kernel's tail (the forward sweep, u, pi, the residual pass).
-  const bool early = a.factors_ready != nullptr;
+  const bool early = a.factors_ready != nullptr && early_req;
   const int egrp = (tid >> 4) - 4;  // 16-lane group among waves 1.. (0 = wave 1's first)
   int* const ecnt = reinterpret_cast<int*>(img + lat_cnt_off(N));
   if (tid == 0) *ecnt = 0;  // (the copy's barrier orders it before any arrival)
@@ -403,15 +406,18 @@ __global__ void __launch_bounds__(kLatThreads, 1) riccati_latency_kernel(Problem
 // reference's call pattern): one workgroup stays on its CU and polls the mailbox in mapped
 // host memory, so a call costs no launch, no dispatch and no completion signal -- the host
 // posts a request number, the kernel solves the QP from the (fixed) staging buffer `a` points
-// into and writes the number back.  It leaves on `quit`, or after idle_ticks (wall clock) with
-// no request, recording its epoch in `exited`; the host relaunches it then.
+// into and writes the number back.  It leaves on `quit`, after idle_ticks (wall clock) with
+// no request, or after the first answer once life_ticks have passed since its launch (a
+// bound on how long anything queued behind it on a shared hardware queue can wait), recording
+// its epoch in `exited`; the host relaunches it then.
 template <bool RES>
 __global__ void __launch_bounds__(kLatThreads, 1)
     riccati_latency_server_kernel(ProblemArgsT<double> a, LatMailbox* mb, int epoch, int last_done,
-                                  long long idle_ticks) {
+                                  long long idle_ticks, long long life_ticks) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   int* const req = reinterpret_cast<int*>(reinterpret_cast<double*>(lds_raw) + lat_cnt_off(a.N)) + 1;
   long long t0 = wall_clock64();
+  const long long t_launch = t0;
   for (;;) {
     if (threadIdx.x == 0) {
       // seq and quit in one 8-byte read of the mailbox, four reads in flight (one issued
@@ -429,7 +435,10 @@ __global__ void __launch_bounds__(kLatThreads, 1)
         }
         return (v >> 32) != 0 || wall_clock64() - t0 > idle_ticks;
       };
-      unsigned long long p0 = poll();
+      // past its lifetime (checked after an answer, by thread 0 alone: the decision reaches
+      // every wave through *req) the server leaves instead of polling
+      const bool expired = t0 != t_launch && t0 - t_launch > life_ticks;
+      unsigned long long p0 = expired ? (1ull << 32) | (unsigned)last_done : poll();
       __builtin_amdgcn_s_sleep(8);
       unsigned long long p1 = poll();
       __builtin_amdgcn_s_sleep(8);
@@ -453,11 +462,14 @@ __global__ void __launch_bounds__(kLatThreads, 1)
       // the request's inputs: drop any cached copy of the mapped staging buffer
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       *req = r;
+      // per-request early-factor switch (the flags pointer is fixed for the server's life, so
+      // alternating callback / plain calls do not relaunch it)
+      req[1] = r < 0 ? 0 : __hip_atomic_load(&mb->arm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
     const int r = *req;
     if (r < 0) break;
-    lat_solve<RES>(a, lds_raw);
+    lat_solve<RES>(a, lds_raw, req[1] != 0);
     // every wave's outputs in the cache, then one write-back to host memory with the answer
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

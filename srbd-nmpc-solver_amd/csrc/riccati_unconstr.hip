@@ -78,8 +78,8 @@ bool unconstr_reads_once<float>(const ProblemArgsT<float>& a) {
 }
 bool latency_server_ok(const ProblemArgsT<double>& a) { return ric_f64::server_ok(a); }
 hipError_t launch_latency_server(const ProblemArgsT<double>& a, LatMailbox* mb, int epoch, int last_done,
-                                 long long idle_ticks, hipStream_t stream) {
-  return ric_f64::launch_server(a, mb, epoch, last_done, idle_ticks, stream);
+                                 long long idle_ticks, long long life_ticks, hipStream_t stream) {
+  return ric_f64::launch_server(a, mb, epoch, last_done, idle_ticks, life_ticks, stream);
 }
 
 }  // namespace srbd

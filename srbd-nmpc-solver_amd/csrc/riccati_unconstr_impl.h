@@ -806,14 +806,14 @@ bool server_ok(const ProblemArgsT<real>& a) {
   return a.batch == 1 && !a.ric_alg && lat_eligible(a) && reads_once(a);
 }
 hipError_t launch_server(const ProblemArgsT<real>& a, LatMailbox* mb, int epoch, int last_done,
-                         long long idle_ticks, hipStream_t stream) {
+                         long long idle_ticks, long long life_ticks, hipStream_t stream) {
   if (!server_ok(a)) return hipErrorInvalidValue;
   if (fused_residuals(a))
     hipLaunchKernelGGL(riccati_latency_server_kernel<true>, dim3(1), dim3(kLatThreads), lat_lds_bytes(a.N), stream,
-                       a, mb, epoch, last_done, idle_ticks);
+                       a, mb, epoch, last_done, idle_ticks, life_ticks);
   else
     hipLaunchKernelGGL(riccati_latency_server_kernel<false>, dim3(1), dim3(kLatThreads), lat_lds_bytes(a.N), stream,
-                       a, mb, epoch, last_done, idle_ticks);
+                       a, mb, epoch, last_done, idle_ticks, life_ticks);
   return hipGetLastError();
 }
 #endif

@@ -238,6 +238,22 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device, srb
 namespace {
 // wall-clock idle time after which a server leaves its CU (the next call relaunches it)
 constexpr int kServerIdleMs = 5;
+// and leaves after its first answer once this long has passed since its launch: whatever
+// shares its hardware queue (other high-priority streams) waits at most about this long
+constexpr int kServerLifeMs = 20;
+// SRBD_LAT_SERVER_IDLE_MS overrides it (0: the server leaves as soon as it finds no request,
+// so a call's post usually lands after the server left -- the test of the relaunch path)
+int server_idle_ms() {
+  const char* v = std::getenv("SRBD_LAT_SERVER_IDLE_MS");  // (read per launch: tests set it)
+  return v && *v ? std::max(0, std::atoi(v)) : kServerIdleMs;
+}
+// test hook: SRBD_LAT_SERVER_POST_DELAY_US holds the post back this long after the host found
+// the server live, so that with a zero idle time the server leaves in between -- every call
+// then takes the wait loop's relaunch-after-post branch
+int server_post_delay_us() {
+  const char* v = std::getenv("SRBD_LAT_SERVER_POST_DELAY_US");
+  return v && *v ? std::max(0, std::atoi(v)) : 0;
+}
 // a request not answered in this long is a device failure (generous: a server launch can
 // queue behind long kernels of other streams before it reaches a CU)
 constexpr auto kServerTimeout = std::chrono::seconds(30);
@@ -263,17 +279,24 @@ bool server_enabled() {
 
 // on the handle's device
 static void server_stop(srbd_qp_handle h) {
-  if (!h->srv_live) return;
-  reinterpret_cast<volatile srbd::LatMailbox*>(h->srv_mb)->quit = 1;
-  hipStreamSynchronize(h->srv_stream);
-  reinterpret_cast<volatile srbd::LatMailbox*>(h->srv_mb)->quit = 0;
-  h->srv_live = false;
+  if (h->srv_live) {
+    reinterpret_cast<volatile srbd::LatMailbox*>(h->srv_mb)->quit = 1;
+    hipStreamSynchronize(h->srv_stream);
+    reinterpret_cast<volatile srbd::LatMailbox*>(h->srv_mb)->quit = 0;
+    h->srv_live = false;
+  }
+  // always off the exit hook's list: a handle whose relaunch failed (srv_live false) may
+  // still be listed, and srbd_qp_destroy frees it and its mailbox right after this
   std::lock_guard<std::mutex> lk(g_srv_mu);
   g_srv_live.erase(std::remove(g_srv_live.begin(), g_srv_live.end(), h), g_srv_live.end());
 }
 
-// (re)launch the server with `a` on the handle's device; requests after h->srv_seq are served
-static hipError_t server_launch(srbd_qp_handle h, const srbd::ProblemArgsT<double>& a) {
+// (re)launch the server with `a` on the handle's device.  `last_done` is the last request
+// number that was answered (or abandoned): the server serves the first mailbox seq that
+// differs from it.  Before a post that is h->srv_seq; after the post (the wait loop's
+// relaunch of a server that idled out just before it) it is h->srv_seq - 1, or the pending
+// request would count as done and never be served.
+static hipError_t server_launch(srbd_qp_handle h, const srbd::ProblemArgsT<double>& a, int last_done) {
   hipError_t e = hipSuccess;
   if (!h->srv_mb) {
     e = hipHostMalloc(reinterpret_cast<void**>(&h->srv_mb), sizeof(srbd::LatMailbox),
@@ -283,7 +306,15 @@ static hipError_t server_launch(srbd_qp_handle h, const srbd::ProblemArgsT<doubl
     void* dev = nullptr;
     e = hipHostGetDevicePointer(&dev, h->srv_mb, 0);
     if (e == hipSuccess) h->srv_mb_dev = reinterpret_cast<srbd::LatMailbox*>(dev);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->srv_stream, hipStreamNonBlocking);
+    // The server's stream at the greatest priority: HIP maps a process's streams onto a few
+    // hardware queues (GPU_MAX_HW_QUEUES, 4 here) per priority, each processing its packets in
+    // order, so a kernel of another stream that shares the server's queue would wait until the
+    // server leaves.  High-priority streams come from their own queue pool, which only other
+    // high-priority streams share (scripts/dev/server_queue_probe.hip: with a plain stream 2 of
+    // 8 other streams were held back by a resident kernel, with a high-priority one none).
+    int prio_lo = 0, prio_hi = 0;
+    if (e == hipSuccess && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&h->srv_stream, hipStreamNonBlocking, prio_hi);
     if (e != hipSuccess) return e;
     static std::once_flag once;
     std::call_once(once, [] { std::atexit(server_atexit); });
@@ -292,8 +323,8 @@ static hipError_t server_launch(srbd_qp_handle h, const srbd::ProblemArgsT<doubl
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) != hipSuccess || khz <= 0)
     khz = 100000;
   std::memcpy(&h->srv_args, &a, sizeof a);
-  e = srbd::launch_latency_server(a, h->srv_mb_dev, ++h->srv_epoch, h->srv_seq, (long long)khz * kServerIdleMs,
-                                  h->srv_stream);
+  e = srbd::launch_latency_server(a, h->srv_mb_dev, ++h->srv_epoch, last_done, (long long)khz * server_idle_ms(),
+                                  (long long)khz * kServerLifeMs, h->srv_stream);
   h->srv_live = e == hipSuccess;
   if (h->srv_live) {
     std::lock_guard<std::mutex> lk(g_srv_mu);
@@ -1068,15 +1099,28 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
       srbd::ProblemArgsT<double> ar = a;
       ar.fuse_res = st->compute_residuals;  // (not embedded: nx = nu = 12)
       served = srbd::latency_server_ok(ar);
+      // the early-factor flags: a fixed pointer for the server's life, switched per request
+      // through the mailbox (LatMailbox::arm), so callback and plain calls share one server
+      if (served && !h->fac_flags) {
+        if (hipHostMalloc(reinterpret_cast<void**>(&h->fac_flags), sizeof(int) * kFacFlagsMax,
+                          hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+          h->fac_flags = nullptr;
+      }
+      void* fdev = nullptr;
+      if (served && (!h->fac_flags || hipHostGetDevicePointer(&fdev, h->fac_flags, 0) != hipSuccess)) fdev = nullptr;
+      ar.factors_ready = reinterpret_cast<int*>(fdev);
+      if (served && arm && !fdev) served = false;  // (cannot happen: arm allocated the flags)
       if (served) {
         // the handle's workspace: earlier work queued on its stream finishes first
         if (hipStreamQuery(h->stream) != hipSuccess) e = hipStreamSynchronize(h->stream);
         if (e == hipSuccess && h->srv_live && std::memcmp(&ar, &h->srv_args, sizeof ar) != 0) server_stop(h);
         if (e == hipSuccess &&
             (!h->srv_live || reinterpret_cast<volatile srbd::LatMailbox*>(h->srv_mb)->exited == h->srv_epoch))
-          e = server_launch(h, ar);
+          e = server_launch(h, ar, h->srv_seq);  // (before the post: nothing pending)
         volatile srbd::LatMailbox* mb = h->srv_mb;
         if (e == hipSuccess) {
+          if (const int us = server_post_delay_us()) std::this_thread::sleep_for(std::chrono::microseconds(us));
+          mb->arm = arm ? 1 : 0;
           std::atomic_thread_fence(std::memory_order_release);  // the staged QP before the post
           mb->seq = ++h->srv_seq;
         }
@@ -1122,7 +1166,13 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
       for (unsigned n = 1; e == hipSuccess && mb->done != h->srv_seq; ++n) {
         if (factors_check()) continue;
         if (mb->exited == h->srv_epoch) {
-          e = server_launch(h, h->srv_args);
+          // the server left: it writes `done` before `exited`, so read `done` again -- it may
+          // have answered this request before leaving (then a relaunch would solve it twice,
+          // the second time under the next call's packing)
+          std::atomic_thread_fence(std::memory_order_acquire);
+          if (mb->done == h->srv_seq) break;
+          // it left before seeing the post: the request is still pending
+          e = server_launch(h, h->srv_args, h->srv_seq - 1);
           continue;
         }
         if ((n & 1023) == 0) {

@@ -188,8 +188,8 @@ def test_general_constraints_vs_oracle(pkg, oracle, dims, ric_alg):
         assert helpers.is_approx(out["pi"][i, 1:], ref["pi"][i, 1:], 1e-6), ("pi", i)
 
 
-@pytest.mark.parametrize("ric_alg,mode,min_ok,path", [(0, "Speed", 63, "batched"), (0, "Speed", 63, "latency"),
-                                                      (1, "Speed", 44, "auto"), (0, "Balance", 64, "auto"),
+@pytest.mark.parametrize("ric_alg,mode,min_ok,path", [(0, "Speed", 64, "batched"), (0, "Speed", 64, "latency"),
+                                                      (1, "Speed", 48, "auto"), (0, "Balance", 64, "auto"),
                                                       (1, "Balance", 64, "auto")])
 def test_degenerate_endgame_family(pkg, oracle, ric_alg, mode, min_ok, path, monkeypatch):
     """The near-degenerate QP above (#12 of (12, 4, 14) seed 200) as 64 copies with Q, R, S,
@@ -198,8 +198,9 @@ def test_degenerate_endgame_family(pkg, oracle, ric_alg, mode, min_ok, path, mon
     (~eps x the 1e13 barrier Hessians) rising past tol_stat.  The oracle, in
     HPIPM's own forms, converges on 64 (ric_alg 0) and 48 (ric_alg 1: the carried joint stage
     factor, s-form predictor, p-form corrector -- ws->valid_ric_p, hpipm_d_ocp_qp_ipm.h:134); the
-    GPU on 64 and 48.  The count of the square-root variant is held to the oracle's within 8
-    (equivalent summation orders move it by about that much).  With HPIPM's refinement of the
+    GPU on 64 and 48.  Each count is held at its measured value (min_ok) and to the oracle's
+    within 4 (equivalent summation orders move the square-root count between 34 and 63,
+    DESIGN.md 4.4, so the window is not a parity measure beyond that).  With HPIPM's refinement of the
     corrector (Balance: 2 corrections at most) both converge on 64 / 64.  The x, u
     of every copy are held to the oracle's at 1e-6 (converged) or 1e-3 (min step).  Speed with
     ric_alg 0 runs on both IPM paths: the batched kernels (SRBD_IPM_LATENCY_MAX=0) and the
@@ -229,7 +230,7 @@ def test_degenerate_endgame_family(pkg, oracle, ric_alg, mode, min_ok, path, mon
     ref = oracle.solve(fam, st, x0=xb)
     n_ref, n_out = (ref["status"] == 0).sum(), (out["status"] == 0).sum()
     assert n_ref >= min_ok, ref["status"]
-    assert n_out >= min_ok and abs(int(n_out) - int(n_ref)) <= 8, (n_out, n_ref, out["status"])
+    assert n_out >= min_ok and abs(int(n_out) - int(n_ref)) <= 4, (n_out, n_ref, out["status"])
     assert set(np.unique(out["status"])) <= {0, 2}, out["status"]
     for i in range(M):
         if ref["status"][i] != 0:

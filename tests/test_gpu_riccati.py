@@ -527,3 +527,144 @@ def test_host_solve_resident_server(pkg, monkeypatch):
         assert ra["status"][0] == 0
     # distinct QPs gave distinct answers (no stale staging data)
     assert not np.array_equal(a[0]["u"], a[1]["u"])
+
+
+def _one_qp_calls(pkg, seeds, cbs):
+    """One-QP host calls through one handle (the reference's call pattern); returns the staged
+    outputs of every call and each call's wall time."""
+    import ctypes as C
+    import time
+    capi = pkg.capi
+    keys_in = ("A", "B", "b", "Q", "S", "R", "q", "r", "x0")
+    keys_out = ("x", "u", "pi", "P", "p", "K", "k", "status", "iter", "res", "obj")
+    sizes = dict(x=21 * 12, u=20 * 12, pi=21 * 12, P=21 * 144, p=21 * 12, K=20 * 144, k=20 * 12, res=4, obj=1)
+    h = capi.Handle(20, 12, 12, capacity=1)
+    outs, times = [], []
+    try:
+        s = capi.settings_struct(dict(ric_alg=0))
+        for seed, cb in zip(seeds, cbs):
+            qp, x0 = pkg.srbd_model.generate_batch(1, N=20, seed=seed, constraints="none")
+            p = qp.packed()
+            p["x0"] = np.ascontiguousarray(x0)
+            d = capi.Data(**{k: 16 for k in keys_in})
+            o = capi.Solution(**{k: 16 for k in keys_out})
+            h.host_staging(1, s, d, o)
+            for k in keys_in:
+                src = np.ascontiguousarray(p[k], dtype=np.float64)
+                C.memmove(getattr(d, k), src.ctypes.data, src.nbytes)
+            calls = []
+            t0 = time.perf_counter()
+            h.solve_host(1, s, d, o, on_factors=(lambda: calls.append(1)) if cb else None)
+            times.append(time.perf_counter() - t0)
+            assert len(calls) == (1 if cb else 0)
+            r = {k: np.ctypeslib.as_array((C.c_double * n).from_address(getattr(o, k))).copy()
+                 for k, n in sizes.items()}
+            r["status"] = np.ctypeslib.as_array((C.c_int * 1).from_address(o.status)).copy()
+            outs.append(r)
+    finally:
+        h.close()
+    return outs, times
+
+
+def test_resident_server_relaunch_after_post(pkg, monkeypatch):
+    """The server leaves between the host's liveness check and its post on EVERY call: zero
+    idle time (SRBD_LAT_SERVER_IDLE_MS=0: it leaves at its first empty poll) and the post held
+    back 1 ms after the check (SRBD_LAT_SERVER_POST_DELAY_US).  The wait loop must relaunch it
+    with the pending request still to serve (round 5 relaunched it with last_done = the posted
+    number, so the request was never served and the call failed after 30 s).  60 calls, with
+    and without the early-factor callback (a per-request mailbox word: no relaunch for it),
+    each answered bit-identically to the launched kernel (SRBD_LAT_SERVER=0) and each in
+    under 5 ms."""
+    seeds = list(range(300, 360))
+    cbs = [i % 3 == 1 for i in range(60)]
+    monkeypatch.setenv("SRBD_LAT_SERVER", "1")
+    monkeypatch.setenv("SRBD_LAT_SERVER_IDLE_MS", "0")
+    monkeypatch.setenv("SRBD_LAT_SERVER_POST_DELAY_US", "1000")
+    a, ta = _one_qp_calls(pkg, seeds, cbs)
+    monkeypatch.delenv("SRBD_LAT_SERVER_IDLE_MS")
+    monkeypatch.delenv("SRBD_LAT_SERVER_POST_DELAY_US")
+    monkeypatch.setenv("SRBD_LAT_SERVER", "0")
+    b, _ = _one_qp_calls(pkg, seeds, cbs)
+    for i, (ra, rb) in enumerate(zip(a, b)):
+        for k in ra:
+            assert np.array_equal(ra[k], rb[k]), (i, k)
+        assert ra["status"][0] == 0
+    assert max(ta) < 5e-3, sorted(ta)[-5:]
+
+
+def test_resident_server_leaves_other_streams_running(pkg, monkeypatch):
+    """A busy server (calls back to back on one handle, so it never idles out) must not hold
+    back kernels of other streams: HIP maps streams onto a few hardware queues (4 per process
+    here) that process their packets in order, so a kernel queued behind the resident server
+    on a shared queue would wait until the server leaves.  The server's stream is created so
+    that it does not share a queue with other streams (srbd_qp_capi.hip server_launch); here a
+    small kernel on each of 8 fresh torch streams, and on torch's default stream, finishes
+    within 50 ms while the server keeps serving; so does one on each of 2 high-priority streams,
+    which may share the server's queue but wait at most its 20 ms lifetime."""
+    import threading
+    import time
+    import torch
+    monkeypatch.setenv("SRBD_LAT_SERVER", "1")
+    stop = threading.Event()
+    n_calls = [0]
+    err = []
+
+    def caller():
+        import ctypes as C
+        try:
+            capi = pkg.capi
+            keys_in = ("A", "B", "b", "Q", "S", "R", "q", "r", "x0")
+            qp, x0 = pkg.srbd_model.generate_batch(1, N=20, seed=5, constraints="none")
+            p = qp.packed()
+            p["x0"] = np.ascontiguousarray(x0)
+            h = capi.Handle(20, 12, 12, capacity=1)
+            try:
+                s = capi.settings_struct(dict(ric_alg=0))
+                d = capi.Data(**{k: 16 for k in keys_in})
+                o = capi.Solution(**{k: 16 for k in ("x", "u", "pi", "status")})
+                h.host_staging(1, s, d, o)
+                for k in keys_in:
+                    src = np.ascontiguousarray(p[k], dtype=np.float64)
+                    C.memmove(getattr(d, k), src.ctypes.data, src.nbytes)
+                while not stop.is_set():
+                    h.solve_host(1, s, d, o)
+                    assert C.c_int.from_address(o.status).value == 0
+                    n_calls[0] += 1
+            finally:
+                h.close()
+        except Exception as e:  # pragma: no cover - reported below
+            err.append(e)
+
+    x = torch.zeros(1024, device="cuda")
+    torch.cuda.synchronize()
+    # 8 default-priority streams (they never share the server's queue) and 2 high-priority ones
+    # (they may: the server leaves after its first answer past 20 ms, so they wait < 50 ms)
+    streams = [torch.cuda.Stream() for _ in range(8)] + [torch.cuda.Stream(priority=-1) for _ in range(2)]
+    for s in streams:  # bind each stream to its hardware queue before the server starts
+        with torch.cuda.stream(s):
+            x.add_(1)
+    torch.cuda.synchronize()
+    t = threading.Thread(target=caller)
+    t.start()
+    try:
+        t_wait = time.perf_counter() + 10
+        while n_calls[0] < 20 and not err and time.perf_counter() < t_wait:
+            time.sleep(0.001)
+        assert n_calls[0] >= 20, (n_calls, err)
+        lat = []
+        for s in streams + [torch.cuda.default_stream()]:
+            ev = torch.cuda.Event()
+            t0 = time.perf_counter()
+            with torch.cuda.stream(s):
+                x.add_(1)
+                ev.record(s)
+            while not ev.query() and time.perf_counter() - t0 < 2.0:
+                time.sleep(0.0002)
+            lat.append(time.perf_counter() - t0)
+        calls_during = n_calls[0]
+    finally:
+        stop.set()
+        t.join()
+    assert not err, err
+    assert calls_during >= 20
+    assert max(lat) < 0.05, [round(v * 1e3, 2) for v in lat]
