@@ -4,8 +4,10 @@
 //
 // Same algorithm as the batched IPM (ipm_box_impl.h) and the oracle (oracle/ocp_qp_oracle.c
 // oracle_solve): HPIPM's d_ocp_qp_ipm_solve (hpipm_d_ocp_qp_ipm.h:238) in the classical
-// Riccati form (ric_alg 0, NMPC_solver.cpp:81), Mehrotra predictor-corrector, no iterative
-// refinement (Speed / SpeedAbs: itref_corr_max 0).  Another summation order: results agree
+// Riccati form (ric_alg 0, NMPC_solver.cpp:81), Mehrotra predictor-corrector, and HPIPM's
+// iterative refinement of the step when the mode asks for it (Balance 2 / Robust 4 corrections,
+// itref_corr_max; the reference test's compareResults runs Balance, test/ocp_qp_ipm_solver.cpp:243).
+// Another summation order: results agree
 // with the batched kernels' and the oracle's to rounding, not bit for bit.
 //
 // Why a separate kernel.  In the batched kernels a QP is one 16-lane group that walks its
@@ -53,8 +55,10 @@ constexpr int kSA = 0, kSB = 144, kSb = 288, kSR = 300, kSS = 444, kSQ = 588, kS
 constexpr int kSlot = 756;
 static_assert(kSb - kSA == 2 * 144 && kRR - kRb == kSR - kSb && kRq - kRb == kSq - kSb, "ring = A, B, record blocks");
 
+// [N+1][12] buffers before the general rows: 15 vectors, 4 x 48 barrier blocks
+constexpr int kV12 = 31;
 __host__ __device__ constexpr size_t lds_doubles(int N, int nch) {
-  return (size_t)31 * (N + 1) * 12 + (size_t)nch * (N + 1) * kGenChunk + (size_t)N * 156 + 648 +
+  return (size_t)kV12 * (N + 1) * 12 + (size_t)nch * (N + 1) * kGenChunk + (size_t)N * 156 + 648 +
          (size_t)kGroups * kRedSlots + 3 * kSlot;
 }
 
@@ -89,9 +93,16 @@ struct Lds {
   __device__ double* bx() const { return base + 19 * S; }
   __device__ double* su() const { return base + 23 * S; }
   __device__ double* sx() const { return base + 27 * S; }
+  // iterative refinement (itref_corr_max) takes buffers that are dead between an iteration's
+  // stage pass and the next one: the check's r_u, r_x in gtu, gtx (the corrector's gradients),
+  // r_b and the correction's P_k+1 r_b in the other x / pi buffer (the next stage pass writes
+  // it afresh), the correction's dx in gtu once its recursion no longer needs r_u
+  __device__ int ref_b() const { return cur ? 0 : 13; }   // = xb(cur ^ 1)
+  __device__ int ref_pb() const { return cur ? 2 : 14; }  // = pib(cur ^ 1)
+  static constexpr int kRefDx = 9;                        // gtu
   // general rows, [N+1][nch][kGenChunk]
-  __device__ double* gb(int k, int ch) const { return base + 31 * S + (k * nch + ch) * kGenChunk; }
-  __device__ double* acl() const { return base + 31 * S + (N + 1) * nch * kGenChunk; }  // [N][156]
+  __device__ double* gb(int k, int ch) const { return base + kV12 * S + (k * nch + ch) * kGenChunk; }
+  __device__ double* acl() const { return base + kV12 * S + (N + 1) * nch * kGenChunk; }  // [N][156]
   // factorization hand-over: G/H tile, two Y tiles, two L factors
   __device__ double* scr() const { return acl() + N * 156; }
   __device__ double* red() const { return scr() + 648; }  // [kGroups][kRedSlots]
@@ -716,13 +727,57 @@ __device__ __forceinline__ void corr_terms(const Qp Q, const Lds L, double smu) 
   }
 }
 
+// [P | p] in the tiles' C/D layout (wave 0) -> [Lp | s]: Lp = chol(P) (lower, a non-positive pivot
+// zeroes its column: BLASFEO dpotrf_l, riccati.h sqrt_factor) and s = Lp^-1 p, the border column
+// of the same elimination; through the G/H tile (column-owned Cholesky, then back)
+__device__ __forceinline__ lat_d4 sqrt_tile(const lat_d4& Pt, double* gh, int g, int c) {
+  const bool cv = c < 12, cw = c <= 12;
+  lds_wave_fence();
+  sfor<0, 3>([&](auto rr) {
+    constexpr int R = decltype(rr)::value;
+    if (cw) gh[c * 12 + g + 4 * R] = Pt[R];
+  });
+  lds_wave_fence();
+  double Pc[12], Lc[12], rs;
+  sfor<0, 12>([&](auto i) {
+    const double v = gh[(cw ? c : 12) * 12 + decltype(i)::value];
+    Pc[decltype(i)::value] = cw ? v : 0.0;
+  });
+  lat_chol<true>(Pc, c, 0.0, Lc, rs, [](auto) {});
+  lds_wave_fence();
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    const double ri = bc<I>(rs);
+    // lane c < 12: column c of Lp (zero above the diagonal); lane 12: s
+    const double v = cv ? (I >= c ? Lc[I] : 0.0) : Lc[I] * ri;
+    if (cw && g == 0) gh[c * 12 + I] = v;
+  });
+  lds_wave_fence();
+  lat_d4 o;
+  sfor<0, 4>([&](auto rr) {
+    constexpr int R = decltype(rr)::value;
+    const int row = g + 4 * R < 12 ? g + 4 * R : 11;
+    const double v = gh[(cw ? c : 12) * 12 + row];
+    o[R] = (g + 4 * R < 12 && cw) ? v : 0.0;
+  });
+  lds_wave_fence();
+  return o;
+}
+
 // ---------------------------------------------------------------------------------------------
 // phase: the factorization (backward, serial in k) on matrix cores -- riccati_latency_impl.h's
 // sweep.  Wave 0: stage k's products and Cholesky; wave 1: stage k+1's K, record and closed
 // loop; wave 2: stage k-1's operands (A, B from the QP, R~ S~ Q~ r~ q~ b~ from the record) into
 // the LDS ring, so no global load sits on the chain.  Records per stage: [K | k] rows, P packed,
 // p, L packed + 1 / diag; [Acl | bcl] rows in LDS.
+// SQRT (ric_alg 1, hpipm-cpp's default; riccati.h riccati_step_sqrt): the chain carries the factor
+// Lp of P_k+1 and s = Lp^-1 p_k+1 instead of [P | p], and the same MFMAs form MB = Lp'B,
+// MA = Lp'[A | b~] + [0 | s], G = R~ + MB'MB, [H | g] = [S~ | r~] + MB'MA, [F | f] = [Q~ | q~] +
+// MA'MA (sums of squares: the classical B'PB, B'P[A | b~], A'P[A | b~] in exact arithmetic);
+// P_k = F - Y'Y goes to the record as in the classical form (the sweeps apply it explicitly) and
+// is factorized again for the next stage (sqrt_tile: a second Cholesky on the chain).
 // ---------------------------------------------------------------------------------------------
+template <bool SQRT>
 __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
   const ProblemArgsT<double>& a = Q.a;
   const int N = Q.N;
@@ -763,6 +818,7 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
       if (cv && row >= c) wn[kRP + packed_col(c) + row - c] = Pt[R];
       if (c == 12) wn[kRp + row] = Pt[R];
     });
+    if constexpr (SQRT) Pt = sqrt_tile(Pt, gh, g, c);
   } else if (wave == 2) {
     load_slot(N - 1);
   }
@@ -822,11 +878,15 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
         St[R] = rok && cw ? sv : 0.0;
         Qt[R] = rok && cw ? qv : 0.0;
       });
-      // WB = P B; G = R~ + B'WB (the critical path)
+      // WB = P B; G = R~ + B'WB (the critical path).  SQRT: the A operand Pt is Lp, so WB = Lp'B
+      // = MB and G = R~ + MB'MB.
       lat_d4 WB = {0.0, 0.0, 0.0, 0.0};
       sfor<0, 3>([&](auto kb) { WB = lat_mfma(Pt[decltype(kb)::value], bo[decltype(kb)::value], WB); });
       lat_d4 Gt = Rt;
-      sfor<0, 3>([&](auto kb) { Gt = lat_mfma(bo[decltype(kb)::value], WB[decltype(kb)::value], Gt); });
+      sfor<0, 3>([&](auto kb) {
+        constexpr int KB = decltype(kb)::value;
+        Gt = lat_mfma(SQRT ? WB[KB] : bo[KB], WB[KB], Gt);
+      });
       // W = P [A | b~] + [0 | p]; [H | g] = [S~ | r~] + B'W; [F | f] = [Q~ | q~] + A'W: one per pivot
       lat_d4 Wt;
       sfor<0, 4>([&](auto rr) { Wt[decltype(rr)::value] = c == 12 ? Pt[decltype(rr)::value] : 0.0; });
@@ -837,10 +897,11 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
           Wt = lat_mfma(Pt[K], ao[K], Wt);
         } else if constexpr (K < 9) {
           constexpr int KB = (K - 3) / 2;
+          // (SQRT: W = MA; H = S~ + MB'MA, F = Q~ + MA'MA)
           if constexpr ((K - 3) % 2 == 0) {
-            Ht = lat_mfma(bo[KB], Wt[KB], Ht);
+            Ht = lat_mfma(SQRT ? WB[KB] : bo[KB], Wt[KB], Ht);
           } else {
-            Ft = lat_mfma(ao[KB], Wt[KB], Ft);
+            Ft = lat_mfma(SQRT ? Wt[KB] : ao[KB], Wt[KB], Ft);
           }
         }
       };
@@ -916,6 +977,8 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
         if (cv && row >= c) rk[kRP + packed_col(c) + row - c] = Pt[R];
         if (c == 12) rk[kRp + row] = Pt[R];
       });
+      if constexpr (SQRT)
+        if (k > 0) Pt = sqrt_tile(Pn, gh, g, c);
     } else if (wave == 1) {
       if (k < N - 1) finish_stage(k + 1);
     } else if (wave == 2) {
@@ -929,8 +992,9 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
 // ---------------------------------------------------------------------------------------------
 // phase: forward recursion dx_k+1 = Acl_k dx_k + bcl_k, dx_0 = 0 (wave 0, row-owned)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void forward(const Lds L, int N) {
+__device__ __forceinline__ void forward(const Lds L, int N, int out = 3) {
   if ((threadIdx.x >> 6) != 0) return;
+  double* const dxo = L.v12(out);  // dx (3), or the refinement's correction
   const int c = opq(threadIdx.x & 15);
   const bool cv = c < 12;
   const int row = cv ? c : 11;
@@ -944,7 +1008,7 @@ __device__ __forceinline__ void forward(const Lds L, int N) {
   load_row(0, Ar, bv);
 #pragma unroll 1
   for (int k = 0; k < N; ++k) {
-    if (threadIdx.x < 12) L.dx()[k * 12 + c] = xv;
+    if (threadIdx.x < 12) dxo[k * 12 + c] = xv;
     double An[12], bn = 0.0;
     if (k + 1 < N) {
       load_row(k + 1, An, bn);
@@ -956,7 +1020,7 @@ __device__ __forceinline__ void forward(const Lds L, int N) {
     sfor<0, 12>([&](auto j) { Ar[decltype(j)::value] = An[decltype(j)::value]; });
     bv = bn;
   }
-  if (threadIdx.x < 12) L.dx()[N * 12 + c] = xv;
+  if (threadIdx.x < 12) dxo[N * 12 + c] = xv;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1063,27 +1127,37 @@ __device__ __forceinline__ void step_pass(const Qp Q, const Lds L, double smu, b
 // stage g_k = B_k'(P_k+1 b~_k + p_k+1) + g~u_k, k_k = -(L L')^-1 g_k, bcl_k = b~_k + B_k k_k.
 // (The oracle's p_k = f + K'g with f = A'Pb + g~x, g = B'Pb + g~u, Pb = P b~ + p_k+1.)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void corr_rhs_stages(const Qp Q, const Lds L) {
+// Right-hand side buffers (v12 indices): the corrector's g~u = gtu, g~x = gtx, b~ = rb, P b~ kept
+// in dpi; the refinement's correction: r_u, r_x in gtu, gtx, r_b in kCrb, P r_b in kCpb.
+struct Rhs {
+  int gu, gx, b, pb;
+};
+constexpr Rhs kRhsCorr{9, 10, 8, 5};
+__device__ __forceinline__ void corr_rhs_stages(const Qp Q, const Lds L, Rhs h = kRhsCorr) {
   const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
   const bool el = j < 12;
   const int jj = el ? j : 11;
+  const double* gu = L.v12(h.gu);
+  const double* gx = L.v12(h.gx);
+  const double* bt = L.v12(h.b);
+  double* pbo = L.v12(h.pb);
   for (int k = grp; k <= N; k += kGroups) {
     if (k == N) {
-      if (el) L.pv()[N * 12 + j] = L.gtx()[N * 12 + j];
+      if (el) L.pv()[N * 12 + j] = gx[N * 12 + j];
       continue;
     }
     double M[12];
     load_packed_sym(Q.rec(k + 1) + kRP, jj, M);
-    const double bj = el ? L.rb()[k * 12 + j] : 0.0;
+    const double bj = el ? bt[k * 12 + j] : 0.0;
     double pb = dot_bcast(M, bj, 0.0);
     if (!el) pb = 0.0;
     const double* rk = Q.rec(k);
     sfor<0, 12>([&](auto i) { M[decltype(i)::value] = rk[kRK + decltype(i)::value * 13 + jj]; });
-    double ck = dot_bcast(M, el ? L.gtu()[k * 12 + j] : 0.0, el ? L.gtx()[k * 12 + j] : 0.0);
+    double ck = dot_bcast(M, el ? gu[k * 12 + j] : 0.0, el ? gx[k * 12 + j] : 0.0);
     sfor<0, 12>([&](auto i) { M[decltype(i)::value] = L.acl()[k * 156 + decltype(i)::value * 13 + jj]; });
     ck = dot_bcast(M, pb, ck);
     if (el) {
-      L.dpi()[k * 12 + j] = pb;
+      pbo[k * 12 + j] = pb;
       L.pv()[k * 12 + j] = ck;
     }
   }
@@ -1114,15 +1188,18 @@ __device__ __forceinline__ void corr_rhs_chain(const Lds L, int N) {
     sfor<0, 12>([&](auto i) { M[decltype(i)::value] = Mn[decltype(i)::value]; });
   }
 }
-__device__ __forceinline__ void corr_k_stages(const Qp Q, const Lds L) {
+__device__ __forceinline__ void corr_k_stages(const Qp Q, const Lds L, Rhs h = kRhsCorr) {
   const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
   const bool el = j < 12;
   const int jj = el ? j : 11;
+  const double* gu = L.v12(h.gu);
+  const double* bt = L.v12(h.b);
+  const double* pb = L.v12(h.pb);
   for (int k = grp; k < N; k += kGroups) {
     double M[12];
     load12(Q.B(k) + jj * 12, M);
-    const double w = el ? L.dpi()[k * 12 + j] + L.pv()[(k + 1) * 12 + j] : 0.0;
-    double gk = dot_bcast(M, w, el ? L.gtu()[k * 12 + j] : 0.0);
+    const double w = el ? pb[k * 12 + j] + L.pv()[(k + 1) * 12 + j] : 0.0;
+    double gk = dot_bcast(M, w, el ? gu[k * 12 + j] : 0.0);
     if (!el) gk = 0.0;
     // k = -(L L')^-1 g: L's columns on lanes 0..11, the right-hand side on lane 12
     const double* rk = Q.rec(k);
@@ -1140,12 +1217,193 @@ __device__ __forceinline__ void corr_k_stages(const Qp Q, const Lds L) {
     });
     // bcl_k = b~_k + B_k k_k (row j of B)
     load_strided(Q.B(k) + jj, 12, M);
-    const double bcl = dot_bcast(M, kk, el ? L.rb()[k * 12 + j] : 0.0);
+    const double bcl = dot_bcast(M, kk, el ? bt[k * 12 + j] : 0.0);
     if (el) {
       L.kv()[k * 12 + j] = kk;
       L.acl()[k * 156 + j * 13 + 12] = bcl;
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// iterative refinement of the step (HPIPM itref_corr_max: Balance 2, Robust 4; the batched
+// kernels' kPhIR / kPhIS / kPhF3, oracle lin_res).  The check: the linear residual of the Newton
+// system at the step (du, dx, dpi and the barrier steps) in its full form -- QP Hessian,
+// multiplier steps, dynamics; the dt / dlam rows hold by construction --
+//   r_u = res_g,u + R du + S dx + B'dpi_k+1 + (dlam_u - dlam_l)_u + D'(dlam_u - dlam_l)_rows
+//   r_x = res_g,x + S'du + Q dx + A'dpi_k+1 - dpi_k + (..)_x + C'(..)_rows        (k >= 1)
+//   r_b = res_b + A dx + B du - dx_k+1                                          (k < N)
+// into gtu, gtx (dead after the corrector) and the other x buffer; its infinity norms to red
+// slots 0, 1.
+// ---------------------------------------------------------------------------------------------
+template <bool HAS_C>
+__device__ __forceinline__ void lin_res_pass(const Qp Q, const Lds L) {
+  const ProblemArgsT<double>& a = Q.a;
+  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
+  const bool el = j < 12;
+  const int jj = el ? j : 11;
+  double ng = 0.0, nb = 0.0;
+  for (int k = grp; k <= N; k += kGroups) {
+    const double duj = (el && k < N) ? L.du()[k * 12 + j] : 0.0;
+    const double dxj = (el && k > 0) ? L.dx()[k * 12 + j] : 0.0;
+    const double dpnj = (el && k < N) ? L.dpi()[(k + 1) * 12 + j] : 0.0;
+    double ru = el ? L.rgu()[k * 12 + j] : 0.0;
+    double rx = el ? L.rgx()[k * 12 + j] - L.dpi()[k * 12 + j] : 0.0;
+    if (el && k < N) {
+      const Side s = side_u(Q, k, j);
+      const BarStep d = ld_step(L.su() + k * 48, j);
+      ru += s.mu * d.dlu - s.ml * d.dll;
+    }
+    if (el && k > 0) {
+      const Side s = side_x(Q, k, j);
+      const BarStep d = ld_step(L.sx() + k * 48, j);
+      rx += s.mu * d.dlu - s.ml * d.dll;
+    }
+    for (int ch = 0; ch < L.nch; ++ch) {
+      const int r = ch * 12 + j;
+      const bool ok = el && r < a.ng;
+      double dl = 0.0;
+      if (ok) {
+        const Side sg = side_g(Q, k, r);
+        const BarStep d = ld_step(L.gb(k, ch) + 48, j);
+        dl = sg.mu * d.dlu - sg.ml * d.dll;
+      }
+      double Yc[12];
+      gen_col<false>(Q, k, ch, jj, el, Yc);
+      ru = dot_bcast(Yc, dl, ru);
+      if constexpr (HAS_C) {
+        gen_col<true>(Q, k, ch, jj, el, Yc);
+        rx = dot_bcast(Yc, dl, rx);
+      }
+    }
+    double M[12];
+    double rb = 0.0;
+    if (k < N) {
+      load12(Q.R(k) + jj * 12, M);
+      ru = dot_bcast(M, duj, ru);  // + R du
+      load_strided(Q.S(k) + jj, 12, M);
+      ru = dot_bcast(M, dxj, ru);  // + S dx
+      load12(Q.B(k) + jj * 12, M);
+      ru = dot_bcast(M, dpnj, ru);  // + B'dpi_k+1
+      load12(Q.S(k) + jj * 12, M);
+      rx = dot_bcast(M, duj, rx);  // + S'du
+      load12(Q.A(k) + jj * 12, M);
+      rx = dot_bcast(M, dpnj, rx);  // + A'dpi_k+1
+      load_strided(Q.A(k) + jj, 12, M);
+      rb = dot_bcast(M, dxj, el ? L.rb()[k * 12 + j] - L.dx()[(k + 1) * 12 + j] : 0.0);  // + A dx
+      load_strided(Q.B(k) + jj, 12, M);
+      rb = dot_bcast(M, duj, rb);  // + B du
+    }
+    load12(Q.Q(k) + jj * 12, M);
+    rx = dot_bcast(M, dxj, rx);  // + Q dx
+    if (!(el && k < N)) ru = 0.0;
+    if (!(el && k > 0)) rx = 0.0;  // (x_0 is fixed)
+    if (!(el && k < N)) rb = 0.0;
+    ng = fmax(ng, fmax(nabs(ru), nabs(rx)));
+    nb = fmax(nb, nabs(rb));
+    if (el) {
+      L.gtu()[k * 12 + j] = ru;
+      L.gtx()[k * 12 + j] = rx;
+      L.v12(L.ref_b())[k * 12 + j] = rb;
+    }
+  }
+  red_put(L, 0, g16max(ng));
+  red_put(L, 1, g16max(nb));
+}
+
+// The correction (solved by the corrector's recursion on the check's residual: ddx in gtu, k, p
+// of the correction in kv, pv) added to the step: du += K ddx + k, dx += ddx, dpi += P ddx + p;
+// the barrier steps are linear in the primal step (ddt = +-ddv, ddlam = -lam ddt / t); then the
+// step ratios of the whole step and the non-finite check, as step_pass leaves them.
+__device__ __forceinline__ void corr_apply_pass(const Qp Q, const Lds L) {
+  const ProblemArgsT<double>& a = Q.a;
+  const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
+  const bool el = j < 12;
+  const int jj = el ? j : 11;
+  double ap = 1e30, ad = 1e30;
+  bool bad = false;
+  auto upd = [&](const Side& sd, const Bar& b, BarStep& d, double dv) {
+    if (sd.ml != 0.0) {
+      d.dtl += dv;
+      d.dll -= b.ll * dv / b.tl;
+    }
+    if (sd.mu != 0.0) {
+      d.dtu -= dv;
+      d.dlu += b.lu * dv / b.tu;
+    }
+  };
+  const double* cdx = L.v12(Lds::kRefDx);
+  for (int k = grp; k <= N; k += kGroups) {
+    const double* rk = Q.rec(k);
+    const double cxj = el ? cdx[k * 12 + j] : 0.0;
+    double cuj = 0.0, cpj = 0.0;
+    if (k < N) {
+      double Kr[12];
+      sfor<0, 12>([&](auto i) { Kr[decltype(i)::value] = rk[kRK + jj * 13 + decltype(i)::value]; });
+      cuj = dot_bcast(Kr, cxj, L.kv()[k * 12 + jj]);
+      if (!el) cuj = 0.0;
+    }
+    if (k > 0) {
+      double Pr[12];
+      load_packed_sym(rk + kRP, jj, Pr);
+      cpj = dot_bcast(Pr, cxj, L.pv()[k * 12 + jj]);
+      if (!el) cpj = 0.0;
+    }
+    if (el) {
+      double duj = 0.0;
+      if (k < N) {
+        duj = L.du()[k * 12 + j] + cuj;
+        L.du()[k * 12 + j] = duj;
+      }
+      const double dxj = L.dx()[k * 12 + j] + cxj;
+      L.dx()[k * 12 + j] = dxj;
+      double dpj = 0.0;
+      if (k > 0) {
+        dpj = L.dpi()[k * 12 + j] + cpj;
+        L.dpi()[k * 12 + j] = dpj;
+      }
+      bad |= huge(duj) || huge(dxj) || huge(dpj);
+    }
+    if (k < N && el) {
+      const Side s = side_u(Q, k, j);
+      const Bar b = ld_bar(L.bu() + k * 48, j);
+      BarStep d = ld_step(L.su() + k * 48, j);
+      upd(s, b, d, cuj);
+      ratio(s, b, d, ap, ad);
+      bad |= huge(d.dtl) || huge(d.dtu) || huge(d.dll) || huge(d.dlu);
+      st_step(L.su() + k * 48, j, d);
+    }
+    if (k > 0 && el) {
+      const Side s = side_x(Q, k, j);
+      const Bar b = ld_bar(L.bx() + k * 48, j);
+      BarStep d = ld_step(L.sx() + k * 48, j);
+      upd(s, b, d, cxj);
+      ratio(s, b, d, ap, ad);
+      bad |= huge(d.dtl) || huge(d.dtu) || huge(d.dll) || huge(d.dlu);
+      st_step(L.sx() + k * 48, j, d);
+    }
+    for (int ch = 0; ch < L.nch; ++ch) {
+      const int r = ch * 12 + j;
+      const bool ok = el && r < a.ng;
+      double Dr[12], Cr[12];
+      load_strided(ok ? Q.Drow(k, r) : nullptr, a.ng, Dr);
+      load_strided(ok ? Q.Crow(k, r) : nullptr, a.ng, Cr);
+      const double dv = dot_bcast(Cr, cxj, dot_bcast(Dr, cuj, 0.0));
+      if (ok) {
+        double* g = L.gb(k, ch);
+        const Side s = side_g(Q, k, r);
+        const Bar b = ld_bar(g, j);
+        BarStep d = ld_step(g + 48, j);
+        upd(s, b, d, dv);
+        ratio(s, b, d, ap, ad);
+        bad |= huge(d.dtl) || huge(d.dtu) || huge(d.dll) || huge(d.dlu);
+        st_step(g + 48, j, d);
+      }
+    }
+  }
+  red_put(L, 0, g16min(ap));
+  red_put(L, 1, g16min(ad));
+  red_put(L, 4, g16max(bad ? 1.0 : 0.0));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1203,7 +1461,9 @@ __device__ __forceinline__ void outputs(const Qp Q, const Lds L) {
   }
 }
 
-template <bool HAS_C>
+// ITREF: HPIPM's iterative refinement of the step (Balance / Robust; a separate instantiation so
+// the Speed path keeps its registers)
+template <bool HAS_C, bool ITREF>
 __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<double> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int N = a.N;
@@ -1310,6 +1570,44 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
       ad = uni(red_min(L, 1));
       bad = uni(red_max(L, 4)) > 0.0;
     }
+    // ---- iterative refinement of the final step (Balance / Robust) ----
+    if (ITREF && a.itref_corr_max > 0) {
+      double n0g = 0.0, n0b = 0.0;
+      int cnt = 0;
+#pragma unroll 1
+      for (int ir = 0; ir < a.itref_corr_max; ++ir) {
+        __syncthreads();  // (red reuse)
+        lin_res_pass<HAS_C>(Q, L);
+        __syncthreads();
+        const double ngr = uni(red_max(L, 0)), nbr = uni(red_max(L, 1));
+        if (ir == 0) {
+          n0g = ngr;
+          n0b = nbr;
+        }
+        if (next) {  // HPIPM stat: lin_res_stat, lin_res_eq of the last check
+          next[14] = ngr;
+          next[15] = nbr;
+        }
+        if ((ngr < a.tol_stat || ngr < 1e-3 * n0g) && (nbr < a.tol_eq || nbr < 1e-3 * n0b)) break;
+        // the correction: the corrector's recursion with (r_u, r_x, r_b) as right-hand side
+        const Rhs ref{9, 10, L.ref_b(), L.ref_pb()};
+        corr_rhs_stages(Q, L, ref);
+        __syncthreads();
+        corr_rhs_chain(L, N);
+        __syncthreads();
+        corr_k_stages(Q, L, ref);
+        __syncthreads();
+        forward(L, N, Lds::kRefDx);
+        __syncthreads();
+        corr_apply_pass(Q, L);
+        __syncthreads();
+        ap = uni(red_min(L, 0));
+        ad = uni(red_min(L, 1));
+        bad = uni(red_max(L, 4)) > 0.0;
+        ++cnt;
+        if (next) next[13] = cnt;  // HPIPM stat: itref_corr
+      }
+    }
     if (bad) {
       ap = 0.0;
       ad = 0.0;
@@ -1353,8 +1651,7 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
 bool ipm_latency_ok(const ProblemArgsT<double>& a, int max_batch) {
   if (a.batch < 1 || a.batch > max_batch) return false;
   if (a.nx != 12 || a.nu != 12 || a.N < 1) return false;
-  if (a.ric_alg || a.itref_corr_max || a.lq_fact || a.warm_start > 1 || a.warm_bars || a.skip_last_rb)
-    return false;
+  if (a.ric_alg || a.lq_fact || a.warm_start > 1 || a.warm_bars || a.skip_last_rb) return false;
   const int nch = (a.ng + 11) / 12;
   if (ipm_lat::lds_doubles(a.N, nch) * sizeof(double) > 160 * 1024) return false;
   return a.ws && a.ws_qp >= (size_t)(a.N + 1) * ipm_lat::kRStage;
@@ -1364,10 +1661,17 @@ hipError_t launch_ipm_latency(const ProblemArgsT<double>& a, hipStream_t stream)
   // (the LDS limit is set once per device: prepare_ipm_latency_device, srbd_qp_create)
   const int nch = (a.ng + 11) / 12;
   const size_t bytes = ipm_lat::lds_doubles(a.N, nch) * sizeof(double);
+  const dim3 grid(a.batch), block(ipm_lat::kThreads);
   if (a.C && a.ng > 0) {
-    hipLaunchKernelGGL(ipm_lat::ipm_latency_kernel<true>, dim3(a.batch), dim3(ipm_lat::kThreads), bytes, stream, a);
+    if (a.itref_corr_max > 0)
+      hipLaunchKernelGGL((ipm_lat::ipm_latency_kernel<true, true>), grid, block, bytes, stream, a);
+    else
+      hipLaunchKernelGGL((ipm_lat::ipm_latency_kernel<true, false>), grid, block, bytes, stream, a);
   } else {
-    hipLaunchKernelGGL(ipm_lat::ipm_latency_kernel<false>, dim3(a.batch), dim3(ipm_lat::kThreads), bytes, stream, a);
+    if (a.itref_corr_max > 0)
+      hipLaunchKernelGGL((ipm_lat::ipm_latency_kernel<false, true>), grid, block, bytes, stream, a);
+    else
+      hipLaunchKernelGGL((ipm_lat::ipm_latency_kernel<false, false>), grid, block, bytes, stream, a);
   }
   return hipGetLastError();
 }
@@ -1376,11 +1680,13 @@ hipError_t launch_ipm_latency(const ProblemArgsT<double>& a, hipStream_t stream)
 // the handle's device, like prepare_riccati_device)
 hipError_t prepare_ipm_latency_device() {
   constexpr int kBytes = 160 * 1024;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<true>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, kBytes);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, kBytes);
+  const void* fns[] = {reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<true, false>),
+                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, false>),
+                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<true, true>),
+                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, true>)};
+  hipError_t e = hipSuccess;
+  for (const void* f : fns)
+    if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kBytes);
   return e;
 }
 

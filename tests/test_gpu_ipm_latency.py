@@ -1,6 +1,7 @@
 """GPU parity of the one-launch latency IPM (srbd-nmpc-solver_amd/csrc/ipm_latency.hip): the
-C-ABI sends fp64 classical-Riccati (ric_alg 0) Speed solves of up to SRBD_IPM_LATENCY_MAX QPs
-(default 512) there, one workgroup per QP, and everything else to the batched kernels.
+C-ABI sends fp64 classical-Riccati (ric_alg 0) solves -- Speed, and since round 6 Balance /
+Robust with HPIPM's iterative refinement -- of up to SRBD_IPM_LATENCY_MAX QPs (default 512)
+there, one workgroup per QP, and everything else to the batched kernels.
 
 Checked against the oracle (oracle/ocp_qp_oracle.c oracle_solve, HPIPM d_ocp_qp_ipm_solve
 restated) and against the batched kernels on the same QPs (SRBD_IPM_LATENCY_MAX=0 forces
@@ -189,3 +190,47 @@ def test_many_general_rows(pkg, oracle):
     out = pkg.capi.solve(qp, x0, st)
     ref = oracle.solve(qp, st, x0=x0)
     _check_vs_oracle(out, ref, qp.batch, oracle_misses=1)
+
+
+@pytest.mark.parametrize("mode,nmax", [("Balance", 2), ("Robust", 4)])
+@pytest.mark.parametrize("dims", [(12, 12, 0, 41), (12, 4, 14, 45), (5, 3, 14, 47)])
+def test_itref_forced_corrections_both_paths(pkg, oracle, mode, nmax, dims):
+    """HPIPM's iterative refinement of the step (Balance: at most 2 corrections per iteration,
+    Robust 4) on the latency IPM (ric_alg 0; the reference test's compareResults runs Balance,
+    test/ocp_qp_ipm_solver.cpp:243).  Tolerances of 1e-30 make every check fail, so every
+    iteration runs all its corrections: the latency IPM, the batched kernels and the oracle
+    (which refines the same way) follow the same iterates to 1e-7, and the stat table counts
+    the corrections (column 13, as the batched kernels do) and holds the checks' norms (14, 15)."""
+    nx, nu, ng, seed = dims
+    qp, x0 = helpers.random_constrained(16, 10, nx, nu, ng, seed, pkg.OcpQpBatch)
+    tiny = dict(tol_stat=1e-30, tol_eq=1e-30, tol_ineq=1e-30, tol_comp=1e-30)
+    st = dict(NMPC, iter_max=8, mode=mode, **tiny)
+    lat, bat = both(pkg, qp, x0, st, stats=True)
+    ref = oracle.solve(qp, st, x0=x0)
+    assert np.all(lat["status"] == 1) and np.all(bat["status"] == 1), (lat["status"], bat["status"])
+    for i in range(qp.batch):
+        for key in ("x", "u"):
+            assert helpers.is_approx(lat[key][i], ref[key][i], 1e-7), (key, i)
+            assert helpers.is_approx(lat[key][i], bat[key][i], 1e-7), (key, i)
+    cnt = lat["stat"][:, 1:9, 13]
+    assert np.all((cnt >= 1) & (cnt <= nmax)), cnt
+    assert np.array_equal(cnt, bat["stat"][:, 1:9, 13]), (cnt, bat["stat"][:, 1:9, 13])
+    assert np.all(np.isfinite(lat["stat"][:, 1:9, 14:16])) and np.all(lat["stat"][:, 1:9, 14:16] >= 0)
+
+
+@pytest.mark.parametrize("mode", ["Balance", "Robust"])
+@pytest.mark.parametrize("constraints", ["box_u", "cone"])
+def test_itref_srbd_converged(pkg, oracle, mode, constraints):
+    """The SRBD QPs of configs 3 / 5 (N = 20, fp64) in Balance / Robust mode on the latency IPM:
+    the oracle's solution at 1e-7 in its iterations +-1, the batched kernels' status, and
+    residuals at the tolerance."""
+    qp, x0 = pkg.srbd_model.generate_batch(16, N=20, seed=616, constraints=constraints)
+    st = dict(NMPC, mode=mode)
+    lat, bat = both(pkg, qp, x0, st, stats=True)
+    ref = oracle.solve(qp, st, x0=x0)
+    _check_vs_oracle(lat, ref, qp.batch)
+    assert np.array_equal(lat["status"], bat["status"])
+    for i in range(qp.batch):
+        for key in ("x", "u"):
+            assert helpers.is_approx(lat[key][i], bat[key][i], 1e-7), (key, i)
+        assert np.all(lat["res"][i] <= 1e-8), lat["res"][i]
