@@ -727,57 +727,13 @@ __device__ __forceinline__ void corr_terms(const Qp Q, const Lds L, double smu) 
   }
 }
 
-// [P | p] in the tiles' C/D layout (wave 0) -> [Lp | s]: Lp = chol(P) (lower, a non-positive pivot
-// zeroes its column: BLASFEO dpotrf_l, riccati.h sqrt_factor) and s = Lp^-1 p, the border column
-// of the same elimination; through the G/H tile (column-owned Cholesky, then back)
-__device__ __forceinline__ lat_d4 sqrt_tile(const lat_d4& Pt, double* gh, int g, int c) {
-  const bool cv = c < 12, cw = c <= 12;
-  lds_wave_fence();
-  sfor<0, 3>([&](auto rr) {
-    constexpr int R = decltype(rr)::value;
-    if (cw) gh[c * 12 + g + 4 * R] = Pt[R];
-  });
-  lds_wave_fence();
-  double Pc[12], Lc[12], rs;
-  sfor<0, 12>([&](auto i) {
-    const double v = gh[(cw ? c : 12) * 12 + decltype(i)::value];
-    Pc[decltype(i)::value] = cw ? v : 0.0;
-  });
-  lat_chol<true>(Pc, c, 0.0, Lc, rs, [](auto) {});
-  lds_wave_fence();
-  sfor<0, 12>([&](auto i) {
-    constexpr int I = decltype(i)::value;
-    const double ri = bc<I>(rs);
-    // lane c < 12: column c of Lp (zero above the diagonal); lane 12: s
-    const double v = cv ? (I >= c ? Lc[I] : 0.0) : Lc[I] * ri;
-    if (cw && g == 0) gh[c * 12 + I] = v;
-  });
-  lds_wave_fence();
-  lat_d4 o;
-  sfor<0, 4>([&](auto rr) {
-    constexpr int R = decltype(rr)::value;
-    const int row = g + 4 * R < 12 ? g + 4 * R : 11;
-    const double v = gh[(cw ? c : 12) * 12 + row];
-    o[R] = (g + 4 * R < 12 && cw) ? v : 0.0;
-  });
-  lds_wave_fence();
-  return o;
-}
-
 // ---------------------------------------------------------------------------------------------
 // phase: the factorization (backward, serial in k) on matrix cores -- riccati_latency_impl.h's
 // sweep.  Wave 0: stage k's products and Cholesky; wave 1: stage k+1's K, record and closed
 // loop; wave 2: stage k-1's operands (A, B from the QP, R~ S~ Q~ r~ q~ b~ from the record) into
 // the LDS ring, so no global load sits on the chain.  Records per stage: [K | k] rows, P packed,
 // p, L packed + 1 / diag; [Acl | bcl] rows in LDS.
-// SQRT (ric_alg 1, hpipm-cpp's default; riccati.h riccati_step_sqrt): the chain carries the factor
-// Lp of P_k+1 and s = Lp^-1 p_k+1 instead of [P | p], and the same MFMAs form MB = Lp'B,
-// MA = Lp'[A | b~] + [0 | s], G = R~ + MB'MB, [H | g] = [S~ | r~] + MB'MA, [F | f] = [Q~ | q~] +
-// MA'MA (sums of squares: the classical B'PB, B'P[A | b~], A'P[A | b~] in exact arithmetic);
-// P_k = F - Y'Y goes to the record as in the classical form (the sweeps apply it explicitly) and
-// is factorized again for the next stage (sqrt_tile: a second Cholesky on the chain).
 // ---------------------------------------------------------------------------------------------
-template <bool SQRT>
 __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
   const ProblemArgsT<double>& a = Q.a;
   const int N = Q.N;
@@ -818,7 +774,6 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
       if (cv && row >= c) wn[kRP + packed_col(c) + row - c] = Pt[R];
       if (c == 12) wn[kRp + row] = Pt[R];
     });
-    if constexpr (SQRT) Pt = sqrt_tile(Pt, gh, g, c);
   } else if (wave == 2) {
     load_slot(N - 1);
   }
@@ -878,15 +833,11 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
         St[R] = rok && cw ? sv : 0.0;
         Qt[R] = rok && cw ? qv : 0.0;
       });
-      // WB = P B; G = R~ + B'WB (the critical path).  SQRT: the A operand Pt is Lp, so WB = Lp'B
-      // = MB and G = R~ + MB'MB.
+      // WB = P B; G = R~ + B'WB (the critical path)
       lat_d4 WB = {0.0, 0.0, 0.0, 0.0};
       sfor<0, 3>([&](auto kb) { WB = lat_mfma(Pt[decltype(kb)::value], bo[decltype(kb)::value], WB); });
       lat_d4 Gt = Rt;
-      sfor<0, 3>([&](auto kb) {
-        constexpr int KB = decltype(kb)::value;
-        Gt = lat_mfma(SQRT ? WB[KB] : bo[KB], WB[KB], Gt);
-      });
+      sfor<0, 3>([&](auto kb) { Gt = lat_mfma(bo[decltype(kb)::value], WB[decltype(kb)::value], Gt); });
       // W = P [A | b~] + [0 | p]; [H | g] = [S~ | r~] + B'W; [F | f] = [Q~ | q~] + A'W: one per pivot
       lat_d4 Wt;
       sfor<0, 4>([&](auto rr) { Wt[decltype(rr)::value] = c == 12 ? Pt[decltype(rr)::value] : 0.0; });
@@ -897,11 +848,10 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
           Wt = lat_mfma(Pt[K], ao[K], Wt);
         } else if constexpr (K < 9) {
           constexpr int KB = (K - 3) / 2;
-          // (SQRT: W = MA; H = S~ + MB'MA, F = Q~ + MA'MA)
           if constexpr ((K - 3) % 2 == 0) {
-            Ht = lat_mfma(SQRT ? WB[KB] : bo[KB], Wt[KB], Ht);
+            Ht = lat_mfma(bo[KB], Wt[KB], Ht);
           } else {
-            Ft = lat_mfma(SQRT ? Wt[KB] : ao[KB], Wt[KB], Ft);
+            Ft = lat_mfma(ao[KB], Wt[KB], Ft);
           }
         }
       };
@@ -977,8 +927,6 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
         if (cv && row >= c) rk[kRP + packed_col(c) + row - c] = Pt[R];
         if (c == 12) rk[kRp + row] = Pt[R];
       });
-      if constexpr (SQRT)
-        if (k > 0) Pt = sqrt_tile(Pn, gh, g, c);
     } else if (wave == 1) {
       if (k < N - 1) finish_stage(k + 1);
     } else if (wave == 2) {

@@ -234,3 +234,4 @@ def test_itref_srbd_converged(pkg, oracle, mode, constraints):
         for key in ("x", "u"):
             assert helpers.is_approx(lat[key][i], bat[key][i], 1e-7), (key, i)
         assert np.all(lat["res"][i] <= 1e-8), lat["res"][i]
+
