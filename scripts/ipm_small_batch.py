@@ -4,7 +4,8 @@ settings (iter_max 30), batches 1 / 16 / 256 / 512 / 1024, one C-ABI call per so
 buffers; prints one JSON line {batch: {median_ms, min_ms, iters_max, iters_mean}}.
 SRBD_QP_LIB selects the library (A/B against an older build); SRBD_IPM_LATENCY_MAX=0 in the
 environment keeps every batch on the batched kernels (ipm_latency.hip is the default up to 512).
-Usage: ipm_small_batch.py [reps] [constraints]"""
+Usage: ipm_small_batch.py [reps] [constraints] [mode]  (mode: HPIPM's Speed / Balance / Robust;
+the NMPC's Speed by default)"""
 import importlib.util
 import json
 import sys
@@ -25,11 +26,14 @@ def main():
     capi = pkg.capi
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
     cons = sys.argv[2] if len(sys.argv) > 2 else "box_u"
+    settings = dict(bench.NMPC_SETTINGS)
+    if len(sys.argv) > 3:
+        settings["mode"] = sys.argv[3]
     out = {}
     for batch in (1, 16, 256, 512, 1024):
         qp, x0 = pkg.srbd_model.generate_batch(batch, N=20, seed=11, constraints=cons)
         h = capi.Handle(20, 12, 12, qp.ng, qp.has_box_u, qp.has_box_x, capacity=batch)
-        s = capi.settings_struct(bench.NMPC_SETTINGS)
+        s = capi.settings_struct(settings)
         dt, st, data, sol = capi.device_buffers(qp, x0)
         torch.cuda.synchronize()
         ts = []
