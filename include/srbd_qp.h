@@ -267,16 +267,27 @@ int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* setti
  * the reference's call pattern) goes to the handle's resident server: a
  * one-workgroup kernel on its own stream that polls a mailbox in mapped host
  * memory, so a call costs no launch; it leaves its CU after 5 ms without a
- * request (or at srbd_qp_destroy / process exit) and the next call relaunches
- * it.  While it is up it holds one CU, and a device-wide synchronize waits
- * for it to leave.  SRBD_LAT_SERVER=0 (environment) launches per call.   */
+ * request, after its first answer once it has been up 20 ms, or at
+ * srbd_qp_destroy / process exit, and the next call relaunches it (also when
+ * it left between the call's check and its post).  While it is up it holds
+ * one CU, and a device-wide synchronize waits for it to leave.  Its stream
+ * has the greatest priority: HIP maps a process's streams onto a few hardware
+ * queues per priority that run their packets in order, so a kernel queued
+ * behind the server on a shared queue would wait for it; default-priority
+ * streams never share its queue, and another high-priority stream that does
+ * waits at most the 20 ms lifetime.  SRBD_LAT_SERVER=0 (environment) launches
+ * per call; SRBD_LAT_SERVER_IDLE_MS overrides the 5 ms (tests).          */
 int srbd_qp_solve_host_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
                            const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol);
 
 /* srbd_qp_solve_host_f64 that hands the caller the Riccati outputs early:
- * `on_factors(ctx)` runs once on the calling thread, before the call returns
- * and only if the solve succeeds, as soon as sol->P, p, K, k are final in the
- * caller's buffers.  On the zero-copy single-QP path (above; fp64 classical
+ * `on_factors(ctx)` runs at most once on the calling thread, before the call
+ * returns, as soon as sol->P, p, K, k have been written to the caller's
+ * buffers.  The call's return code and sol->status then decide whether they
+ * are valid: the callback can run and the call still return an error (a
+ * device failure after the factors were written) or a QP end with status 3
+ * (NaN: the status is set after the callback), so a caller keeps what it
+ * unpacked only on SRBD_QP_OK and status 0.  On the zero-copy single-QP path (above; fp64 classical
  * Riccati, N <= 20) that is while the kernel still runs its forward sweep,
  * u / pi and residual passes, so a caller can unpack the factors (the bulk of
  * the outputs) under the kernel's tail; elsewhere it runs after the solve.

@@ -120,11 +120,14 @@ __device__ __forceinline__ Bar warm_bar(const real* p, const Side& s) {
 // The RB sweep's per-group LDS blocks (A, B, S: 3 x 144 reals per QP group).  One
 // function, so one allocation per kernel: the fused RB -> F1 kernel's F1 reuses them.
 // RB also stages each stage's factor record there (kRecSize reals) once the blocks are dead
-// (kRecImg: the box kernels; the general-row kernels' LDS and registers are at their limits
-// -- the fp32 ones' fp64 G scratch leaves no room for the larger block at 3 workgroups per
-// CU, the fp64 ones spill -- and they store the record directly).
+// (kRecImg: the box kernels and the fp32 general-row kernels; the fp64 general-row ones, at
+// their register limit, store the record directly).
+// The record is 348 reals, below the block's 432 since the open-loop sweeps (round 3), so the
+// fp32 general-row kernels stage it too with no more LDS: cone fp32 N = 40 175.4 vs 180.2 ms
+// (round 6, same-box A/B against direct stores, profiles/round6/ab_recimg_cone_n40_f32.log).
+// The fp64 general-row kernels (not benchmarked; they spill) keep direct stores.
 template <int GEN>
-constexpr bool kRecImg = GEN == 0;
+constexpr bool kRecImg = GEN == 0 || sizeof(real) == 4;
 template <int GEN>
 constexpr int kGroupLds = kRecImg<GEN> && kRecSize > 3 * 144 ? kRecSize : 3 * 144;
 template <int GEN>
