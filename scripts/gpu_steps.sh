@@ -16,7 +16,9 @@
 #   degen                       scripts/dev/degen_counts.py: degenerate-family counts per path
 #   profile:WORKLOAD            scripts/profile.sh (kernel trace + FETCH / WRITE passes)
 #   refcase:CASE                rocprofv3 kernel trace of build/hpipm_cpp_test CASE
-#   callpattern                 build/call_pattern_bench (the reference's one-QP call pattern)
+#   callpattern[:TREE]          bench.py's reference_call_pattern line (the reference's one-QP
+#                               call pattern, build/call_pattern_bench) 3 times; with TREE (a
+#                               built worktree, e.g. build/r05tree) alternating with that tree
 #   bench                       the default bench.py line
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -43,7 +45,13 @@ for step in "$@"; do
     profile) timeout -k 10 900 ./scripts/profile.sh steps "$a" > "$O/profile_$a.log" 2>&1 ;;
     refcase) timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$O/ref_$a" -o "$a" -- \
                ./build/hpipm_cpp_test --golden tests/golden "$a" > "$O/ref_$a.log" 2>&1 ;;
-    callpattern) timeout -k 10 120 ./build/call_pattern_bench > "$O/call_pattern.log" 2>&1 ;;
+    callpattern)
+      for r in 1 2 3; do
+        timeout -k 10 120 python -u scripts/dev/call_pattern.py >> "$O/call_pattern.log" 2>&1 || exit $?
+        if [ -n "$a" ]; then
+          (cd "$a" && timeout -k 10 120 python -u scripts/dev/call_pattern.py) >> "$O/call_pattern_$(basename "$a").log" 2>&1 || exit $?
+        fi
+      done ;;
     bench) timeout -k 10 600 python3 bench.py > "$O/bench_default.json" 2> "$O/bench_default.log" ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
