@@ -20,6 +20,7 @@
 #                               call pattern, build/call_pattern_bench) 3 times; with TREE (a
 #                               built worktree, e.g. build/r05tree) alternating with that tree
 #   bench                       the default bench.py line
+#   smoke                       __graft_entry__.smoke()
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -53,6 +54,7 @@ for step in "$@"; do
         fi
       done ;;
     bench) timeout -k 10 600 python3 bench.py > "$O/bench_default.json" 2> "$O/bench_default.log" ;;
+    smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
   rc=$?
