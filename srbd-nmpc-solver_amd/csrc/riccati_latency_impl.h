@@ -36,9 +36,6 @@
 // d_ocp_qp_fact_solve_kkt_unconstr), another summation order: the outputs match the batched
 // kernel's to rounding (tests/test_gpu_riccati.py), not bit for bit.
 
-#ifndef SRBD_LAT_AUG
-#define SRBD_LAT_AUG 0
-#endif
 constexpr int kLatThreads = 512;  // wave 0: factorization, wave 1: records, all: the passes
 constexpr int kLatTile = 156;     // 13 columns x 12 rows, column-major (ld 12)
 constexpr int kLatL = 90;         // packed L (78) + 1 / diag (12)
@@ -176,100 +173,6 @@ __device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigne
       sfor<0, 3>([&](auto kb) { WB = lat_mfma(Pt[decltype(kb)::value], bo[decltype(kb)::value], WB); });
       lat_d4 Gt = Rt;
       sfor<0, 3>([&](auto kb) { Gt = lat_mfma(bo[decltype(kb)::value], WB[decltype(kb)::value], Gt); });
-#if SRBD_LAT_AUG
-      // One elimination of the stage's augmented matrix [G H; H' F] (with [g; f] as its last
-      // column) over G's 12 pivots: G's columns become the Cholesky factor, [H | g] becomes
-      // L_unit^-1 [H | g] (Y = D^-1/2 times it) and the trailing block becomes the Schur
-      // complement [F | f] - Y'[Y | y] = [P | p]_k, pivot by pivot in registers: no separate
-      // triangular solve, no LDS hand-over and no Y'Y product on the chain.  The W, H, F products
-      // are issued right behind G (the elimination needs them from its first pivot).
-      lat_d4 Wt;
-      sfor<0, 4>([&](auto rr) { Wt[decltype(rr)::value] = c == 12 ? Pt[decltype(rr)::value] : 0.0; });
-      sfor<0, 3>([&](auto kb) { Wt = lat_mfma(Pt[decltype(kb)::value], ao[decltype(kb)::value], Wt); });
-      lat_d4 Ht = St, Ft = Qt;
-      sfor<0, 3>([&](auto kb) {
-        Ht = lat_mfma(bo[decltype(kb)::value], Wt[decltype(kb)::value], Ht);
-        Ft = lat_mfma(ao[decltype(kb)::value], Wt[decltype(kb)::value], Ft);
-      });
-      tstamp(1);
-      double* yb = ybuf + (k & 1) * kLatTile;  // (free until this stage's Y goes in: the H tile)
-      double* lb = lbuf + (k & 1) * kLatL;
-      lds_wave_fence();
-      sfor<0, 3>([&](auto rr) {
-        constexpr int R = decltype(rr)::value;
-        if (cv) gh[c * 12 + g + 4 * R] = Gt[R];
-        if (cw) yb[c * 12 + g + 4 * R] = Ht[R];
-      });
-      lds_wave_fence();
-      double Gc[12], Hc[12], Fc[12];
-      sfor<0, 12>([&](auto i) {
-        constexpr int I = decltype(i)::value;
-        const double gv = gh[cc * 12 + I];
-        Gc[I] = cv ? gv : 0.0;
-        const double hv = yb[(cw ? c : 12) * 12 + I];
-        Hc[I] = cw ? hv : 0.0;
-      });
-      lds_wave_fence();
-      sfor<0, 3>([&](auto rr) {
-        constexpr int R = decltype(rr)::value;
-        if (cw) gh[c * 12 + g + 4 * R] = Ft[R];
-      });
-      lds_wave_fence();
-      sfor<0, 12>([&](auto i) {
-        constexpr int I = decltype(i)::value;
-        const double fv = gh[(cw ? c : 12) * 12 + I];
-        Fc[I] = cw ? fv : 0.0;
-      });
-      tstamp(3);
-      // pivot K: G's columns right of it and every [H | g] column lose G[:, K] (G[K][.] / d_K);
-      // the trailing block loses h_K h_K' / d_K with h_K = row K of [H | g] (lane i: H[K][i])
-      double dmine = 1.0;
-      sfor<0, 12>([&](auto kk) {
-        constexpr int K = decltype(kk)::value;
-        const double dk = bc<K>(Gc[K]) + a.reg;
-        const double inv = dk > 0.0 ? lat_recip(dk) : 0.0;
-        const double sg = c > K ? Gc[K] * inv : 0.0;
-        const double th = Hc[K] * inv;
-        sfor<K + 1, 12>([&](auto i) {
-          constexpr int I = decltype(i)::value;
-          const double gik = bc<K>(Gc[I]);
-          Gc[I] = fmadd(-gik, sg, Gc[I]);
-          Hc[I] = fmadd(-gik, th, Hc[I]);
-        });
-        fma_bcast_lanes(Fc, Hc[K], -th);
-        dmine = c == K ? dk : dmine;
-      });
-      double rs, inv_l, Lc[12], Yc[12];
-      pivot_rs(dmine, rs, inv_l);
-      sfor<0, 12>([&](auto i) {
-        constexpr int I = decltype(i)::value;
-        Lc[I] = Gc[I] * inv_l;
-        Yc[I] = cw ? apply_rs(Hc[I], bc<I>(rs)) : 0.0;
-      });
-      tstamp(7);
-      // hand L and [Y | y] to wave 1
-      if (l < 16) {
-        if (cw) store12(yb + c * 12, Yc);
-        if (cv) {
-          store_packed_col(lb, c, Lc);
-          lb[78 + c] = rs;
-        }
-      }
-      // [P | p]_k: lane (g, c) of the tile takes rows g, g + 4, g + 8 of its column
-      sfor<0, 3>([&](auto rr) {
-        constexpr int R = decltype(rr)::value;
-        const double v = g == 0 ? Fc[4 * R] : g == 1 ? Fc[4 * R + 1] : g == 2 ? Fc[4 * R + 2] : Fc[4 * R + 3];
-        Pt[R] = cw ? v : 0.0;
-      });
-      Pt[3] = 0.0;
-      tstamp(9);
-      // record: P packed, p (the batched kernel's layout), from the column-owned registers
-      double* rk = rec(k);
-      if (l < 16) {
-        if (cv) store_packed_col(rk + kWsP, c, Fc);
-        if (c == 12) store12(rk + kWsp, Fc);
-      }
-#else
       // W = P [A | b] + [0 | p]; [H | g] = [S | r] + B'W; [F | f] = [Q | q] + A'W: issued one
       // per pivot inside the Cholesky below (W0 W1 W2 H0 F0 H1 F1 H2 F2)
       lat_d4 Wt;
@@ -347,7 +250,6 @@ __device__ __forceinline__ void lat_solve(const ProblemArgsT<double>& a, unsigne
         if (cv && row >= c) rk[kWsP + packed_col(c) + row - c] = Pt[R];
         if (c == 12) rk[kWsp + row] = Pt[R];
       });
-#endif
     } else if (wave == 1 && k < N - 1) {
       finish_stage(k + 1);
     }
