@@ -159,13 +159,13 @@ bool unconstr_reads_once(const ProblemArgsT<T>& a);
 // mapped, coherent host memory; the host writes seq / quit, the kernel done / exited.
 struct alignas(8) LatMailbox {
   int seq;     // host: number of the request posted last
-  int quit;    // host: leave now (seq and quit: one 8-byte word the server polls)
+  int flags;   // host: kLatQuit (leave now), kLatArm (this request writes the early factors and
+               // sets factors_ready, the launch's fixed flags pointer); seq and flags are one
+               // 8-byte word the server polls, a post writes both at once
   int done;    // device: number of the request finished last
   int exited;  // device: epoch of the server launch that has left
-  int arm;     // host, per request: write the early factors and set factors_ready (the
-               // launch's fixed flags pointer); written before seq
-  int pad;
 };
+constexpr int kLatQuit = 1, kLatArm = 2;
 // true when launch_riccati_unconstr(a) would be one latency-kernel workgroup reading its QP
 // once (batch 1, classical Riccati, N <= 20): the server can take the call instead
 bool latency_server_ok(const ProblemArgsT<double>& a);

@@ -265,7 +265,7 @@ void server_atexit() {
   std::lock_guard<std::mutex> lk(g_srv_mu);
   for (srbd_qp_handle h : g_srv_live) {
     volatile srbd::LatMailbox* mb = h->srv_mb;
-    mb->quit = 1;
+    mb->flags = srbd::kLatQuit;
     const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
     while (mb->exited != h->srv_epoch && std::chrono::steady_clock::now() < t_end) std::this_thread::yield();
   }
@@ -280,9 +280,9 @@ bool server_enabled() {
 // on the handle's device
 static void server_stop(srbd_qp_handle h) {
   if (h->srv_live) {
-    reinterpret_cast<volatile srbd::LatMailbox*>(h->srv_mb)->quit = 1;
+    reinterpret_cast<volatile srbd::LatMailbox*>(h->srv_mb)->flags = srbd::kLatQuit;
     hipStreamSynchronize(h->srv_stream);
-    reinterpret_cast<volatile srbd::LatMailbox*>(h->srv_mb)->quit = 0;
+    reinterpret_cast<volatile srbd::LatMailbox*>(h->srv_mb)->flags = 0;
     h->srv_live = false;
   }
   // always off the exit hook's list: a handle whose relaunch failed (srv_live false) may
@@ -1120,9 +1120,11 @@ static int solve_host_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* 
         volatile srbd::LatMailbox* mb = h->srv_mb;
         if (e == hipSuccess) {
           if (const int us = server_post_delay_us()) std::this_thread::sleep_for(std::chrono::microseconds(us));
-          mb->arm = arm ? 1 : 0;
           std::atomic_thread_fence(std::memory_order_release);  // the staged QP before the post
-          mb->seq = ++h->srv_seq;
+          // seq and the request's flags in one 8-byte store (the server reads them as one word)
+          const unsigned long long post =
+              ((unsigned long long)(unsigned)(arm ? srbd::kLatArm : 0) << 32) | (unsigned)++h->srv_seq;
+          *reinterpret_cast<volatile unsigned long long*>(mb) = post;
         }
       }
     }
