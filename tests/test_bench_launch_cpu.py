@@ -42,3 +42,20 @@ def test_single_gpu_needs_no_launcher():
                        env=_env(), capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert json.loads(r.stdout.strip())["world"] == 1
+
+
+def test_roofline_ceiling_derivation():
+    """bench.py's roofline.ceiling: the two-sweep Riccati's minimum traffic per QP
+    is the algorithmic bytes + the stage records written and read back (246 doubles) + the A, B,
+    b the forward sweep reads again; at the achievable 6.3 TB/s that caps the algorithmic
+    fraction of the 8 TB/s peak at 0.396 for N = 20, nx = nu = 12."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    c = bench.unconstr_ceiling(128256, 65536)
+    assert c["record_round_trip_per_qp"] == 20 * 246 * 8 * 2
+    assert c["forward_reread_per_qp"] == 20 * (144 + 144 + 12) * 8
+    assert c["min_traffic_per_qp"] == 128256 + 78720 + 48000
+    assert abs(c["ceiling"] - 128256 / 254976 * 6300 / 8000) < 1e-12
+    assert 0.39 < c["ceiling"] < 0.40
