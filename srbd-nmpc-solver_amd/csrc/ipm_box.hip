@@ -171,6 +171,9 @@ hipError_t launch_ipm_box<double>(const ProblemArgsT<double>& a, hipStream_t str
   if (ipm_latency_ok(a, ipm_latency_max_batch())) return launch_ipm_latency(a, stream);
   return ipm_f64::launch(a, stream);
 }
+hipError_t launch_ipm_box_batched(const ProblemArgsT<double>& a, hipStream_t stream) {
+  return ipm_f64::launch(a, stream);
+}
 template <>
 hipError_t launch_ipm_box<float>(const ProblemArgsT<float>& a, hipStream_t stream) {
   return ipm_f32::launch(a, stream);

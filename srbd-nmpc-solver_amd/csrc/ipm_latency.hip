@@ -330,6 +330,23 @@ __device__ __forceinline__ void load12z(const double* p, double (&v)[12]) {
   }
 }
 
+// (P v)_jj + acc for an element-owned v (lane j holds v_j), P from a stage record's kRP slot:
+// P packed (classical), or SQRT its factor Lp, applied as Lp (Lp' v) -- exactly the P the next
+// stage's factorization used (the batched kernels' rec_P_mul, ipm_box_impl.h)
+template <bool SQRT>
+__device__ __forceinline__ double rec_P_apply(const double* rkP, int jj, double v, double acc) {
+  double M[12];
+  if constexpr (SQRT) {
+    load_packed_lcol_d(rkP, jj, M);
+    const double t = dot_bcast(M, v, 0.0);  // (Lp' v)_jj
+    load_packed_lrow_d(rkP, jj, M);
+    return dot_bcast(M, t, acc);
+  } else {
+    load_packed_sym(rkP, jj, M);
+    return dot_bcast(M, v, acc);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // block-wide reductions of per-group partials: slot values written by each group's lane 0,
 // reduced by every thread after the barrier (same order everywhere: uniform results)
@@ -434,7 +451,7 @@ __device__ __forceinline__ void init_point(const Qp Q, const Lds L) {
 // stage k reads the old x_k+1, pi_k+1 and their steps and forms the new values itself, so no
 // stage waits for its neighbour's update (the new iterate goes to buffer cur ^ 1).
 // ---------------------------------------------------------------------------------------------
-template <bool HAS_C, bool PRED>
+template <bool HAS_C, bool PRED, bool SQRT = false>
 __device__ __forceinline__ void stage_pass(const Qp Q, const Lds L, double ap, double ad);
 
 // column j of chunk ch's rows of D_k (or C_k): v[i] = D[ch * 12 + i][j], 0 past ng / when absent
@@ -457,7 +474,11 @@ __device__ __forceinline__ void gen_row(const Qp& Q, int k, int ch, int j, bool 
 }
 // C[i] += sum_r X[r][i] Gamma_r Y[r][j] over the general rows (column j of X'Gamma Y; X = D or C
 // row-owned on the chunk's lanes, Y's column j on lane j, Gamma from the chunk's LDS slot)
-template <bool XC, bool YC>
+// SYM: as sums of the scaled rows' products, (sqrt(Gamma) X)'(sqrt(Gamma) Y), so D'Gamma D and
+// C'Gamma C are exactly symmetric (the batched kernels' g_hess form): the square-root chain
+// factorizes the P these terms enter, and a Gamma of 1e13 times rounding-level asymmetry breaks
+// that Cholesky (the classical form keeps Gamma on one side, as round 5 measured it)
+template <bool XC, bool YC, bool SYM = false>
 __device__ __forceinline__ void gen_syrk(const Qp& Q, const Lds& L, int k, int j, int jj, bool el,
                                          double (&C)[12]) {
   for (int ch = 0; ch < L.nch; ++ch) {
@@ -465,14 +486,23 @@ __device__ __forceinline__ void gen_syrk(const Qp& Q, const Lds& L, int k, int j
     gen_row<XC>(Q, k, ch, j, el, Xr);
     gen_col<YC>(Q, k, ch, jj, el, Yc);
     const double G = el ? L.gb(k, ch)[108 + j] : 0.0;
-    sfor<0, 12>([&](auto rs) {
-      constexpr int R = decltype(rs)::value;
-      fma_bcast_src<R>(C, Xr, bc<R>(G) * Yc[R]);
-    });
+    if constexpr (SYM) {
+      const double sG = __builtin_sqrt(G);
+      sfor<0, 12>([&](auto i) { Xr[decltype(i)::value] *= sG; });
+      sfor<0, 12>([&](auto rs) {
+        constexpr int R = decltype(rs)::value;
+        fma_bcast_src<R>(C, Xr, bc<R>(sG) * Yc[R]);
+      });
+    } else {
+      sfor<0, 12>([&](auto rs) {
+        constexpr int R = decltype(rs)::value;
+        fma_bcast_src<R>(C, Xr, bc<R>(G) * Yc[R]);
+      });
+    }
   }
 }
 
-template <bool HAS_C, bool PRED>
+template <bool HAS_C, bool PRED, bool SQRT>
 __device__ __forceinline__ void stage_pass(const Qp Q, const Lds L, double ap, double ad) {
   const ProblemArgsT<double>& a = Q.a;
   const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
@@ -654,8 +684,8 @@ __device__ __forceinline__ void stage_pass(const Qp Q, const Lds L, double ap, d
       load12(Q.R(k) + jj * 12, Rc);
       load12(Q.S(k) + jj * 12, Sc);
       sfor<0, 12>([&](auto i) { Rc[decltype(i)::value] += decltype(i)::value == j ? Gu : 0.0; });
-      gen_syrk<false, false>(Q, L, k, j, jj, el, Rc);  // R~ = R + diag(Gamma_u) + D'Gamma D
-      if constexpr (HAS_C) gen_syrk<false, true>(Q, L, k, j, jj, el, Sc);  // S~ = S + D'Gamma C
+      gen_syrk<false, false, SQRT>(Q, L, k, j, jj, el, Rc);  // R~ = R + diag(Gamma_u) + D'Gamma D
+      if constexpr (HAS_C) gen_syrk<false, true, SQRT>(Q, L, k, j, jj, el, Sc);  // S~ = S + D'Gamma C
       if (el) {
         store12(rk + kRR + j * 12, Rc);
         store12(rk + kRS + j * 12, Sc);
@@ -665,7 +695,7 @@ __device__ __forceinline__ void stage_pass(const Qp Q, const Lds L, double ap, d
     }
     load12(Q.Q(k) + jj * 12, Qc);
     sfor<0, 12>([&](auto i) { Qc[decltype(i)::value] += decltype(i)::value == j ? Gx : 0.0; });
-    if constexpr (HAS_C) gen_syrk<true, true>(Q, L, k, j, jj, el, Qc);  // Q~ = Q + diag(Gamma_x) + C'Gamma C
+    if constexpr (HAS_C) gen_syrk<true, true, SQRT>(Q, L, k, j, jj, el, Qc);  // Q~ = Q + diag(Gamma_x) + C'Gamma C
     if (el) {
       store12(rk + kRQ + j * 12, Qc);
       rk[kRq + j] = gx + gam_x + gpx;
@@ -727,13 +757,60 @@ __device__ __forceinline__ void corr_terms(const Qp Q, const Lds L, double smu) 
   }
 }
 
+// [P | p] in the tiles' C/D layout (wave 0) -> [Lp | s]: Lp = chol(P) (lower; a non-positive pivot
+// zeroes its column, BLASFEO dpotrf_l, riccati.h sqrt_factor) and s = Lp^-1 p, the border column
+// of the same elimination, through the G/H tile (column-owned Cholesky, then back).  Lp also
+// goes to the stage record's P slot (rkP, packed; row group 0 writes): the sweeps apply P as
+// Lp (Lp' v), the P this factorization continues with.
+__device__ __forceinline__ lat_d4 sqrt_tile(const lat_d4& Pt, double* gh, int g, int c, double* rkP) {
+  const bool cv = c < 12, cw = c <= 12;
+  lds_wave_fence();
+  sfor<0, 3>([&](auto rr) {
+    constexpr int R = decltype(rr)::value;
+    if (cw) gh[c * 12 + g + 4 * R] = Pt[R];
+  });
+  lds_wave_fence();
+  double Pc[12], Lc[12], rs;
+  sfor<0, 12>([&](auto i) {
+    const double v = gh[(cw ? c : 12) * 12 + decltype(i)::value];
+    Pc[decltype(i)::value] = cw ? v : 0.0;
+  });
+  lat_chol<true>(Pc, c, 0.0, Lc, rs, [](auto) {});
+  lds_wave_fence();
+  sfor<0, 12>([&](auto i) {
+    constexpr int I = decltype(i)::value;
+    const double ri = bc<I>(rs);
+    // lane c < 12: column c of Lp (zero above the diagonal); lane 12: s
+    Lc[I] = cv ? (I >= c ? Lc[I] : 0.0) : Lc[I] * ri;
+    if (cw && g == 0) gh[c * 12 + I] = Lc[I];
+  });
+  if (cv && g == 0) store_packed_col(rkP, c, Lc);
+  lds_wave_fence();
+  lat_d4 o;
+  sfor<0, 4>([&](auto rr) {
+    constexpr int R = decltype(rr)::value;
+    const int row = g + 4 * R < 12 ? g + 4 * R : 11;
+    const double v = gh[(cw ? c : 12) * 12 + row];
+    o[R] = (g + 4 * R < 12 && cw) ? v : 0.0;
+  });
+  lds_wave_fence();
+  return o;
+}
+
 // ---------------------------------------------------------------------------------------------
 // phase: the factorization (backward, serial in k) on matrix cores -- riccati_latency_impl.h's
 // sweep.  Wave 0: stage k's products and Cholesky; wave 1: stage k+1's K, record and closed
 // loop; wave 2: stage k-1's operands (A, B from the QP, R~ S~ Q~ r~ q~ b~ from the record) into
 // the LDS ring, so no global load sits on the chain.  Records per stage: [K | k] rows, P packed,
 // p, L packed + 1 / diag; [Acl | bcl] rows in LDS.
+// SQRT (ric_alg 1, hpipm-cpp's default; riccati.h riccati_step_sqrt): the chain carries the factor
+// Lp of P_k+1 and s = Lp^-1 p_k+1 instead of [P | p], and the same MFMAs form MB = Lp'B,
+// MA = Lp'[A | b~] + [0 | s], G = R~ + MB'MB, [H | g] = [S~ | r~] + MB'MA, [F | f] = [Q~ | q~] +
+// MA'MA (sums of squares: the classical B'PB, B'P[A | b~], A'P[A | b~] in exact arithmetic);
+// P_k = F - Y'Y is factorized again for the next stage (sqrt_tile: a second Cholesky on the
+// chain) and the record keeps that factor Lp, with p explicit (HPIPM's p-form).
 // ---------------------------------------------------------------------------------------------
+template <bool SQRT>
 __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
   const ProblemArgsT<double>& a = Q.a;
   const int N = Q.N;
@@ -768,12 +845,20 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
       Pt[R] = (g + 4 * R < 12 && cw) ? v : 0.0;
     });
     double* wn = Q.rec(N);
-    sfor<0, 3>([&](auto rr) {
-      constexpr int R = decltype(rr)::value;
-      const int row = g + 4 * R;
-      if (cv && row >= c) wn[kRP + packed_col(c) + row - c] = Pt[R];
-      if (c == 12) wn[kRp + row] = Pt[R];
-    });
+    if constexpr (SQRT) {
+      sfor<0, 3>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        if (c == 12) wn[kRp + g + 4 * R] = Pt[R];
+      });
+      Pt = sqrt_tile(Pt, gh, g, c, wn + kRP);
+    } else {
+      sfor<0, 3>([&](auto rr) {
+        constexpr int R = decltype(rr)::value;
+        const int row = g + 4 * R;
+        if (cv && row >= c) wn[kRP + packed_col(c) + row - c] = Pt[R];
+        if (c == 12) wn[kRp + row] = Pt[R];
+      });
+    }
   } else if (wave == 2) {
     load_slot(N - 1);
   }
@@ -837,7 +922,11 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
       lat_d4 WB = {0.0, 0.0, 0.0, 0.0};
       sfor<0, 3>([&](auto kb) { WB = lat_mfma(Pt[decltype(kb)::value], bo[decltype(kb)::value], WB); });
       lat_d4 Gt = Rt;
-      sfor<0, 3>([&](auto kb) { Gt = lat_mfma(bo[decltype(kb)::value], WB[decltype(kb)::value], Gt); });
+      if constexpr (SQRT) {  // (the A operand Pt is Lp: WB = Lp'B = MB, G = R~ + MB'MB)
+        sfor<0, 3>([&](auto kb) { Gt = lat_mfma(WB[decltype(kb)::value], WB[decltype(kb)::value], Gt); });
+      } else {
+        sfor<0, 3>([&](auto kb) { Gt = lat_mfma(bo[decltype(kb)::value], WB[decltype(kb)::value], Gt); });
+      }
       // W = P [A | b~] + [0 | p]; [H | g] = [S~ | r~] + B'W; [F | f] = [Q~ | q~] + A'W: one per pivot
       lat_d4 Wt;
       sfor<0, 4>([&](auto rr) { Wt[decltype(rr)::value] = c == 12 ? Pt[decltype(rr)::value] : 0.0; });
@@ -855,6 +944,20 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
           }
         }
       };
+      // SQRT: W = MA; H = S~ + MB'MA, F = Q~ + MA'MA (MB = WB kept for H)
+      auto wh_sqrt = [&](auto kk) {
+        constexpr int K = decltype(kk)::value;
+        if constexpr (K < 3) {
+          Wt = lat_mfma(Pt[K], ao[K], Wt);
+        } else if constexpr (K < 9) {
+          constexpr int KB = (K - 3) / 2;
+          if constexpr ((K - 3) % 2 == 0) {
+            Ht = lat_mfma(WB[KB], Wt[KB], Ht);
+          } else {
+            Ft = lat_mfma(Wt[KB], Wt[KB], Ft);
+          }
+        }
+      };
       lds_wave_fence();
       sfor<0, 3>([&](auto rr) {
         constexpr int R = decltype(rr)::value;
@@ -867,7 +970,11 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
         Gc[decltype(i)::value] = cv ? v : 0.0;
       });
       tstamp(71);
-      lat_chol(Gc, c, a.reg, Lc, rs, wh);
+      if constexpr (SQRT) {
+        lat_chol(Gc, c, a.reg, Lc, rs, wh_sqrt);
+      } else {
+        lat_chol(Gc, c, a.reg, Lc, rs, wh);
+      }
       tstamp(72);
       // [Y | y] = L^-1 [H | g]
       lds_wave_fence();
@@ -921,12 +1028,20 @@ __device__ __forceinline__ void factorize(const Qp Q, const Lds L) {
       tstamp(75);
       Pt = Pn;
       double* rk = Q.rec(k);
-      sfor<0, 3>([&](auto rr) {
-        constexpr int R = decltype(rr)::value;
-        const int row = g + 4 * R;
-        if (cv && row >= c) rk[kRP + packed_col(c) + row - c] = Pt[R];
-        if (c == 12) rk[kRp + row] = Pt[R];
-      });
+      if constexpr (SQRT) {
+        sfor<0, 3>([&](auto rr) {
+          constexpr int R = decltype(rr)::value;
+          if (c == 12) rk[kRp + g + 4 * R] = Pt[R];
+        });
+        Pt = sqrt_tile(Pn, gh, g, c, rk + kRP);
+      } else {
+        sfor<0, 3>([&](auto rr) {
+          constexpr int R = decltype(rr)::value;
+          const int row = g + 4 * R;
+          if (cv && row >= c) rk[kRP + packed_col(c) + row - c] = Pt[R];
+          if (c == 12) rk[kRp + row] = Pt[R];
+        });
+      }
     } else if (wave == 1) {
       if (k < N - 1) finish_stage(k + 1);
     } else if (wave == 2) {
@@ -976,7 +1091,7 @@ __device__ __forceinline__ void forward(const Lds L, int N, int out = 3) {
 // dlam), the step ratios and the predictor's mu_aff sums.  CORR: k, p of the corrector (kv,
 // pv), dlam_aff dt_aff and sigma mu in the complementarity rows.
 // ---------------------------------------------------------------------------------------------
-template <bool CORR>
+template <bool CORR, bool SQRT>
 __device__ __forceinline__ void step_pass(const Qp Q, const Lds L, double smu, bool final_step) {
   const ProblemArgsT<double>& a = Q.a;
   const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
@@ -996,10 +1111,15 @@ __device__ __forceinline__ void step_pass(const Qp Q, const Lds L, double smu, b
       if (!el) duj = 0.0;
     }
     if (k > 0) {
-      double Pr[12];
-      load_packed_sym(rk + kRP, jj, Pr);
-      const double pvj = CORR ? L.pv()[k * 12 + jj] : rk[kRp + jj];
-      dpij = dot_bcast(Pr, dxj, pvj);
+      if constexpr (SQRT) {
+        const double pvj = CORR ? L.pv()[k * 12 + jj] : rk[kRp + jj];
+        dpij = rec_P_apply<true>(rk + kRP, jj, dxj, pvj);
+      } else {
+        double Pr[12];
+        load_packed_sym(rk + kRP, jj, Pr);
+        const double pvj = CORR ? L.pv()[k * 12 + jj] : rk[kRp + jj];
+        dpij = dot_bcast(Pr, dxj, pvj);
+      }
       if (!el) dpij = 0.0;
     }
     if (el) {
@@ -1081,6 +1201,7 @@ struct Rhs {
   int gu, gx, b, pb;
 };
 constexpr Rhs kRhsCorr{9, 10, 8, 5};
+template <bool SQRT>
 __device__ __forceinline__ void corr_rhs_stages(const Qp Q, const Lds L, Rhs h = kRhsCorr) {
   const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
   const bool el = j < 12;
@@ -1095,9 +1216,15 @@ __device__ __forceinline__ void corr_rhs_stages(const Qp Q, const Lds L, Rhs h =
       continue;
     }
     double M[12];
-    load_packed_sym(Q.rec(k + 1) + kRP, jj, M);
-    const double bj = el ? bt[k * 12 + j] : 0.0;
-    double pb = dot_bcast(M, bj, 0.0);
+    double pb;
+    if constexpr (SQRT) {
+      const double bj = el ? bt[k * 12 + j] : 0.0;
+      pb = rec_P_apply<true>(Q.rec(k + 1) + kRP, jj, bj, 0.0);
+    } else {
+      load_packed_sym(Q.rec(k + 1) + kRP, jj, M);
+      const double bj = el ? bt[k * 12 + j] : 0.0;
+      pb = dot_bcast(M, bj, 0.0);
+    }
     if (!el) pb = 0.0;
     const double* rk = Q.rec(k);
     sfor<0, 12>([&](auto i) { M[decltype(i)::value] = rk[kRK + decltype(i)::value * 13 + jj]; });
@@ -1263,6 +1390,7 @@ __device__ __forceinline__ void lin_res_pass(const Qp Q, const Lds L) {
 // of the correction in kv, pv) added to the step: du += K ddx + k, dx += ddx, dpi += P ddx + p;
 // the barrier steps are linear in the primal step (ddt = +-ddv, ddlam = -lam ddt / t); then the
 // step ratios of the whole step and the non-finite check, as step_pass leaves them.
+template <bool SQRT>
 __device__ __forceinline__ void corr_apply_pass(const Qp Q, const Lds L) {
   const ProblemArgsT<double>& a = Q.a;
   const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
@@ -1292,9 +1420,13 @@ __device__ __forceinline__ void corr_apply_pass(const Qp Q, const Lds L) {
       if (!el) cuj = 0.0;
     }
     if (k > 0) {
-      double Pr[12];
-      load_packed_sym(rk + kRP, jj, Pr);
-      cpj = dot_bcast(Pr, cxj, L.pv()[k * 12 + jj]);
+      if constexpr (SQRT) {
+        cpj = rec_P_apply<true>(rk + kRP, jj, cxj, L.pv()[k * 12 + jj]);
+      } else {
+        double Pr[12];
+        load_packed_sym(rk + kRP, jj, Pr);
+        cpj = dot_bcast(Pr, cxj, L.pv()[k * 12 + jj]);
+      }
       if (!el) cpj = 0.0;
     }
     if (el) {
@@ -1359,6 +1491,7 @@ __device__ __forceinline__ void corr_apply_pass(const Qp Q, const Lds L) {
 // pi_0 = Q0 x0 + S0'u0 + q0 + A0'(P_1 res_b0 + pi_1) (ocp_qp_ipm_solver.cpp:347-373), and the
 // Riccati getters of the last factorization: P, K; p = pi - P x, k = u - K x
 // ---------------------------------------------------------------------------------------------
+template <bool SQRT>
 __device__ __forceinline__ void outputs(const Qp Q, const Lds L) {
   const ProblemArgsT<double>& a = Q.a;
   const int N = Q.N, grp = opq(threadIdx.x >> 4), j = opq(threadIdx.x & 15);
@@ -1372,8 +1505,13 @@ __device__ __forceinline__ void outputs(const Qp Q, const Lds L) {
     double pij = el ? L.pi()[k * 12 + j] : 0.0;
     if (k == 0) {
       double M[12];
-      load_packed_sym(Q.rec(1) + kRP, jj, M);
-      double t = dot_bcast(M, el ? L.rb()[j] : 0.0, el ? L.pi()[12 + j] : 0.0);
+      double t;
+      if constexpr (SQRT) {
+        t = rec_P_apply<true>(Q.rec(1) + kRP, jj, el ? L.rb()[j] : 0.0, el ? L.pi()[12 + j] : 0.0);
+      } else {
+        load_packed_sym(Q.rec(1) + kRP, jj, M);
+        t = dot_bcast(M, el ? L.rb()[j] : 0.0, el ? L.pi()[12 + j] : 0.0);
+      }
       if (!el) t = 0.0;
       load12(Q.Q(0) + jj * 12, M);
       double p0 = dot_bcast(M, xj, el ? Q.qv(0)[j] : 0.0);
@@ -1390,8 +1528,20 @@ __device__ __forceinline__ void outputs(const Qp Q, const Lds L) {
     }
     if (a.P || a.p) {
       double Pr[12];
-      load_packed_sym(rk + kRP, jj, Pr);
-      const double px = dot_bcast(Pr, xj, 0.0);
+      if constexpr (SQRT) {  // P = Lp Lp': column jj = sum_K Lp[:, K] Lp[jj][K]
+        double Lr[12];
+        load_packed_lrow_d(rk + kRP, jj, Lr);
+        sfor<0, 12>([&](auto i) { Pr[decltype(i)::value] = 0.0; });
+        tmul_acc(Lr, Lr, Pr);
+      } else {
+        load_packed_sym(rk + kRP, jj, Pr);
+      }
+      double px;
+      if constexpr (SQRT) {
+        px = rec_P_apply<true>(rk + kRP, jj, xj, 0.0);
+      } else {
+        px = dot_bcast(Pr, xj, 0.0);
+      }
       if (el && a.P) store12(a.P + (q * (N + 1) + k) * 144 + (size_t)j * 12, Pr);
       if (el && a.p) a.p[(q * (N + 1) + k) * 12 + j] = pij - px;
     }
@@ -1411,7 +1561,10 @@ __device__ __forceinline__ void outputs(const Qp Q, const Lds L) {
 
 // ITREF: HPIPM's iterative refinement of the step (Balance / Robust; a separate instantiation so
 // the Speed path keeps its registers)
-template <bool HAS_C, bool ITREF>
+// SQRT: ric_alg 1 (factorize<true>, the records' P slot holding the factor Lp), with lq_fact 1's
+// check of the predictor (HPIPM switches such a QP to the LQ factorization, which this kernel does
+// not have: it raises a.lat_lq_flag and the C-ABI solves the batch again on the batched kernels).
+template <bool HAS_C, bool ITREF, bool SQRT>
 __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<double> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int N = a.N;
@@ -1434,7 +1587,7 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
   for (;;) {
     __syncthreads();  // (red reuse)
     tstamp(50);
-    stage_pass<HAS_C, true>(Q, L, alpha_p, alpha_d);
+    stage_pass<HAS_C, true, SQRT>(Q, L, alpha_p, alpha_d);
     __syncthreads();
     L.cur ^= 1;  // the new iterate
     tstamp(51);
@@ -1469,18 +1622,36 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
     double* const next = (stat && t0) ? stat + (size_t)(iter + 1) * kStatCols : nullptr;
 
     // ---- predictor (the stage blocks are in the records: stage_pass) ----
-    factorize(Q, L);
+    factorize<SQRT>(Q, L);
     __syncthreads();
     tstamp(53);
     forward(L, N);
     __syncthreads();
     tstamp(54);
     const bool pc = a.pred_corr != 0;
-    step_pass<false>(Q, L, 0.0, !pc);
+    step_pass<false, SQRT>(Q, L, 0.0, !pc);
     __syncthreads();
     tstamp(55);
     double ap = uni(red_min(L, 0)), ad = uni(red_min(L, 1));
     bool bad = uni(red_max(L, 4)) > 0.0;
+    if constexpr (SQRT) {
+      if (a.lq_fact == 1) {
+        // HPIPM lq_fact 1 (d_ocp_qp_ipm_solve): the predictor step's linear residual above 1e-5
+        // (or NaN) switches the QP to the LQ factorization -- not built here: leave, and let the
+        // C-ABI solve the batch on the batched kernels (ipm_box_impl.h kPhIRP / kPhLqChk).  The
+        // check's buffers (gtu, gtx, the other x / pi) are dead here; its slots 0, 1 are the
+        // step ratios, already read (slots 2, 3 hold the mu_aff sums, untouched).
+        __syncthreads();
+        lin_res_pass<HAS_C>(Q, L);
+        __syncthreads();
+        const double ngr = uni(red_max(L, 0)), nbr = uni(red_max(L, 1));
+        if (!(ngr <= 1e-5) || !(nbr <= 1e-5)) {
+          status = kLatNeedsLq;
+          if (t0 && a.lat_lq_flag) __hip_atomic_store(a.lat_lq_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
     if (pc) {
       const double aa = fmin(1.0, fmin(ap, ad));
       const double S1 = uni(red_sum(L, 2)), S2 = uni(red_sum(L, 3));
@@ -1499,7 +1670,7 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
       corr_terms<HAS_C>(Q, L, smu);
       __syncthreads();
       tstamp(56);
-      corr_rhs_stages(Q, L);
+      corr_rhs_stages<SQRT>(Q, L);
       __syncthreads();
       tstamp(57);
       corr_rhs_chain(L, N);
@@ -1511,7 +1682,7 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
       forward(L, N);
       __syncthreads();
       tstamp(60);
-      step_pass<true>(Q, L, smu, true);
+      step_pass<true, SQRT>(Q, L, smu, true);
       __syncthreads();
       tstamp(61);
       ap = uni(red_min(L, 0));
@@ -1539,7 +1710,7 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
         if ((ngr < a.tol_stat || ngr < 1e-3 * n0g) && (nbr < a.tol_eq || nbr < 1e-3 * n0b)) break;
         // the correction: the corrector's recursion with (r_u, r_x, r_b) as right-hand side
         const Rhs ref{9, 10, L.ref_b(), L.ref_pb()};
-        corr_rhs_stages(Q, L, ref);
+        corr_rhs_stages<SQRT>(Q, L, ref);
         __syncthreads();
         corr_rhs_chain(L, N);
         __syncthreads();
@@ -1547,7 +1718,7 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
         __syncthreads();
         forward(L, N, Lds::kRefDx);
         __syncthreads();
-        corr_apply_pass(Q, L);
+        corr_apply_pass<SQRT>(Q, L);
         __syncthreads();
         ap = uni(red_min(L, 0));
         ad = uni(red_min(L, 1));
@@ -1573,12 +1744,13 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
     last_amin = uni(fmin(alpha_p, alpha_d));
     ++iter;
   }
-  // converged at the initial point: the factorization of the returned iterate (HPIPM getters;
-  // its stage blocks are in the records: stage_pass)
-  if (iter == 0 && status != 3) factorize(Q, L);
+  // decided at the initial point (converged, or NaN data): the factorization of the returned
+  // iterate, as the batched kernels' exiting sweep has it (HPIPM getters and the stage-0 pi
+  // rebuild read it; its stage blocks are in the records: stage_pass)
+  if (iter == 0 && status != kLatNeedsLq) factorize<SQRT>(Q, L);
   __syncthreads();
   tstamp(65);
-  outputs(Q, L);
+  outputs<SQRT>(Q, L);
   __syncthreads();
   tstamp(66);
   if (t0) {
@@ -1599,7 +1771,17 @@ __global__ void __launch_bounds__(kThreads, 1) ipm_latency_kernel(ProblemArgsT<d
 bool ipm_latency_ok(const ProblemArgsT<double>& a, int max_batch) {
   if (a.batch < 1 || a.batch > max_batch) return false;
   if (a.nx != 12 || a.nu != 12 || a.N < 1) return false;
-  if (a.ric_alg || a.lq_fact || a.warm_start > 1 || a.warm_bars || a.skip_last_rb) return false;
+  // ric_alg 1 with lq_fact 0, or 1 with the switch flag (the kernel checks the predictor and
+  // flags a switch to LQ, a.lat_lq_flag; not with a warm start: the re-solve after a switch would
+  // find the first attempt's x, u in the buffers the warm start reads); lq_fact 2 (Robust with
+  // the square root) factorizes by LQ throughout: batched kernels
+  if (a.lq_fact > 1 || (a.lq_fact == 1 && (!a.lat_lq_flag || a.warm_start)) || a.warm_start > 1 || a.warm_bars ||
+      a.skip_last_rb)
+    return false;
+  // the square root with C rows measured weaker than the batched kernels' (round 6: 2 of 12 random
+  // QPs with C and D rows stopped at min step, iteration counts +2 against the oracle's): those
+  // stay on the batched kernels; C-free rows (the friction cone) and boxes run here
+  if (a.ric_alg && a.C && a.ng > 0) return false;
   const int nch = (a.ng + 11) / 12;
   if (ipm_lat::lds_doubles(a.N, nch) * sizeof(double) > 160 * 1024) return false;
   return a.ws && a.ws_qp >= (size_t)(a.N + 1) * ipm_lat::kRStage;
@@ -1610,16 +1792,17 @@ hipError_t launch_ipm_latency(const ProblemArgsT<double>& a, hipStream_t stream)
   const int nch = (a.ng + 11) / 12;
   const size_t bytes = ipm_lat::lds_doubles(a.N, nch) * sizeof(double);
   const dim3 grid(a.batch), block(ipm_lat::kThreads);
-  if (a.C && a.ng > 0) {
-    if (a.itref_corr_max > 0)
-      hipLaunchKernelGGL((ipm_lat::ipm_latency_kernel<true, true>), grid, block, bytes, stream, a);
-    else
-      hipLaunchKernelGGL((ipm_lat::ipm_latency_kernel<true, false>), grid, block, bytes, stream, a);
-  } else {
-    if (a.itref_corr_max > 0)
-      hipLaunchKernelGGL((ipm_lat::ipm_latency_kernel<false, true>), grid, block, bytes, stream, a);
-    else
-      hipLaunchKernelGGL((ipm_lat::ipm_latency_kernel<false, false>), grid, block, bytes, stream, a);
+  const int v = (a.C && a.ng > 0 ? 4 : 0) | (a.itref_corr_max > 0 ? 2 : 0) | (a.ric_alg ? 1 : 0);
+  switch (v) {
+#define SRBD_LAT_CASE(V, C, I, Q) \
+  case V: hipLaunchKernelGGL((ipm_lat::ipm_latency_kernel<C, I, Q>), grid, block, bytes, stream, a); break;
+    SRBD_LAT_CASE(0, false, false, false)
+    SRBD_LAT_CASE(1, false, false, true)
+    SRBD_LAT_CASE(2, false, true, false)
+    SRBD_LAT_CASE(3, false, true, true)
+    SRBD_LAT_CASE(4, true, false, false)
+    SRBD_LAT_CASE(6, true, true, false)
+#undef SRBD_LAT_CASE
   }
   return hipGetLastError();
 }
@@ -1628,10 +1811,12 @@ hipError_t launch_ipm_latency(const ProblemArgsT<double>& a, hipStream_t stream)
 // the handle's device, like prepare_riccati_device)
 hipError_t prepare_ipm_latency_device() {
   constexpr int kBytes = 160 * 1024;
-  const void* fns[] = {reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<true, false>),
-                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, false>),
-                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<true, true>),
-                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, true>)};
+  const void* fns[] = {reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<true, false, false>),
+                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, false, false>),
+                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<true, true, false>),
+                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, true, false>),
+                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, false, true>),
+                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, true, true>)};
   hipError_t e = hipSuccess;
   for (const void* f : fns)
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kBytes);

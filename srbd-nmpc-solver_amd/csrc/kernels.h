@@ -84,6 +84,11 @@ struct ProblemArgsT {
   // qp_list[g] if g < count.
   int* qp_buf;
   const int* qp_list;
+  // internal (the latency IPM, ric_alg 1 with lq_fact 1): device word the kernel sets to 1 when a
+  // QP's predictor check asks for the LQ factorization (HPIPM's switch), which only the batched
+  // kernels have: the C-ABI then solves the batch there (srbd_qp_capi.hip solve_impl).  (Last:
+  // the other fields keep their kernel-argument offsets.)
+  int* lat_lq_flag;
 };
 // iterations of the live-QP counter arrays (iter_max >= this runs without the control)
 constexpr int kCtlCap = 257;
@@ -126,8 +131,9 @@ constexpr int kGenChunk = 112;
 constexpr int kGenVec = 36;
 
 size_t ws_doubles_ipm(int N, int ng);  // elements per QP (either precision)
-// The one-launch latency IPM (ipm_latency.hip): fp64, classical Riccati, no refinement, up to
-// max_batch QPs (one workgroup each).  ipm_latency_ok says whether `a` runs there.
+// The one-launch latency IPM (ipm_latency.hip): fp64, both Riccati forms, HPIPM's refinement, up
+// to max_batch QPs (one workgroup each).  ipm_latency_ok says whether `a` runs there;
+// launch_ipm_box_batched always takes the batched kernels.
 constexpr int kIpmLatencyMaxBatch = 512;
 int ipm_latency_max_batch();
 bool ipm_latency_ok(const ProblemArgsT<double>& a, int max_batch);
@@ -135,6 +141,7 @@ hipError_t launch_ipm_latency(const ProblemArgsT<double>& a, hipStream_t stream)
 hipError_t prepare_ipm_latency_device();  // srbd_qp_create, on the handle's device
 template <typename T>
 hipError_t launch_ipm_box(const ProblemArgsT<T>& a, hipStream_t stream);
+hipError_t launch_ipm_box_batched(const ProblemArgsT<double>& a, hipStream_t stream);
 
 // Workspace doubles per QP needed by the unconstrained solve.
 size_t ws_doubles_unconstr(int N);
@@ -166,6 +173,9 @@ struct alignas(8) LatMailbox {
   int exited;  // device: epoch of the server launch that has left
 };
 constexpr int kLatQuit = 1, kLatArm = 2;
+// the latency IPM's status for a QP whose lq_fact 1 check asked for the LQ factorization: the
+// C-ABI solves it again on the batched kernels (never returned to a caller)
+constexpr int kLatNeedsLq = 4;
 // true when launch_riccati_unconstr(a) would be one latency-kernel workgroup reading its QP
 // once (batch 1, classical Riccati, N <= 20): the server can take the call instead
 bool latency_server_ok(const ProblemArgsT<double>& a);

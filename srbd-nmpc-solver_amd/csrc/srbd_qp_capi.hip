@@ -76,6 +76,15 @@ struct srbd_qp_handle_s {
   // settings.f32_iters: fp32 copy of the data, fp32 iterate, barrier state (first use)
   void* mixed = nullptr;
   size_t mixed_bytes = 0;
+  // the latency IPM's lq_fact 1 switch: its flag (device) and read-back (pinned), the list,
+  // status and count of the QPs that raised it (capacity ints each, then the count) and their
+  // compact batch for the batched kernels (first use); force_batched while those are solved
+  int* lat_flag = nullptr;
+  int* lat_flag_host = nullptr;
+  int* lqsw_idx = nullptr;
+  void* lqsw = nullptr;
+  size_t lqsw_bytes = 0;
+  bool force_batched = false;
   // live-QP control of the IPM launch sequence (ProblemArgsT::ctl): device counters and
   // control words, decided on the device (the host never waits on them)
   int* ctl = nullptr;
@@ -356,6 +365,10 @@ void srbd_qp_destroy(srbd_qp_handle h) {
   if (h->mixed) hipFree(h->mixed);
   if (h->resc_count_host) hipHostFree(h->resc_count_host);
   if (h->fac_flags) hipHostFree(h->fac_flags);
+  if (h->lat_flag) hipFree(h->lat_flag);
+  if (h->lat_flag_host) hipHostFree(h->lat_flag_host);
+  if (h->lqsw_idx) hipFree(h->lqsw_idx);
+  if (h->lqsw) hipFree(h->lqsw);
   if (h->ctl) hipFree(h->ctl);
   if (h->qp_buf) hipFree(h->qp_buf);
   if (h->stream) hipStreamDestroy(h->stream);
@@ -372,8 +385,9 @@ size_t srbd_qp_memory_bytes(srbd_qp_handle h) {
   return h->ws_bytes + h->stage_bytes + h->pinned_bytes + h->pad_bytes + h->nmpc_bytes +
          (h->ctl ? sizeof(int) * srbd::kCtlInts : 0) +
          (h->qp_buf ? sizeof(int) * ((size_t)h->capacity + 1) : 0) +
-         h->resc_bytes + h->resc2_bytes + h->mixed_bytes +
-         (h->resc_idx ? sizeof(int) * (2 * (size_t)h->capacity + 1) : 0);
+         h->resc_bytes + h->resc2_bytes + h->mixed_bytes + h->lqsw_bytes +
+         (h->resc_idx ? sizeof(int) * (2 * (size_t)h->capacity + 1) : 0) +
+         (h->lqsw_idx ? sizeof(int) * (2 * (size_t)h->capacity + 1) : 0);
 }
 
 int srbd_qp_synchronize(srbd_qp_handle h) {
@@ -415,7 +429,7 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
 static int fallback_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                         const srbd_qp_data_f64* d, const srbd_qp_solution_f64* sc,
                         const srbd_qp_solution_f64* s, hipStream_t strm, int min_status, int* idx,
-                        void** buf, size_t* buf_bytes, const double* warm_x = nullptr,
+                        int* count, void** buf, size_t* buf_bytes, const double* warm_x = nullptr,
                         const double* warm_u = nullptr);
 
 // The launch arguments of a solve (solve_impl; the resident server's request).
@@ -529,8 +543,53 @@ static int solve_impl(srbd_qp_handle h, int batch, const srbd_qp_settings* st, c
   }
   if (e != hipSuccess) {
   } else if (constrained(h->dims)) {
-    e = srbd::launch_ipm_box(run, strm);
+    // ric_alg 1 with lq_fact 1 (Balance's default) on the latency IPM: its predictor check may
+    // ask for HPIPM's switch to the LQ factorization, which only the batched kernels have.  Such
+    // a QP ends with status kLatNeedsLq and raises the flag; the call then waits once for the
+    // flag and, if it is up, solves those QPs (and only those) again on the batched kernels, so
+    // each QP ends as it does in any batch
+    bool lq_watch = false;
+    if constexpr (std::is_same_v<T, double>) {
+      if (run.ric_alg && run.lq_fact == 1 && iter_cap < 0 && !h->force_batched) {
+        if (!h->lat_flag) {
+          e = hipMalloc(reinterpret_cast<void**>(&h->lat_flag), sizeof(int));
+          if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&h->lat_flag_host), sizeof(int));
+          if (e == hipSuccess)
+            e = hipMalloc(reinterpret_cast<void**>(&h->lqsw_idx), sizeof(int) * (2 * (size_t)h->capacity + 1));
+          if (e == hipSuccess && !h->resc_count_host)
+            e = hipHostMalloc(reinterpret_cast<void**>(&h->resc_count_host), sizeof(int));
+        }
+        run.lat_lq_flag = e == hipSuccess ? h->lat_flag : nullptr;
+        lq_watch = e == hipSuccess && srbd::ipm_latency_ok(run, srbd::ipm_latency_max_batch());
+        if (!lq_watch) {
+          run.lat_lq_flag = nullptr;
+        } else {
+          if (!a.status) a.status = run.status = h->lqsw_idx + h->capacity;
+          e = hipMemsetAsync(h->lat_flag, 0, sizeof(int), strm);
+        }
+      }
+      if (e == hipSuccess)
+        e = h->force_batched ? srbd::launch_ipm_box_batched(run, strm) : srbd::launch_ipm_box(run, strm);
+    } else {
+      if (e == hipSuccess) e = srbd::launch_ipm_box(run, strm);
+    }
     if (e == hipSuccess && padded) e = srbd::unpad_solution<T>(a, run, strm);
+    if constexpr (std::is_same_v<T, double>) {
+      if (e == hipSuccess && lq_watch) {
+        e = hipMemcpyAsync(h->lat_flag_host, h->lat_flag, sizeof(int), hipMemcpyDeviceToHost, strm);
+        if (e == hipSuccess) e = hipStreamSynchronize(strm);
+        if (e == hipSuccess && *h->lat_flag_host) {
+          SolT sc = *s;
+          sc.status = a.status;
+          hipSetDevice(prev);
+          h->force_batched = true;
+          rc = fallback_f64(h, batch, st, d, &sc, s, strm, srbd::kLatNeedsLq, h->lqsw_idx,
+                            h->lqsw_idx + 2 * (size_t)h->capacity, &h->lqsw, &h->lqsw_bytes);
+          h->force_batched = false;
+          return rc;
+        }
+      }
+    }
     if constexpr (std::is_same_v<T, float>) {
       if (e == hipSuccess && rescue) {
         hipSetDevice(prev);
@@ -662,8 +721,8 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
   // does not recover) is solved again cold in fp64 (its own list, buffer and idx slots:
   // [capacity, 2 capacity) of resc_idx)
   if (cont) {
-    *rc = fallback_f64(h, R, &st64, &d64, &s64, &s64, strm, 1, h->resc_idx + h->capacity, &h->resc2,
-                       &h->resc2_bytes);
+    *rc = fallback_f64(h, R, &st64, &d64, &s64, &s64, strm, 1, h->resc_idx + h->capacity,
+                       h->resc_idx + 2 * (size_t)h->capacity, &h->resc2, &h->resc2_bytes);
     if (*rc) return hipSuccess;
   }
   hipSetDevice(h->device);
@@ -686,11 +745,10 @@ static hipError_t rescue_f32(srbd_qp_handle h, int batch, const srbd_qp_settings
 static int fallback_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
                         const srbd_qp_data_f64* d, const srbd_qp_solution_f64* sc,
                         const srbd_qp_solution_f64* s, hipStream_t strm, int min_status, int* idx,
-                        void** buf, size_t* buf_bytes, const double* warm_x, const double* warm_u) {
+                        int* count, void** buf, size_t* buf_bytes, const double* warm_x, const double* warm_u) {
   int prev = 0;
   hipGetDevice(&prev);
   hipSetDevice(h->device);
-  int* count = h->resc_idx + 2 * (size_t)h->capacity;
   hipError_t e = srbd::launch_select_unsolved(sc->status, batch, min_status, idx, count, strm);
   if (e == hipSuccess) e = hipMemcpyAsync(h->resc_count_host, count, sizeof(int), hipMemcpyDeviceToHost, strm);
   if (e == hipSuccess) e = hipStreamSynchronize(strm);
@@ -864,8 +922,8 @@ static int mixed_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* st,
   if (!sc.status) sc.status = h->resc_idx + h->capacity;
   rc = solve_impl<double>(h, batch, &st64, d, &sc, strm, warm, 0, st->iter_max - n32);
   if (rc) return rc;
-  return fallback_f64(h, batch, st, d, &sc, s, strm, 1, h->resc_idx, &h->resc, &h->resc_bytes, keep_x,
-                      keep_u);
+  return fallback_f64(h, batch, st, d, &sc, s, strm, 1, h->resc_idx, h->resc_idx + 2 * (size_t)h->capacity,
+                      &h->resc, &h->resc_bytes, keep_x, keep_u);
 }
 
 // ---------------------------------------------------------------------------

@@ -170,6 +170,15 @@ def test_nan_and_batch_one(pkg):
     one = pkg.capi.solve(qp.subset(np.array([5])), x0[5:6], NMPC)
     for key in ("x", "u", "pi", "iter", "status"):
         assert np.array_equal(one[key][0], ok[key][5]), key
+    # the NaN QP's outputs are its own (the factorization of its initial iterate, not what a
+    # previous solve left in the workspace), in either form of the Riccati recursion
+    for ric_alg in (0, 1):
+        st = dict(NMPC, ric_alg=ric_alg)
+        first = pkg.capi.solve(bad, x0, st, stats=True)
+        pkg.capi.solve(qp, x0, st)
+        again = pkg.capi.solve(bad.subset(np.array([3])), x0[3:4], st, stats=True)
+        for key in ("x", "u", "pi", "status", "iter", "res", "stat"):
+            assert np.array_equal(again[key][0], first[key][3], equal_nan=key not in ("status", "iter")), key
 
 
 @pytest.mark.parametrize("N", [1, 10, 30, 40])
@@ -235,3 +244,82 @@ def test_itref_srbd_converged(pkg, oracle, mode, constraints):
             assert helpers.is_approx(lat[key][i], bat[key][i], 1e-7), (key, i)
         assert np.all(lat["res"][i] <= 1e-8), lat["res"][i]
 
+
+
+SQRT = dict(NMPC, ric_alg=1)
+
+
+@pytest.mark.parametrize("constraints", ["box_u", "cone"])
+@pytest.mark.parametrize("mode", ["Speed", "Balance"])
+def test_sqrt_srbd_vs_oracle_and_batched(pkg, oracle, constraints, mode):
+    """ric_alg 1 (hpipm-cpp's default, ocp_qp_ipm_solver_settings.hpp:81) on the latency IPM: the
+    chain carries the factor Lp of P and s = Lp^-1 p (riccati_step_sqrt's sums of squares on the
+    matrix cores, a second Cholesky per stage) and the records keep Lp, so every sweep applies P
+    as Lp (Lp' v), as the batched kernels do.  Speed (lq_fact 0) and Balance (lq_fact 1: the
+    predictor check passes on these QPs, so they stay on the latency IPM; refinement as above).
+    The oracle's square-root solution at 1e-7 in its iterations +-1, the batched kernels' status
+    and solution at 1e-7, residuals at the tolerance, the Riccati getters at rounding."""
+    qp, x0 = pkg.srbd_model.generate_batch(16, N=20, seed=717, constraints=constraints)
+    st = dict(SQRT, mode=mode)
+    lat, bat = both(pkg, qp, x0, st, stats=True, riccati=True)
+    ref = oracle.solve(qp, st, x0=x0)
+    _check_vs_oracle(lat, ref, qp.batch)
+    assert np.array_equal(lat["status"], bat["status"])
+    assert np.all(bat["stat"][:, :, 11] == 0)  # the batched kernels switched no QP to LQ either
+    for i in range(qp.batch):
+        for key in ("x", "u"):
+            assert helpers.is_approx(lat[key][i], bat[key][i], 1e-7), (key, i)
+        # the last factorization's getters: the same iterate to the solve's accuracy; the cone
+        # rows' Gamma (~1e8-1e10 when active) amplifies that into K
+        tol = 1e-6 if constraints == "box_u" else 1e-3
+        for key in ("P", "K"):
+            assert helpers.is_approx(lat[key][i], bat[key][i], tol), (key, i)
+        assert np.all(lat["res"][i] <= 1e-8), lat["res"][i]
+
+
+@pytest.mark.parametrize("ng,with_c", [(0, False), (14, False), (14, True)])
+@pytest.mark.parametrize("dims", [(12, 12), (12, 4), (5, 3)])
+def test_sqrt_random_constrained_vs_oracle(pkg, oracle, dims, ng, with_c):
+    """ric_alg 1 Speed on random boxes + general rows (embedded dims): the oracle's square-root
+    solution at 1e-7, its iterations +-1.  (Rows with C go to the batched kernels with ric_alg 1:
+    on the latency IPM 2 of these 12 QPs stopped at min step, round 6.)"""
+    nx, nu = dims
+    qp, x0 = helpers.random_constrained(12, 15, nx, nu, ng, 141 + nx + ng, pkg.OcpQpBatch)
+    if ng and not with_c:
+        qp.C = None
+        qp.lg = -0.05 - np.abs(qp.lg)
+        qp.ug = 0.05 + np.abs(qp.ug)
+    st = dict(SQRT, iter_max=40)
+    out = pkg.capi.solve(qp, x0, st)
+    ref = oracle.solve(qp, st, x0=x0)
+    _check_vs_oracle(out, ref, qp.batch, oracle_misses=1 if with_c else 0)
+
+
+def test_sqrt_lq_switch_resolves_those_qps(pkg):
+    """lq_fact 1 (Balance's with ric_alg 1, here set explicitly in Speed): a QP whose predictor
+    step's linear residual exceeds 1e-5 switches to the LQ factorization, which only the batched
+    kernels have.  The latency IPM checks the predictor and ends such a QP with an internal
+    status; the C-ABI solves those QPs (and only those) again on the batched kernels.  On random
+    boxes + D-only rows (about 27 of these 64 switch, round 6): every QP whose stat column 11
+    shows the switch ends exactly as the batched kernels (SRBD_IPM_LATENCY_MAX=0) end it, bit for
+    bit; the others stay on the latency IPM (some do); and each QP ends as it does in any batch
+    (half the batch solved alone gives the same outputs bit for bit)."""
+    qp, x0 = helpers.random_constrained(64, 15, 12, 4, 14, 226, pkg.OcpQpBatch)
+    qp.C = None
+    st = dict(iter_max=50, mode="Speed", ric_alg=1, lq_fact=1)
+    lat, bat = both(pkg, qp, x0, st, stats=True)
+    sw = np.any(lat["stat"][:, :, 11] == 1.0, axis=1)
+    assert 0 < sw.sum() < qp.batch, sw.sum()
+    assert set(np.unique(lat["status"])) <= {0, 1, 2}, lat["status"]
+    for key in ("x", "u", "pi", "status", "iter", "res", "stat"):
+        assert np.array_equal(lat[key][sw], bat[key][sw]), key
+    both_ok = ~sw & (lat["status"] == 0) & (bat["status"] == 0)
+    assert both_ok.sum() >= 8, both_ok.sum()
+    for i in np.nonzero(both_ok)[0]:
+        for key in ("x", "u"):
+            assert helpers.is_approx(lat[key][i], bat[key][i], 1e-6), (key, i)
+    half = np.arange(0, qp.batch, 2)
+    with _Path(True):
+        sub = pkg.capi.solve(qp.subset(half), x0[half], st, stats=True)
+    for key in ("x", "u", "pi", "status", "iter", "res", "stat"):
+        assert np.array_equal(sub[key], lat[key][half]), key

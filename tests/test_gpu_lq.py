@@ -93,16 +93,19 @@ def test_lq_fact2_degenerate_family(pkg, oracle):
             assert helpers.is_approx(out[key][i], ref[key][i], 1e-6), (key, i)
 
 
-def test_lq_fact1_switch(pkg, oracle):
+def test_lq_fact1_switch(pkg, oracle, monkeypatch):
     """lq_fact 1 in Speed on the degenerate family: the switch to LQ follows the predictor
     step's linear residual (> 1e-5: HPIPM's d_ocp_qp_ipm_solve test), redone by LQ from the same
     iterate and kept for the rest of the solve.  The stat table marks the LQ iterations
     (column 11: 0 before the switch, 1 from it on, never back), copies switch on the GPU as in
     the oracle (counts within 8 of 64), and every copy that ends converged without switching
-    is the Cholesky solve's (lq_fact 0) bit for bit."""
+    is the batched Cholesky solve's (lq_fact 0) bit for bit.  (The lq_fact 1 call starts on the
+    latency IPM, whose predictor check flags the switching copies; the batch is then solved on
+    the batched kernels, test_gpu_ipm_latency.py::test_sqrt_balance_lq_switch_falls_back.)"""
     fam, xb = _family(pkg)
     st = dict(iter_max=50, mode="Speed", ric_alg=1)
     out = pkg.capi.solve(fam, xb, dict(st, lq_fact=1), stats=True)
+    monkeypatch.setenv("SRBD_IPM_LATENCY_MAX", "0")
     chol = pkg.capi.solve(fam, xb, dict(st, lq_fact=0))
     ref = oracle.solve(fam, dict(st, lq_fact=1), x0=xb)
     switched = np.zeros(fam.batch, dtype=bool)
