@@ -9,8 +9,9 @@
 #   suite                       the whole GPU suite (pytest -m gpu)
 #   tests:EXPR                  pytest -m gpu -k EXPR, verbose
 #   file:PATH                   pytest PATH, verbose (a test file, GPU tests included)
-#   small:MODE:CONS             scripts/ipm_small_batch.py (batches 1..1024, N = 20) in HPIPM mode
-#                               MODE on SRBD QPs CONS (box_u / cone), latency IPM and batched
+#   small:MODE:CONS[:RIC]       scripts/ipm_small_batch.py (batches 1..1024, N = 20) in HPIPM mode
+#                               MODE on SRBD QPs CONS (box_u / cone), latency IPM and batched;
+#                               RIC: ric_alg (0 classical, the default; 1 square root)
 #   ab:VARIANT:WORKLOAD         scripts/dev/ab_variants.py: product vs build/variants/VARIANT
 #   modes:CONS                  scripts/ipm_modes.py: IPM cost by mode / lq_fact, 65536 QPs
 #   degen                       scripts/dev/degen_counts.py: degenerate-family counts per path
@@ -29,16 +30,16 @@ if [ "$1" = "-o" ]; then O=$2; shift 2; fi
 mkdir -p "$O"
 PYT="python -u -m pytest --timeout 300 --timeout-method thread"
 for step in "$@"; do
-  IFS=: read -r kind a b <<< "$step"
+  IFS=: read -r kind a b c <<< "$step"
   echo "== $step" >&2
   case $kind in
     suite) timeout -k 10 900 $PYT tests -m gpu -q > "$O/suite.log" 2>&1 ;;
     tests) timeout -k 10 600 $PYT tests -m gpu -v -k "$a" > "$O/tests_${a//[^A-Za-z0-9_]/_}.log" 2>&1 ;;
     file) timeout -k 10 600 $PYT "$a" -v > "$O/file_$(basename "$a" .py).log" 2>&1 ;;
     small)
-      timeout -k 10 300 python -u scripts/ipm_small_batch.py 20 "$b" "$a" > "$O/small_${a}_${b}_lat.json" &&
-        SRBD_IPM_LATENCY_MAX=0 timeout -k 10 300 python -u scripts/ipm_small_batch.py 20 "$b" "$a" \
-          > "$O/small_${a}_${b}_batched.json" ;;
+      timeout -k 10 300 python -u scripts/ipm_small_batch.py 20 "$b" "$a" ${c:-0} > "$O/small_${a}_${b}${c:+_ric$c}_lat.json" &&
+        SRBD_IPM_LATENCY_MAX=0 timeout -k 10 300 python -u scripts/ipm_small_batch.py 20 "$b" "$a" ${c:-0} \
+          > "$O/small_${a}_${b}${c:+_ric$c}_batched.json" ;;
     ab) timeout -k 10 900 python -u scripts/dev/ab_variants.py "product,$a" --workload "$b" --steps 5 --warmup 2 \
           --no-pipeline --no-host-path --no-secondary > "$O/ab_${a}_${b}.log" 2>&1 ;;
     modes) timeout -k 10 600 python scripts/ipm_modes.py 65536 3 "$a" > "$O/modes_$a.json" 2> "$O/modes_$a.log" ;;

@@ -4,8 +4,8 @@ settings (iter_max 30), batches 1 / 16 / 256 / 512 / 1024, one C-ABI call per so
 buffers; prints one JSON line {batch: {median_ms, min_ms, iters_max, iters_mean}}.
 SRBD_QP_LIB selects the library (A/B against an older build); SRBD_IPM_LATENCY_MAX=0 in the
 environment keeps every batch on the batched kernels (ipm_latency.hip is the default up to 512).
-Usage: ipm_small_batch.py [reps] [constraints] [mode]  (mode: HPIPM's Speed / Balance / Robust;
-the NMPC's Speed by default)"""
+Usage: ipm_small_batch.py [reps] [constraints] [mode] [ric_alg]  (mode: HPIPM's Speed / Balance /
+Robust; the NMPC's Speed and classical Riccati (ric_alg 0) by default)"""
 import importlib.util
 import json
 import sys
@@ -29,6 +29,8 @@ def main():
     settings = dict(bench.NMPC_SETTINGS)
     if len(sys.argv) > 3:
         settings["mode"] = sys.argv[3]
+    if len(sys.argv) > 4:
+        settings["ric_alg"] = int(sys.argv[4])
     out = {}
     for batch in (1, 16, 256, 512, 1024):
         qp, x0 = pkg.srbd_model.generate_batch(batch, N=20, seed=11, constraints=cons)
