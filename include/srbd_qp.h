@@ -252,10 +252,13 @@ int srbd_qp_create(const srbd_qp_dims* dims, int batch_capacity, int device,
  * Cost of the asynchronous stop: the batched IPM enqueues all iter_max
  * iterations up front; the iterations after the device has stopped the solve
  * cost their dispatch only (about 2 to 6 launches per iteration, a few
- * microseconds each, so ~0.1 ms for the NMPC's iter_max 30).  fp64 solves with
- * the classical Riccati (ric_alg 0; any mode: Balance / Robust refine in the same
- * launch) of up to 512 QPs run as one launch instead (the latency IPM, DESIGN.md
- * 4.12), which stops where it converges.
+ * microseconds each, so ~0.1 ms for the NMPC's iter_max 30).  fp64 solves of
+ * up to 512 QPs with the classical Riccati (ric_alg 0), or the square root
+ * without C rows (any mode: Balance / Robust refine in the same launch) run as
+ * one launch instead (the latency IPM), which stops where it
+ * converges.  With the square root and lq_fact 1 (Balance's) that call waits
+ * for its stream once: a QP asking for the LQ factorization is solved again,
+ * alone, on the batched kernels before the call returns.
  * SRBD_IPM_LATENCY_MAX (environment, QPs; 0 = off) moves that switch.     */
 int srbd_qp_solve_f64(srbd_qp_handle h, int batch, const srbd_qp_settings* settings,
                       const srbd_qp_data_f64* data, const srbd_qp_solution_f64* sol,
