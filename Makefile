@@ -51,10 +51,14 @@ $(LIB): $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
 oracle:
 	$(MAKE) -s -C oracle
 
-# A/B builds of the HIP library: make variant NAME=x VFLAGS="-DFOO=0"
-variant:
+# A/B builds of the HIP library: make variant NAME=x VFLAGS="-DFOO=0" [VSRCS="csrc/a.hip ..."]
+# (VSRCS: the sources compiled with VFLAGS; the others are the product's objects, build/obj)
+VSRCS ?= $(HIP_SRCS)
+variant: $(if $(filter-out $(HIP_SRCS),$(VSRCS)),,$(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(filter-out $(VSRCS),$(HIP_SRCS))))
 	@mkdir -p build/variants/$(NAME)
-	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $$f -o build/variants/$(NAME)/$$(basename $$f .hip).o || exit 1; done
+	for f in $(HIP_SRCS); do b=build/variants/$(NAME)/$$(basename $$f .hip).o; \
+	  case " $(VSRCS) " in *" $$f "*) $(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $$f -o $$b || exit 1 ;; \
+	  *) cp $(OBJDIR)/$$(basename $$f .hip).o $$b ;; esac; done
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/$(NAME)/libsrbd_qp.so build/variants/$(NAME)/*.o
 
 clean:

@@ -32,6 +32,14 @@
 #include "kernels.h"
 #include "mfma_lat.h"
 
+// dev builds only (make variant VFLAGS=-DSRBD_LAT_SQRT_C=1): the square root with C rows here too
+// (ipm_latency_ok): at -O3 that instantiation leaves the C-free one on C = 0 data, at -O1 / -O2
+// it does not
+#ifndef SRBD_LAT_SQRT_C
+#define SRBD_LAT_SQRT_C 0
+#endif
+
+
 namespace srbd {
 namespace ipm_lat {
 
@@ -1781,7 +1789,7 @@ bool ipm_latency_ok(const ProblemArgsT<double>& a, int max_batch) {
   // the square root with C rows measured weaker than the batched kernels' (round 6: 2 of 12 random
   // QPs with C and D rows stopped at min step, iteration counts +2 against the oracle's): those
   // stay on the batched kernels; C-free rows (the friction cone) and boxes run here
-  if (a.ric_alg && a.C && a.ng > 0) return false;
+  if (!SRBD_LAT_SQRT_C && a.ric_alg && a.C && a.ng > 0) return false;
   const int nch = (a.ng + 11) / 12;
   if (ipm_lat::lds_doubles(a.N, nch) * sizeof(double) > 160 * 1024) return false;
   return a.ws && a.ws_qp >= (size_t)(a.N + 1) * ipm_lat::kRStage;
@@ -1802,6 +1810,10 @@ hipError_t launch_ipm_latency(const ProblemArgsT<double>& a, hipStream_t stream)
     SRBD_LAT_CASE(3, false, true, true)
     SRBD_LAT_CASE(4, true, false, false)
     SRBD_LAT_CASE(6, true, true, false)
+#if SRBD_LAT_SQRT_C
+    SRBD_LAT_CASE(5, true, false, true)
+    SRBD_LAT_CASE(7, true, true, true)
+#endif
 #undef SRBD_LAT_CASE
   }
   return hipGetLastError();
@@ -1816,7 +1828,12 @@ hipError_t prepare_ipm_latency_device() {
                        reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<true, true, false>),
                        reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, true, false>),
                        reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, false, true>),
-                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, true, true>)};
+                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<false, true, true>),
+#if SRBD_LAT_SQRT_C
+                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<true, false, true>),
+                       reinterpret_cast<const void*>(&ipm_lat::ipm_latency_kernel<true, true, true>),
+#endif
+  };
   hipError_t e = hipSuccess;
   for (const void* f : fns)
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kBytes);
