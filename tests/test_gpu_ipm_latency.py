@@ -97,6 +97,24 @@ def test_random_constrained_vs_oracle(pkg, oracle, dims, ng, with_c):
         assert np.array_equal(out["x"][i, 0], x0[i])
 
 
+@pytest.mark.parametrize("mode", ["Speed", "Balance"])
+def test_zero_c_equals_no_c(pkg, mode):
+    """The C-row instantiation of the latency IPM on C = 0 equals the C-free one bit for bit
+    (it only adds zeros): a guard on the shipped instantiations' code generation -- the square
+    root's C instantiation, not shipped, fails exactly this at -O3."""
+    qp, x0 = helpers.random_constrained(12, 15, 12, 12, 14, 167, pkg.OcpQpBatch)
+    qz = qp.subset(np.arange(qp.batch))
+    qz.C = np.zeros_like(np.asarray(qz.C))
+    qn = qp.subset(np.arange(qp.batch))
+    qn.C = None
+    st = dict(iter_max=40, mode=mode, ric_alg=0)
+    with _Path(True):
+        rz = pkg.capi.solve(qz, x0, st, stats=True)
+        rn = pkg.capi.solve(qn, x0, st, stats=True)
+    for key in ("x", "u", "pi", "status", "iter", "res", "stat"):
+        assert np.array_equal(rz[key], rn[key]), key
+
+
 def test_outputs_match_batched(pkg):
     """The whole output set of the two paths on one problem family: res / obj to rounding,
     the Riccati getters P, p, K, k of the last factorization, and the statistics rows
