@@ -40,6 +40,7 @@
 #endif
 
 
+
 namespace srbd {
 namespace ipm_lat {
 
@@ -783,7 +784,9 @@ __device__ __forceinline__ lat_d4 sqrt_tile(const lat_d4& Pt, double* gh, int g,
     const double v = gh[(cw ? c : 12) * 12 + decltype(i)::value];
     Pc[decltype(i)::value] = cw ? v : 0.0;
   });
-  lat_chol<true>(Pc, c, 0.0, Lc, rs, [](auto) {});
+  // (pivots by lat_recip, as the G factor: IEEE division measured 2% slower at batch 1, box-u,
+  // with the same iteration counts -- profiles/round6/sqrt_recip/)
+  lat_chol(Pc, c, 0.0, Lc, rs, [](auto) {});
   lds_wave_fence();
   sfor<0, 12>([&](auto i) {
     constexpr int I = decltype(i)::value;
