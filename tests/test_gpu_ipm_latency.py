@@ -313,7 +313,8 @@ def test_sqrt_random_constrained_vs_oracle(pkg, oracle, dims, ng, with_c):
     _check_vs_oracle(out, ref, qp.batch, oracle_misses=1 if with_c else 0)
 
 
-def test_sqrt_lq_switch_resolves_those_qps(pkg):
+@pytest.mark.parametrize("dims", [(12, 4, 226), (5, 3, 219)])
+def test_sqrt_lq_switch_resolves_those_qps(pkg, dims):
     """lq_fact 1 (Balance's with ric_alg 1, here set explicitly in Speed): a QP whose predictor
     step's linear residual exceeds 1e-5 switches to the LQ factorization, which only the batched
     kernels have.  The latency IPM checks the predictor and ends such a QP with an internal
@@ -321,8 +322,10 @@ def test_sqrt_lq_switch_resolves_those_qps(pkg):
     boxes + D-only rows (about 27 of these 64 switch, round 6): every QP whose stat column 11
     shows the switch ends exactly as the batched kernels (SRBD_IPM_LATENCY_MAX=0) end it, bit for
     bit; the others stay on the latency IPM (some do); and each QP ends as it does in any batch
-    (half the batch solved alone gives the same outputs bit for bit)."""
-    qp, x0 = helpers.random_constrained(64, 15, 12, 4, 14, 226, pkg.OcpQpBatch)
+    (half the batch solved alone gives the same outputs bit for bit).  5 x 3: embedded in 12 x 12,
+    the re-solve pads its compact batch again."""
+    nx, nu, seed = dims
+    qp, x0 = helpers.random_constrained(64, 15, nx, nu, 14, seed, pkg.OcpQpBatch)
     qp.C = None
     st = dict(iter_max=50, mode="Speed", ric_alg=1, lq_fact=1)
     lat, bat = both(pkg, qp, x0, st, stats=True)
