@@ -585,12 +585,20 @@ def ipm_small_batch(pkg, capi, device, seed, N=20, reps=20, with_cpu=True):
     """Small-batch IPM latency: box-u (config 3's QP) at batch 1 / 16 / 256 and the friction
     cone (config 5's QP, fp64) at batch 1, the NMPC settings, device buffers, one C-ABI call per
     solve, wall time per call (median).  Up to 512 QPs these run on the one-launch latency IPM
-    (ipm_latency.hip); beside batch 1 box-u, the oracle's solve of the same QP on one host core."""
+    (ipm_latency.hip); beside batch 1 box-u, the oracle's solve of the same QP on one host core.
+    Batch 1 also with hpipm-cpp's default square-root Riccati (ric_alg 1, Speed and Balance: the
+    `_ric1` cases) and the reference test's Balance with the classical Riccati (`_balance`)."""
     import torch
-    st = capi.settings_struct(NMPC_SETTINGS)
+    ric1 = dict(NMPC_SETTINGS, ric_alg=1)
+    cases = [("", "box_u", (1, 16, 256), NMPC_SETTINGS), ("", "cone", (1,), NMPC_SETTINGS),
+             ("_balance", "box_u", (1,), dict(NMPC_SETTINGS, mode="Balance")),
+             ("_ric1", "box_u", (1,), ric1), ("_ric1", "cone", (1,), ric1),
+             ("_ric1_balance", "box_u", (1,), dict(ric1, mode="Balance"))]
     out = {"what": "wall ms per srbd_qp_solve_f64 call (launch + solve + sync), device buffers, "
-                   "NMPC settings; ipm_latency.hip up to 512 QPs", "N": N, "cases": {}}
-    for cons, batches in (("box_u", (1, 16, 256)), ("cone", (1,))):
+                   "NMPC settings unless the case says otherwise; ipm_latency.hip up to 512 QPs",
+           "N": N, "cases": {}}
+    for tag, cons, batches, settings in cases:
+        st = capi.settings_struct(settings)
         for b in batches:
             qp, x0 = pkg.srbd_model.generate_batch(b, N=N, seed=seed + 17, constraints=cons)
             h = capi.Handle(N, 12, 12, qp.ng, qp.has_box_u, qp.has_box_x, capacity=b,
@@ -604,10 +612,10 @@ def ipm_small_batch(pkg, capi, device, seed, N=20, reps=20, with_cpu=True):
                 h.synchronize()
                 ts.append(time.perf_counter() - t0)
             it = stt["iter"].cpu().numpy()
-            out["cases"][f"{cons}_batch{b}"] = {
+            out["cases"][f"{cons}_batch{b}{tag}"] = {
                 "median_ms": float(np.median(ts[2:])) * 1e3, "min_ms": float(np.min(ts[2:])) * 1e3,
                 "iters_mean": float(it.mean()), "success_rate": float((stt["status"].cpu().numpy() == 0).mean())}
-            if with_cpu and cons == "box_u" and b == 1:
+            if with_cpu and cons == "box_u" and b == 1 and not tag:
                 sys.path.insert(0, str(REPO / "oracle"))
                 import oracle  # test infrastructure: CPU baseline leg only
                 ts = []
